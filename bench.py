@@ -1,0 +1,266 @@
+#!/usr/bin/env python3
+# SPDX-License-Identifier: GPL-2.0
+"""Headline benchmark: device-resident parse + checksum + jhash + verdict on
+BASELINE.json config 2 (16 M synthetic 64 B IPv4/UDP frames in one packed
+UMEM pool, xdpsock geometry), one pool shard per GPU (config 5 at N > 1).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+A step = one launch of the RX kernel over the whole 16 M-frame shard that is
+resident in HBM.  Timing: W untimed steps, barrier + synchronize, K timed
+steps, synchronize + barrier, max over ranks.  value = frames processed by
+all ranks / that time (Mpps, whole job).  The roofline figure is the
+dominant kernel's algorithmic bytes (113 B/frame) over its
+average duration from HIP events on the launch stream.  The CPU baseline is
+the oracle (oracle/xdp_oracle.c, a restatement of the reference C) timed on
+this host, rank 0 at N = 1 only, on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "bpf-examples_amd"))
+
+import torch  # noqa: E402  (before libxdpgpu: one HIP runtime)
+import torch.distributed as dist  # noqa: E402
+
+import xdpgpu  # noqa: E402
+
+BYTES_PER_FRAME = 16 + 64 + 16 + 16 + 1   # desc + frame + result + tuple + verdict
+HBM_PEAK_GBS = 8000.0                      # MI355X HBM3E, MI355X_MICROARCH.md
+METRIC = ("Mpps + GB/s device-resident parse+csum+jhash, 64B & 1500B frames, "
+          "1/2/4/8 GPU")
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def to_dev(a: np.ndarray, dev, pad: int = 64) -> torch.Tensor:
+    t = torch.empty(a.nbytes + pad, dtype=torch.uint8, device=dev)
+    t[a.nbytes:].zero_()
+    t[: a.nbytes].copy_(torch.from_numpy(a.view(np.uint8).reshape(-1)))
+    return t
+
+
+def time_device(ctx, d_umem, usize, d_desc, n, d_v, d_res, d_tup, stream,
+                steps, warmup, world):
+    """W untimed + K timed launches; returns (wall seconds, avg kernel ms)."""
+    for _ in range(warmup):
+        ctx.process_dev(d_umem, usize, d_desc, n, d_v, d_res, d_tup, stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    t0 = time.perf_counter()
+    for s, e in ev:
+        s.record(stream)
+        ctx.process_dev(d_umem, usize, d_desc, n, d_v, d_res, d_tup, stream)
+        e.record(stream)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    kms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    return t1 - t0, kms
+
+
+def cpu_baseline(umem, descs, budget_s: float = 10.0):
+    """The oracle (restated reference C) on this host's cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    oracle.lib()
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    threads = max(1, min(16, cores))
+    sample = descs[: 1 << 21]
+    # calibrate on one pass, then size the run to ~budget_s of wall time
+    t1 = oracle.bench(umem, sample[: 1 << 18], 1, 1)
+    st_mpps = (1 << 18) / t1 / 1e6
+    dt = oracle.bench(umem, sample, threads, 1)
+    reps = max(1, int(budget_s / max(dt, 1e-3)))
+    dt = oracle.bench(umem, sample, threads, reps)
+    mpps = len(sample) * reps / dt / 1e6
+    return {"value": round(mpps, 2), "unit": "Mpps", "cores": threads,
+            "kind": "port",
+            "gbps": round(mpps * 1e6 * BYTES_PER_FRAME / 1e9, 2),
+            "single_thread_mpps": round(st_mpps, 2),
+            "sample": f"{len(sample)} config-2 frames x {reps} passes of oracle/xdp_oracle.c "
+                      f"(gcc -O2) on {threads} threads ({dt:.1f} s)"}
+
+
+def pmc_traffic():
+    """HBM bytes per launch of the RX kernel from the committed rocprofv3
+    PMC summary (profiles/*_pmc.json, see tools/pmc_traffic.py), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
+    if not files:
+        return None
+    try:
+        with open(files[-1]) as f:
+            d = json.load(f)
+        return d.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--frames", type=int, default=16 << 20, help="frames per GPU")
+    ap.add_argument("--size", type=int, default=64)
+    ap.add_argument("--window", type=int, default=64)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--e2e", action="store_true", help="also time the host path")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    # config 2 shard (config 5 at N > 1: same per-GPU content, seed offset)
+    t = time.time()
+    n = args.frames
+    umem, descs, expect = xdpgpu.pool_generate(n, xdpgpu.POOL_UDP4, args.size,
+                                               0x5EED0002 + rank)
+    log(f"[rank {rank}] pool {n} x {args.size} B generated in {time.time() - t:.1f} s")
+    d_umem = to_dev(umem, dev)
+    d_desc = to_dev(descs, dev, 0)
+    d_v = torch.empty(n, dtype=torch.uint8, device=dev)
+    d_res = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    d_tup = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    ctx = xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT, 0, xdpgpu.TUPLE_V4, args.window)
+    stream = torch.cuda.Stream(dev)
+
+    wall, kms = time_device(ctx, d_umem, umem.nbytes, d_desc, n, d_v, d_res, d_tup,
+                            stream, args.steps, args.warmup, world)
+    # correctness spot check of the timed outputs against the generator
+    v = d_v.cpu().numpy()
+    ok = bool(np.array_equal(v, expect))
+    wall_t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    frames_t = torch.tensor([float(n) * args.steps], dtype=torch.float64, device=dev)
+    ok_t = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(frames_t, op=dist.ReduceOp.SUM)
+        dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
+    wall_max = float(wall_t.item())
+    total_frames = float(frames_t.item())
+    mpps = total_frames / wall_max / 1e6
+    gbps = total_frames * BYTES_PER_FRAME / wall_max / 1e9
+    achieved = BYTES_PER_FRAME * n / (kms * 1e-3) / 1e9
+
+    secondary = None
+    if not args.no_secondary and rank == 0 and world == 1:
+        # 1500 B frames (BASELINE metric names both sizes): payload checksum
+        # by the cooperative wave path; 2 M frames (3 GB) per launch
+        del d_umem
+        torch.cuda.empty_cache()
+        n2 = 2 << 20
+        u2, ds2, ex2 = xdpgpu.pool_generate(n2, xdpgpu.POOL_UDP4, 1500, 0x5EED0012)
+        g_umem = to_dev(u2, dev)
+        g_desc = to_dev(ds2, dev, 0)
+        w2, k2 = time_device(ctx, g_umem, u2.nbytes, g_desc, n2, d_v, d_res, d_tup,
+                             stream, max(5, args.steps // 5), 2, 1)
+        ok2 = bool(np.array_equal(d_v[:n2].cpu().numpy(), ex2))
+        b2 = 16 + 1500 + 16 + 16 + 1
+        secondary = {"workload": "config2-geometry 2M x 1500B IPv4/UDP",
+                     "mpps": round(n2 * max(5, args.steps // 5) / w2 / 1e6, 1),
+                     "gbps": round(n2 * b2 / (k2 * 1e-3) / 1e9, 1),
+                     "kernel_ms": round(k2, 4),
+                     "roofline_frac": round(n2 * b2 / (k2 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "verdicts_ok": ok2}
+        del g_umem, g_desc
+
+    e2e = None
+    if args.e2e and rank == 0 and world == 1:
+        # host path: pinned UMEM, H2D span + descs, kernel, D2H outputs
+        n3 = min(n, 4 << 20)
+        h = xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT, 0, xdpgpu.TUPLE_V4, 64,
+                          max_batch=1 << 20)
+        h.register_umem(umem)
+        B = 1 << 20
+        v3 = np.zeros(n3, np.uint8)
+        r3 = np.zeros(n3, xdpgpu.RESULT_DTYPE)
+        t3 = np.zeros(n3, xdpgpu.TUPLE4_DTYPE)
+        sub = [np.ascontiguousarray(descs[lo:lo + B]) for lo in range(0, n3, B)]
+        for rep in range(2):
+            t0 = time.perf_counter()
+            for k, d in enumerate(sub):
+                slot = k & 1
+                if k >= 2:
+                    h.wait(slot)
+                lo = k * B
+                h.submit(slot, d, v3[lo:lo + len(d)], r3[lo:lo + len(d)],
+                         t3[lo:lo + len(d)])
+            h.wait(0)
+            h.wait(1)
+            te = time.perf_counter() - t0
+        e2e = {"mpps": round(n3 / te / 1e6, 1), "frames": n3, "batch": B,
+               "verdicts_ok": bool(np.array_equal(v3, expect[:n3]))}
+        h.close()
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(umem, descs)
+
+    if rank == 0:
+        traffic = pmc_traffic()
+        line = {
+            "metric": METRIC,
+            "value": round(mpps, 1),
+            "unit": "Mpps",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {"workload": f"config2: {n} x {args.size}B IPv4/UDP frames per GPU, "
+                                   "packed 64B-stride UMEM, 1% bad L3 / 1% bad L4 / "
+                                   "0.5% malformed / 0.1% ARP / 0.1% NDP",
+                       "frames_per_gpu": n, "frame_size": args.size,
+                       "header_window": args.window, "parallelism": f"shard{world}"},
+            "gbps": round(gbps, 1),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic,
+                         "kernel_ms": round(kms, 4),
+                         "bytes_per_frame": BYTES_PER_FRAME},
+            "cpu_baseline": cpu,
+            "verdicts_ok": bool(ok_t.item() > 0),
+        }
+        if secondary:
+            line["secondary_1500B"] = secondary
+        if e2e:
+            line["e2e_host_path"] = e2e
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,455 @@
+// SPDX-License-Identifier: GPL-2.0
+/*
+ * xdpgpu.cpp - host side of the C ABI in include/xdpgpu.h.
+ *
+ * A context owns one device, two HIP streams (two in-flight RX batches), a
+ * device mirror of the registered host UMEM and per-block counter slots.
+ * The host path copies the UMEM span a batch touches (or, for a sparse
+ * batch, lets the kernel read the pinned UMEM in place), the descriptors,
+ * launches the RX kernel and copies verdicts/results/tuples back.
+ */
+#include <hip/hip_runtime.h>
+
+#include <errno.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <new>
+
+#include "xdpgpu.h"
+#include "xdpgpu_internal.h"
+
+using namespace xdpgpu;
+
+namespace {
+
+constexpr uint32_t kSlots = 2;
+constexpr uint32_t kDefaultMaxBatch = 1u << 20;
+
+struct Slot {
+	hipStream_t stream = nullptr;
+	hipEvent_t done = nullptr;
+	unsigned long long *d_stats = nullptr; /* kMaxRxBlocks * CNT_SLOT */
+	xdpgpu_desc *d_desc = nullptr;
+	uint8_t *d_verdict = nullptr;
+	xdpgpu_result *d_res = nullptr;
+	uint8_t *d_tup = nullptr;
+	bool busy = false;
+	/* pending host copies for xdpgpu_wait() */
+	uint32_t n = 0;
+};
+
+} // namespace
+
+struct xdpgpu_ctx {
+	xdpgpu_cfg cfg;
+	uint32_t max_blocks = kMaxRxBlocks;
+	Slot slot[kSlots];
+	/* registered host UMEM */
+	uint8_t *h_umem = nullptr;
+	uint64_t umem_size = 0;
+	bool pinned = false;
+	uint8_t *d_umem = nullptr;       /* device mirror                  */
+	uint8_t *d_umem_mapped = nullptr; /* device view of pinned host UMEM */
+	char err[256];
+};
+
+static int set_err(xdpgpu_ctx *ctx, int rc, const char *fmt, ...)
+{
+	if (ctx) {
+		va_list ap;
+		va_start(ap, fmt);
+		vsnprintf(ctx->err, sizeof(ctx->err), fmt, ap);
+		va_end(ap);
+	}
+	return rc;
+}
+
+#define HIP_TRY(ctx, call)                                                   \
+	do {                                                                 \
+		hipError_t e_ = (call);                                      \
+		if (e_ != hipSuccess)                                        \
+			return set_err((ctx), -EIO, "%s: %s", #call,         \
+				       hipGetErrorString(e_));               \
+	} while (0)
+
+static uint32_t tuple_bytes(uint32_t fmt)
+{
+	return fmt == XDPGPU_TUPLE_NET ? 44u : fmt == XDPGPU_TUPLE_V4 ? 16u : 0u;
+}
+
+extern "C" {
+
+int xdpgpu_abi_version(void)
+{
+	return XDPGPU_ABI_VERSION;
+}
+
+int xdpgpu_device_count(void)
+{
+	int n = 0;
+	if (hipGetDeviceCount(&n) != hipSuccess)
+		return 0;
+	return n;
+}
+
+const char *xdpgpu_last_error(xdpgpu_ctx *ctx)
+{
+	return ctx ? ctx->err : "no context";
+}
+
+static void free_slot(Slot &s)
+{
+	if (s.d_stats)
+		(void)hipFree(s.d_stats);
+	if (s.d_desc)
+		(void)hipFree(s.d_desc);
+	if (s.d_verdict)
+		(void)hipFree(s.d_verdict);
+	if (s.d_res)
+		(void)hipFree(s.d_res);
+	if (s.d_tup)
+		(void)hipFree(s.d_tup);
+	if (s.done)
+		(void)hipEventDestroy(s.done);
+	if (s.stream)
+		(void)hipStreamDestroy(s.stream);
+	s = Slot();
+}
+
+void xdpgpu_fini(xdpgpu_ctx *ctx)
+{
+	if (!ctx)
+		return;
+	(void)hipSetDevice(ctx->cfg.device);
+	(void)hipDeviceSynchronize();
+	for (uint32_t i = 0; i < kSlots; i++)
+		free_slot(ctx->slot[i]);
+	if (ctx->d_umem)
+		(void)hipFree(ctx->d_umem);
+	if (ctx->pinned)
+		(void)hipHostUnregister(ctx->h_umem);
+	delete ctx;
+}
+
+int xdpgpu_init(const xdpgpu_cfg *cfg, xdpgpu_ctx **out)
+{
+	if (!cfg || !out)
+		return -EINVAL;
+	if (cfg->window != 0 && cfg->window != 64 && cfg->window != 128)
+		return -EINVAL;
+	if (cfg->tuple_fmt > XDPGPU_TUPLE_NET)
+		return -EINVAL;
+	int ndev = xdpgpu_device_count();
+	if (ndev <= 0)
+		return -ENODEV;
+	if (cfg->device < 0 || cfg->device >= ndev)
+		return -EINVAL;
+
+	xdpgpu_ctx *ctx = new (std::nothrow) xdpgpu_ctx();
+	if (!ctx)
+		return -ENOMEM;
+	ctx->cfg = *cfg;
+	if (!ctx->cfg.window)
+		ctx->cfg.window = 64;
+	if (!ctx->cfg.max_batch)
+		ctx->cfg.max_batch = kDefaultMaxBatch;
+	ctx->err[0] = 0;
+
+	int rc = 0;
+	do {
+		hipDeviceProp_t prop;
+		if (hipSetDevice(cfg->device) != hipSuccess ||
+		    hipGetDeviceProperties(&prop, cfg->device) != hipSuccess) {
+			rc = set_err(ctx, -EIO, "hipSetDevice(%d) failed", cfg->device);
+			break;
+		}
+		ctx->max_blocks = std::min<uint32_t>(kMaxRxBlocks,
+			(uint32_t)prop.multiProcessorCount * 8u);
+		for (uint32_t i = 0; i < kSlots && !rc; i++) {
+			Slot &s = ctx->slot[i];
+			size_t stat_bytes = (size_t)kMaxRxBlocks * CNT_SLOT * 8;
+			if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||
+			    hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess ||
+			    hipMalloc(&s.d_stats, stat_bytes) != hipSuccess ||
+			    hipMemset(s.d_stats, 0, stat_bytes) != hipSuccess)
+				rc = set_err(ctx, -ENOMEM, "slot %u allocation failed", i);
+		}
+	} while (0);
+	if (rc) {
+		xdpgpu_fini(ctx);
+		return rc;
+	}
+	*out = ctx;
+	return 0;
+}
+
+int xdpgpu_register_umem(xdpgpu_ctx *ctx, void *base, uint64_t size,
+			 uint32_t chunk_size, uint32_t headroom, uint32_t flags)
+{
+	if (!ctx || !base || !size)
+		return -EINVAL;
+	if (!(flags & XDPGPU_UMEM_UNALIGNED_CHUNK_FLAG) && chunk_size &&
+	    (chunk_size & (chunk_size - 1)))
+		return set_err(ctx, -EINVAL, "chunk_size %u not a power of two",
+			       chunk_size);
+	if (headroom && chunk_size && headroom >= chunk_size)
+		return -EINVAL;
+	HIP_TRY(ctx, hipSetDevice(ctx->cfg.device));
+	if (ctx->d_umem) {
+		HIP_TRY(ctx, hipDeviceSynchronize());
+		(void)hipFree(ctx->d_umem);
+		ctx->d_umem = nullptr;
+	}
+	if (ctx->pinned) {
+		(void)hipHostUnregister(ctx->h_umem);
+		ctx->pinned = false;
+	}
+	ctx->h_umem = (uint8_t *)base;
+	ctx->umem_size = size;
+	ctx->d_umem_mapped = nullptr;
+	/* pin (and map) the caller's UMEM; pageable memory still works,
+	 * only slower */
+	if (hipHostRegister(base, size, hipHostRegisterMapped) == hipSuccess) {
+		ctx->pinned = true;
+		void *dp = nullptr;
+		if (hipHostGetDevicePointer(&dp, base, 0) == hipSuccess)
+			ctx->d_umem_mapped = (uint8_t *)dp;
+	} else {
+		(void)hipGetLastError();
+	}
+	/* +64: 16-byte loads of a frame's last chunk stay inside the mirror */
+	if (hipMalloc(&ctx->d_umem, size + 64) != hipSuccess)
+		return set_err(ctx, -ENOMEM, "device UMEM mirror of %llu bytes",
+			       (unsigned long long)size);
+	return 0;
+}
+
+static int ensure_slot_buffers(xdpgpu_ctx *ctx, Slot &s, uint32_t n)
+{
+	if (s.d_desc)
+		return 0;
+	uint32_t cap = ctx->cfg.max_batch;
+	uint32_t tb = tuple_bytes(ctx->cfg.tuple_fmt);
+	if (hipMalloc(&s.d_desc, (size_t)cap * sizeof(xdpgpu_desc)) != hipSuccess ||
+	    hipMalloc(&s.d_verdict, (size_t)cap) != hipSuccess ||
+	    hipMalloc(&s.d_res, (size_t)cap * sizeof(xdpgpu_result)) != hipSuccess ||
+	    (tb && hipMalloc(&s.d_tup, (size_t)cap * tb) != hipSuccess))
+		return set_err(ctx, -ENOMEM, "batch buffers for %u descriptors", cap);
+	(void)n;
+	return 0;
+}
+
+static int enqueue_rx(xdpgpu_ctx *ctx, uint8_t *d_umem, uint64_t usize,
+		      const xdpgpu_desc *d_desc, uint32_t n, uint8_t *d_verdict,
+		      xdpgpu_result *d_res, uint8_t *d_tup,
+		      unsigned long long *d_stats, hipStream_t stream)
+{
+	RxArgs a;
+	a.umem = d_umem;
+	a.usize = usize;
+	a.desc = d_desc;
+	a.n = n;
+	a.tuple_fmt = d_tup ? ctx->cfg.tuple_fmt : XDPGPU_TUPLE_NONE;
+	a.verdict = d_verdict;
+	a.res = d_res;
+	a.tup = d_tup;
+	a.flags = ctx->cfg.flags;
+	a.initval = ctx->cfg.jhash_initval;
+	a.stats = (ctx->cfg.flags & XDPGPU_CFG_STATS) ? d_stats : nullptr;
+	uint32_t blocks = rx_grid_blocks(n, ctx->max_blocks);
+	HIP_TRY(ctx, launch_rx(a, ctx->cfg.window, blocks, stream));
+	return 0;
+}
+
+int xdpgpu_process_dev(xdpgpu_ctx *ctx, void *d_umem, uint64_t umem_size,
+		       const xdpgpu_desc *d_descs, uint32_t n,
+		       uint8_t *d_verdict, xdpgpu_result *d_res, void *d_tuples,
+		       void *stream)
+{
+	if (!ctx || !d_umem || !d_descs || !d_verdict)
+		return -EINVAL;
+	if (n == 0)
+		return 0;
+	hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
+	return enqueue_rx(ctx, (uint8_t *)d_umem, umem_size, d_descs, n,
+			  d_verdict, d_res, (uint8_t *)d_tuples,
+			  ctx->slot[0].d_stats, st);
+}
+
+int xdpgpu_submit(xdpgpu_ctx *ctx, uint32_t slot, const xdpgpu_desc *descs,
+		  uint32_t n, uint8_t *verdict, xdpgpu_result *res,
+		  void *tuples)
+{
+	if (!ctx || slot >= kSlots || !descs || !verdict)
+		return -EINVAL;
+	if (!ctx->h_umem)
+		return set_err(ctx, -EINVAL, "no UMEM registered");
+	if (n > ctx->cfg.max_batch)
+		return -E2BIG;
+	Slot &s = ctx->slot[slot];
+	if (s.busy)
+		return set_err(ctx, -EBUSY, "slot %u in flight", slot);
+	HIP_TRY(ctx, hipSetDevice(ctx->cfg.device));
+	int rc = ensure_slot_buffers(ctx, s, n);
+	if (rc)
+		return rc;
+	s.n = n;
+	if (n == 0)
+		return 0;
+
+	/* UMEM span this batch touches (+1 byte: udp_csum's odd over-read) */
+	uint64_t lo = UINT64_MAX, hi = 0, used = 0;
+	for (uint32_t i = 0; i < n; i++) {
+		uint64_t eff = (descs[i].addr & ((1ull << 48) - 1)) +
+			       (descs[i].addr >> 48);
+		if (eff >= ctx->umem_size)
+			continue;
+		uint64_t end = eff + descs[i].len + 1;
+		if (end > ctx->umem_size)
+			end = ctx->umem_size;
+		lo = std::min(lo, eff);
+		hi = std::max(hi, end);
+		used += descs[i].len;
+	}
+	uint8_t *kumem = ctx->d_umem;
+	bool zero_copy = false;
+	if (hi > lo) {
+		uint64_t span = hi - lo;
+		/* sparse batch over pinned memory: read the frames in place */
+		if (ctx->d_umem_mapped && !(ctx->umem_size & 15) &&
+		    span > 4 * used + (1u << 20)) {
+			kumem = ctx->d_umem_mapped;
+			zero_copy = true;
+		} else {
+			HIP_TRY(ctx, hipMemcpyAsync(ctx->d_umem + lo, ctx->h_umem + lo,
+						    span, hipMemcpyHostToDevice,
+						    s.stream));
+		}
+	}
+	HIP_TRY(ctx, hipMemcpyAsync(s.d_desc, descs, (size_t)n * sizeof(*descs),
+				    hipMemcpyHostToDevice, s.stream));
+	uint8_t *d_tup = (tuples && ctx->cfg.tuple_fmt) ? s.d_tup : nullptr;
+	rc = enqueue_rx(ctx, kumem, ctx->umem_size, s.d_desc, n, s.d_verdict,
+			res ? s.d_res : nullptr, d_tup, s.d_stats, s.stream);
+	if (rc)
+		return rc;
+	HIP_TRY(ctx, hipMemcpyAsync(verdict, s.d_verdict, n,
+				    hipMemcpyDeviceToHost, s.stream));
+	if (res)
+		HIP_TRY(ctx, hipMemcpyAsync(res, s.d_res, (size_t)n * sizeof(*res),
+					    hipMemcpyDeviceToHost, s.stream));
+	if (d_tup)
+		HIP_TRY(ctx, hipMemcpyAsync(tuples, d_tup,
+					    (size_t)n * tuple_bytes(ctx->cfg.tuple_fmt),
+					    hipMemcpyDeviceToHost, s.stream));
+	/* echo rewrites happened in the mirror: bring the span back */
+	if ((ctx->cfg.flags & XDPGPU_CFG_ICMP6_ECHO) && !zero_copy && hi > lo)
+		HIP_TRY(ctx, hipMemcpyAsync(ctx->h_umem + lo, ctx->d_umem + lo,
+					    hi - lo, hipMemcpyDeviceToHost, s.stream));
+	HIP_TRY(ctx, hipEventRecord(s.done, s.stream));
+	s.busy = true;
+	return 0;
+}
+
+int xdpgpu_wait(xdpgpu_ctx *ctx, uint32_t slot)
+{
+	if (!ctx || slot >= kSlots)
+		return -EINVAL;
+	Slot &s = ctx->slot[slot];
+	if (!s.busy)
+		return 0;
+	s.busy = false;
+	HIP_TRY(ctx, hipEventSynchronize(s.done));
+	return 0;
+}
+
+int xdpgpu_process(xdpgpu_ctx *ctx, const xdpgpu_desc *descs, uint32_t n,
+		   uint8_t *verdict, xdpgpu_result *res, void *tuples)
+{
+	int rc = xdpgpu_submit(ctx, 0, descs, n, verdict, res, tuples);
+	if (rc)
+		return rc;
+	return xdpgpu_wait(ctx, 0);
+}
+
+int xdpgpu_sync(xdpgpu_ctx *ctx, void *stream)
+{
+	if (!ctx)
+		return -EINVAL;
+	HIP_TRY(ctx, hipSetDevice(ctx->cfg.device));
+	if (stream) {
+		HIP_TRY(ctx, hipStreamSynchronize((hipStream_t)stream));
+		return 0;
+	}
+	for (uint32_t i = 0; i < kSlots; i++)
+		HIP_TRY(ctx, hipStreamSynchronize(ctx->slot[i].stream));
+	return 0;
+}
+
+int xdpgpu_stats(xdpgpu_ctx *ctx, struct xdpgpu_stats *out)
+{
+	if (!ctx || !out)
+		return -EINVAL;
+	HIP_TRY(ctx, hipSetDevice(ctx->cfg.device));
+	HIP_TRY(ctx, hipDeviceSynchronize());
+	memset(out, 0, sizeof(*out));
+	static thread_local unsigned long long host[kMaxRxBlocks * CNT_SLOT];
+	for (uint32_t i = 0; i < kSlots; i++) {
+		HIP_TRY(ctx, hipMemcpy(host, ctx->slot[i].d_stats, sizeof(host),
+				       hipMemcpyDeviceToHost));
+		for (uint32_t b = 0; b < kMaxRxBlocks; b++) {
+			const unsigned long long *c = host + (size_t)b * CNT_SLOT;
+			out->frames += c[CNT_FRAMES];
+			out->bytes += c[CNT_BYTES];
+			for (int v = 0; v < XDPGPU_NUM_VERDICTS; v++)
+				out->verdict[v] += c[CNT_VERDICT0 + v];
+			out->l3_bad += c[CNT_L3_BAD];
+			out->l4_bad += c[CNT_L4_BAD];
+			out->l4_absent += c[CNT_L4_ABSENT];
+			out->frag += c[CNT_FRAG];
+		}
+	}
+	return 0;
+}
+
+int xdpgpu_stats_reset(xdpgpu_ctx *ctx)
+{
+	if (!ctx)
+		return -EINVAL;
+	HIP_TRY(ctx, hipSetDevice(ctx->cfg.device));
+	HIP_TRY(ctx, hipDeviceSynchronize());
+	for (uint32_t i = 0; i < kSlots; i++)
+		HIP_TRY(ctx, hipMemset(ctx->slot[i].d_stats, 0,
+				       (size_t)kMaxRxBlocks * CNT_SLOT * 8));
+	return 0;
+}
+
+int xdpgpu_jhash_dev(xdpgpu_ctx *ctx, const void *d_keys, uint32_t key_len,
+		     uint32_t key_stride, uint32_t n, uint32_t initval,
+		     uint32_t *d_out, void *stream)
+{
+	if (!ctx || (!d_keys && n) || (!d_out && n) || key_stride < key_len)
+		return -EINVAL;
+	hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
+	HIP_TRY(ctx, launch_jhash((const uint8_t *)d_keys, key_len, key_stride,
+				  n, initval, d_out, st));
+	return 0;
+}
+
+int xdpgpu_ip_fast_csum_dev(xdpgpu_ctx *ctx, const void *d_hdrs,
+			    uint32_t hdr_stride, uint32_t n, uint16_t *d_out,
+			    void *stream)
+{
+	if (!ctx || (!d_hdrs && n) || (!d_out && n) || hdr_stride < 60)
+		return -EINVAL;
+	hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
+	HIP_TRY(ctx, launch_ip_fast_csum((const uint8_t *)d_hdrs, hdr_stride, n,
+					 d_out, st));
+	return 0;
+}
+
+} // extern "C"

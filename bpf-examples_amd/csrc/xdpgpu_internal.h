@@ -1,0 +1,55 @@
+// SPDX-License-Identifier: GPL-2.0
+/* Internal interface between the host C-ABI (xdpgpu.cpp) and the kernels
+ * (xdp_rx.hip).  Not installed; include/xdpgpu.h is the public boundary. */
+#ifndef XDPGPU_INTERNAL_H
+#define XDPGPU_INTERNAL_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "xdpgpu.h"
+
+namespace xdpgpu {
+
+/* Per-block counter slot layout (u64 each); slots summed by xdpgpu_stats. */
+enum {
+	CNT_FRAMES = 0,
+	CNT_BYTES = 1,
+	CNT_VERDICT0 = 2, /* .. +4 */
+	CNT_L3_BAD = 7,
+	CNT_L4_BAD = 8,
+	CNT_L4_ABSENT = 9,
+	CNT_FRAG = 10,
+	CNT_SLOT = 16,
+};
+
+/* Upper bound on the RX kernel grid (blocks of 256 threads): 8 per CU on a
+ * 256-CU MI355X.  Sizes the per-block counter area. */
+constexpr uint32_t kMaxRxBlocks = 2048;
+
+struct RxArgs {
+	uint8_t *umem;
+	uint64_t usize;
+	const xdpgpu_desc *desc;
+	uint32_t n;
+	uint32_t tuple_fmt;
+	uint8_t *verdict;
+	xdpgpu_result *res;
+	uint8_t *tup;
+	uint32_t flags;
+	uint32_t initval;
+	unsigned long long *stats; /* [kMaxRxBlocks][CNT_SLOT] or null */
+};
+
+hipError_t launch_rx(const RxArgs &a, uint32_t window, uint32_t blocks,
+		     hipStream_t stream);
+uint32_t rx_grid_blocks(uint32_t n, uint32_t max_blocks);
+
+hipError_t launch_jhash(const uint8_t *keys, uint32_t key_len,
+			uint32_t stride, uint32_t n, uint32_t initval,
+			uint32_t *out, hipStream_t stream);
+hipError_t launch_ip_fast_csum(const uint8_t *hdrs, uint32_t stride,
+			       uint32_t n, uint16_t *out, hipStream_t stream);
+
+} // namespace xdpgpu
+
+#endif

@@ -1,0 +1,260 @@
+/* SPDX-License-Identifier: GPL-2.0 */
+/*
+ * xdpgpu.h - C ABI of the MI355X (gfx950) AF_XDP receive-path transform.
+ *
+ * This is the drop-in boundary for the per-packet hot path of
+ * xdp-project/bpf-examples: Ethernet/VLAN/IPv4/IPv6/L4 parse
+ * (include/xdp/parsing_helpers.h), Internet one's-complement checksum
+ * verify/recompute (AF_XDP-interaction/lib_checksum.h) and jhash flow-key
+ * hashing (include/jhash.h), with the per-packet XDP verdict of
+ * AF_XDP-interaction/af_xdp_kern.c.
+ *
+ * Plain C: pointers, sizes and fixed-layout structs only.  Every entry point
+ * returns 0 or a negative errno (-EINVAL, -ENOMEM, -EIO for a HIP failure,
+ * -E2BIG for a batch above cfg.max_batch, -ENODEV when no GPU is present).
+ * Per-frame problems are never errors: they are verdicts (XDPGPU_ABORTED).
+ *
+ * Which reference interface each entry point replaces is noted on the entry
+ * point (file:line into the reference tree).  See INTEGRATION.md for the
+ * binding a maintainer adds on the reference side.
+ */
+#ifndef XDPGPU_H
+#define XDPGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define XDPGPU_ABI_VERSION 1
+
+/* Per-frame verdicts: the numeric values of enum xdp_action
+ * (headers/linux/bpf.h:6283-6289). */
+enum xdpgpu_verdict {
+	XDPGPU_ABORTED  = 0, /* parse error / truncated / bad descriptor    */
+	XDPGPU_DROP     = 1, /* bad IPv4 header or L4 checksum              */
+	XDPGPU_PASS     = 2, /* ARP or IPv6 NDP: left to the kernel stack   */
+	XDPGPU_TX       = 3, /* ICMPv6 echo request rewritten into a reply  */
+	XDPGPU_REDIRECT = 4, /* delivered to the application (XSK)          */
+};
+#define XDPGPU_NUM_VERDICTS 5
+
+/* Descriptor: identical layout to struct xdp_desc
+ * (headers/linux/if_xdp.h:109-113).  In unaligned-chunk mode the frame
+ * offset lives in bits 63..48 (XSK_UNALIGNED_BUF_OFFSET_SHIFT,
+ * headers/linux/if_xdp.h:104-106); the effective UMEM offset is always
+ * (addr & ((1<<48)-1)) + (addr >> 48), which equals addr in aligned mode. */
+struct xdpgpu_desc {
+	uint64_t addr;
+	uint32_t len;
+	uint32_t options;
+};
+
+/* Result flags */
+#define XDPGPU_F_L3_OK     0x01 /* IPv4 header checksum verifies (or IPv6)  */
+#define XDPGPU_F_L4_OK     0x02 /* L4 checksum verifies (or is absent)      */
+#define XDPGPU_F_VLAN      0x04 /* at least one 802.1Q/802.1ad tag consumed */
+#define XDPGPU_F_IPV6      0x08
+#define XDPGPU_F_FRAG      0x10 /* IPv4 MF/offset or IPv6 fragment header    */
+#define XDPGPU_F_L4_ABSENT 0x20 /* IPv4/UDP with stored checksum 0          */
+#define XDPGPU_F_IP        0x40 /* an IPv4 or IPv6 header was parsed        */
+#define XDPGPU_F_L4        0x80 /* a TCP/UDP/ICMP/ICMPv6 header was parsed  */
+
+/* Per-frame result record, 16 bytes.  Checksum words are u16 values as
+ * stored in memory on little-endian (the two bytes are the wire bytes).
+ * Frames with verdict ABORTED or PASS carry an all-zero record: they are
+ * not delivered to the application (af_xdp_kern.c:178-183). */
+struct xdpgpu_result {
+	uint32_t hash;     /* jhash(network_tuple, 44, initval)  jhash.h:68  */
+	uint16_t l3_csum;  /* recomputed IPv4 header checksum (check as 0)   */
+	uint16_t l4_csum;  /* recomputed TCP/UDP/ICMP(v6) checksum            */
+	uint8_t  flags;    /* XDPGPU_F_*                                      */
+	uint8_t  l4_proto; /* IPv4 protocol / final IPv6 next header          */
+	uint8_t  l3_off;   /* offset of the L3 header (14 + 4 * vlans)        */
+	uint8_t  nvlan;    /* VLAN tags consumed (0..2)                       */
+	uint16_t l4_off;   /* offset of the L4 header                         */
+	uint16_t l4_len;   /* L4 bytes covered by the checksum                */
+};
+
+/* Tuple formats */
+#define XDPGPU_TUPLE_NONE 0
+#define XDPGPU_TUPLE_V4   1 /* struct xdpgpu_tuple4, 16 B               */
+#define XDPGPU_TUPLE_NET  2 /* struct xdpgpu_network_tuple, 44 B        */
+
+/* IPv4-compact 5-tuple.  Addresses and ports in wire order. */
+struct xdpgpu_tuple4 {
+	uint32_t saddr;
+	uint32_t daddr;
+	uint16_t sport;
+	uint16_t dport;
+	uint8_t  proto;
+	uint8_t  ipv;      /* 2 (AF_INET), 10 (AF_INET6) or 0 (not IP)  */
+	uint16_t vlan_id;  /* outer VID (TCI & 0x0fff), host order       */
+};
+
+/* Flow key hashed by jhash: the layout of pping's struct network_tuple
+ * (pping/pping.h:120-139); IPv4 addresses mapped to ::ffff:a.b.c.d
+ * (pping/pping_kern.c:212-217).  Ports in wire order, 0 for non-TCP/UDP. */
+struct xdpgpu_network_tuple {
+	uint8_t  saddr[16];
+	uint16_t sport;
+	uint16_t rsvd0;
+	uint8_t  daddr[16];
+	uint16_t dport;
+	uint16_t rsvd1;
+	uint16_t proto;
+	uint8_t  ipv;
+	uint8_t  rsvd2;
+};
+
+/* cfg.flags */
+#define XDPGPU_CFG_VERIFY_CSUM 0x1 /* bad checksum -> XDP_DROP (xdp_synproxy_kern.c:610-623) */
+#define XDPGPU_CFG_ICMP6_ECHO  0x2 /* process_packet echo responder (af_xdp_user.c:968-1040)  */
+#define XDPGPU_CFG_STATS       0x4 /* keep per-verdict counters (xdpgpu_stats)                */
+#define XDPGPU_CFG_DEFAULT     (XDPGPU_CFG_VERIFY_CSUM | XDPGPU_CFG_STATS)
+
+struct xdpgpu_cfg {
+	int32_t  device;        /* HIP device ordinal                          */
+	uint32_t flags;         /* XDPGPU_CFG_*                                */
+	uint32_t max_batch;     /* max descriptors per host-path call (0: 2^20) */
+	uint32_t jhash_initval; /* initval of jhash (CLI option, default 0)    */
+	uint32_t tuple_fmt;     /* XDPGPU_TUPLE_*                              */
+	uint32_t window;        /* header bytes staged in LDS: 64 or 128 (0: 64) */
+	uint32_t rsvd[2];
+};
+
+/* UMEM registration flags (headers/linux/if_xdp.h:31) */
+#define XDPGPU_UMEM_UNALIGNED_CHUNK_FLAG (1u << 0)
+
+struct xdpgpu_stats {
+	uint64_t frames;
+	uint64_t bytes;
+	uint64_t verdict[XDPGPU_NUM_VERDICTS];
+	uint64_t l3_bad;
+	uint64_t l4_bad;
+	uint64_t l4_absent;
+	uint64_t frag;
+	uint64_t rsvd[5];
+};
+
+struct xdpgpu_ctx;
+
+/* Create a context bound to one GPU and one HIP stream pair.  A context is
+ * the GPU analogue of one xsk_socket_info (af_xdp_user.c:85-98): one per RX
+ * thread/queue, not re-entrant. */
+int xdpgpu_init(const struct xdpgpu_cfg *cfg, struct xdpgpu_ctx **out);
+void xdpgpu_fini(struct xdpgpu_ctx *ctx);
+
+/* Register the host UMEM (replaces xsk_umem__create's buffer argument,
+ * af_xdp_user.c:433 / xdpsock.c:1004).  The memory stays owned by the caller;
+ * it is pinned (hipHostRegister) and mirrored on the device. */
+int xdpgpu_register_umem(struct xdpgpu_ctx *ctx, void *base, uint64_t size,
+			 uint32_t chunk_size, uint32_t headroom, uint32_t flags);
+
+/* Batch replacement of the per-descriptor loop
+ *   for each desc: process_packet(xsk, addr, len)   (af_xdp_user.c:1092-1100)
+ * and of the kernel-side verdict xdp_sock_prog() (af_xdp_kern.c:150-191).
+ * Host buffers: descs[n] in, verdict[n] out (required), res[n] and
+ * tuples[n] (format cfg.tuple_fmt) out, both nullable.  Synchronous.
+ * With XDPGPU_CFG_ICMP6_ECHO, TX frames are rewritten in the host UMEM. */
+int xdpgpu_process(struct xdpgpu_ctx *ctx, const struct xdpgpu_desc *descs,
+		   uint32_t n, uint8_t *verdict, struct xdpgpu_result *res,
+		   void *tuples);
+
+/* Asynchronous form of xdpgpu_process on one of two in-flight slots
+ * (double buffering of the RX batches).  Output buffers must stay valid
+ * until xdpgpu_wait(ctx, slot) returns. */
+int xdpgpu_submit(struct xdpgpu_ctx *ctx, uint32_t slot,
+		  const struct xdpgpu_desc *descs, uint32_t n, uint8_t *verdict,
+		  struct xdpgpu_result *res, void *tuples);
+int xdpgpu_wait(struct xdpgpu_ctx *ctx, uint32_t slot);
+
+/* Device-resident form: every pointer is device memory (d_umem is written
+ * only for ICMPv6 echo rewrites).  stream is a hipStream_t (NULL: the
+ * context's stream).  Returns after the launch is enqueued.  d_umem must
+ * be readable up to round_up(umem_size, 16) (the kernel loads 16-byte
+ * aligned chunks and masks what lies past umem_size). */
+int xdpgpu_process_dev(struct xdpgpu_ctx *ctx, void *d_umem,
+		       uint64_t umem_size, const struct xdpgpu_desc *d_descs,
+		       uint32_t n, uint8_t *d_verdict,
+		       struct xdpgpu_result *d_res, void *d_tuples,
+		       void *stream);
+
+/* Counters accumulated over every launch of this context (synchronises). */
+int xdpgpu_stats(struct xdpgpu_ctx *ctx, struct xdpgpu_stats *out);
+int xdpgpu_stats_reset(struct xdpgpu_ctx *ctx);
+
+/* Device primitives, one lane per item (device pointers, stream as above).
+ * jhash over n keys of key_len bytes at key_stride   (include/jhash.h:68-105)
+ * ip_fast_csum over n IPv4 headers at hdr_stride      (lib_checksum.h:103-106) */
+int xdpgpu_jhash_dev(struct xdpgpu_ctx *ctx, const void *d_keys,
+		     uint32_t key_len, uint32_t key_stride, uint32_t n,
+		     uint32_t initval, uint32_t *d_out, void *stream);
+int xdpgpu_ip_fast_csum_dev(struct xdpgpu_ctx *ctx, const void *d_hdrs,
+			    uint32_t hdr_stride, uint32_t n, uint16_t *d_out,
+			    void *stream);
+
+/* Wait for all work of the context (or of stream if non-NULL). */
+int xdpgpu_sync(struct xdpgpu_ctx *ctx, void *stream);
+
+int xdpgpu_device_count(void);
+const char *xdpgpu_last_error(struct xdpgpu_ctx *ctx);
+int xdpgpu_abi_version(void);
+
+/* ------------------------------------------------------------------ */
+/* Synthetic UMEM pool generator (host).  Replaces the reference's packet
+ * generators gen_eth_hdr_data (xdpsock.c:893-971) and gen_base_pkt
+ * (af_xdp_user.c:688-700) for pool mode.                              */
+
+enum xdpgpu_pool_kind {
+	XDPGPU_POOL_UDP4       = 0, /* fixed-size IPv4/UDP from a flow table   */
+	XDPGPU_POOL_IMIX       = 1, /* 64/570/1500 7:4:1, VLAN/QinQ, v4/v6, ... */
+	XDPGPU_POOL_XDPSOCK    = 2, /* xdpsock txonly base frame, replicated    */
+	XDPGPU_POOL_AFXDP_USER = 3, /* af_xdp_user base frame, replicated       */
+};
+
+struct xdpgpu_pool_spec {
+	uint32_t kind;         /* enum xdpgpu_pool_kind                       */
+	uint32_t frame_size;   /* declared size S (L2 = S-4 + 4 B FCS slot)   */
+	uint32_t stride;       /* bytes between frames (0: round_up(S, 64))   */
+	uint32_t headroom;     /* bytes before each frame inside its stride   */
+	uint64_t seed;
+	uint32_t flow_bits;    /* log2 of the flow table (0: 20)              */
+	uint32_t ppm_bad_l3;   /* per-million corrupt IPv4 header checksums    */
+	uint32_t ppm_bad_l4;   /* per-million corrupt L4 checksums             */
+	uint32_t ppm_malformed;/* per-million truncated / malformed frames     */
+	uint32_t ppm_arp;
+	uint32_t ppm_ndp;
+	uint32_t ppm_echo6;    /* per-million ICMPv6 echo requests             */
+	uint32_t vlan;         /* xdpsock -V: tag frames with vlan_id/pri      */
+	uint16_t vlan_id;
+	uint16_t vlan_pri;
+	uint32_t fill_pattern; /* xdpsock -P / af_xdp_user opt_pkt_fill_pattern */
+	uint8_t  dmac[6];
+	uint8_t  smac[6];
+	uint32_t saddr;        /* wire order; 0 = the generator's default     */
+	uint32_t daddr;
+	uint32_t threads;      /* 0: hardware concurrency                     */
+	uint32_t rsvd[3];
+};
+
+/* Bytes of UMEM needed for n frames of this spec. */
+uint64_t xdpgpu_pool_size(const struct xdpgpu_pool_spec *spec, uint32_t n);
+
+/* Fill umem (>= xdpgpu_pool_size bytes) and descs[n]; expect[n] (nullable)
+ * receives the verdict the generator intended for each frame under
+ * XDPGPU_CFG_VERIFY_CSUM without ICMP6_ECHO. */
+int xdpgpu_pool_generate(const struct xdpgpu_pool_spec *spec, uint8_t *umem,
+			 uint64_t umem_size, struct xdpgpu_desc *descs,
+			 uint32_t n, uint8_t *expect);
+
+/* Set a spec to the defaults of BASELINE config kind (frame size S). */
+void xdpgpu_pool_spec_default(struct xdpgpu_pool_spec *spec, uint32_t kind,
+			      uint32_t frame_size, uint64_t seed);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* XDPGPU_H */

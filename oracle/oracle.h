@@ -1,0 +1,57 @@
+/* SPDX-License-Identifier: GPL-2.0 */
+/*
+ * oracle.h - TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference algorithms on the hot path, used as the
+ * parity checker by tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg.  Nothing in the product (bpf-examples_amd/) links,
+ * loads or calls this code.
+ */
+#ifndef XDP_ORACLE_H
+#define XDP_ORACLE_H
+
+#include <stdint.h>
+#include "xdpgpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* primitives (see xdp_oracle.c for the reference file:line of each) */
+uint32_t oracle_do_csum(const uint8_t *buf, int len);
+uint16_t oracle_ip_fast_csum(const uint8_t *iph, unsigned int ihl);
+uint16_t oracle_csum_fold(uint32_t csum);
+uint32_t oracle_csum_tcpudp_nofold(uint32_t saddr, uint32_t daddr, uint32_t len,
+				   uint8_t proto, uint32_t sum);
+uint16_t oracle_csum_tcpudp_magic(uint32_t saddr, uint32_t daddr, uint32_t len,
+				  uint8_t proto, uint32_t sum);
+uint16_t oracle_udp_csum(uint32_t saddr, uint32_t daddr, uint32_t len,
+			 uint8_t proto, const uint8_t *l4);
+uint16_t oracle_csum_ipv6_magic(const uint8_t *saddr, const uint8_t *daddr,
+				uint32_t len, uint8_t proto, uint32_t csum);
+uint16_t oracle_csum_replace2(uint16_t sum, uint16_t old, uint16_t new_);
+uint32_t oracle_jhash(const void *key, uint32_t length, uint32_t initval);
+uint32_t oracle_jhash2(const uint32_t *k, uint32_t length, uint32_t initval);
+uint32_t oracle_jhash_3words(uint32_t a, uint32_t b, uint32_t c, uint32_t initval);
+
+/* Whole per-frame pipeline over a batch: same inputs and outputs as
+ * xdpgpu_process_dev.  umem is written only for ICMPv6 echo rewrites. */
+int oracle_process(uint8_t *umem, uint64_t umem_size,
+		   const struct xdpgpu_desc *descs, uint32_t n,
+		   uint32_t cfg_flags, uint32_t initval, uint32_t tuple_fmt,
+		   uint8_t *verdict, struct xdpgpu_result *res, void *tuples,
+		   struct xdpgpu_stats *stats);
+
+/* CPU baseline: run oracle_process over descs[0..n) `reps` times on
+ * `threads` threads, each on a contiguous slice.  Returns wall seconds. */
+double oracle_bench(uint8_t *umem, uint64_t umem_size,
+		    const struct xdpgpu_desc *descs, uint32_t n,
+		    uint32_t cfg_flags, uint32_t initval, uint32_t tuple_fmt,
+		    uint8_t *verdict, struct xdpgpu_result *res, void *tuples,
+		    uint32_t threads, uint32_t reps);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

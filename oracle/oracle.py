@@ -1,0 +1,167 @@
+# SPDX-License-Identifier: GPL-2.0
+"""TEST INFRASTRUCTURE ONLY: ctypes binding of the parity oracle.
+
+oracle/liboracle.so is the CPU restatement of the reference pipeline
+(oracle/xdp_oracle.c).  Only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg import this module.  oracle/_ref/libref.so (reference
+headers compiled in place) is optional and only exists where /root/reference
+does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from typing import Optional
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "liboracle.so")
+REF_SO = os.path.join(HERE, "_ref", "libref.so")
+
+DESC_DTYPE = np.dtype([("addr", "<u8"), ("len", "<u4"), ("options", "<u4")])
+RESULT_DTYPE = np.dtype([
+    ("hash", "<u4"), ("l3_csum", "<u2"), ("l4_csum", "<u2"),
+    ("flags", "u1"), ("l4_proto", "u1"), ("l3_off", "u1"), ("nvlan", "u1"),
+    ("l4_off", "<u2"), ("l4_len", "<u2"),
+])
+TUPLE_BYTES = {0: 0, 1: 16, 2: 44}
+
+
+class OStats(C.Structure):
+    _fields_ = [("frames", C.c_uint64), ("bytes", C.c_uint64),
+                ("verdict", C.c_uint64 * 5), ("l3_bad", C.c_uint64),
+                ("l4_bad", C.c_uint64), ("l4_absent", C.c_uint64),
+                ("frag", C.c_uint64), ("rsvd", C.c_uint64 * 5)]
+
+
+_o = None
+_r = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib() -> C.CDLL:
+    global _o
+    if _o is None:
+        if not os.path.exists(ORACLE_SO):
+            build()
+        o = C.CDLL(ORACLE_SO)
+        u8p, vp, u32, u64 = C.c_char_p, C.c_void_p, C.c_uint32, C.c_uint64
+        o.oracle_do_csum.argtypes = [vp, C.c_int]
+        o.oracle_do_csum.restype = u32
+        o.oracle_ip_fast_csum.argtypes = [vp, C.c_uint]
+        o.oracle_ip_fast_csum.restype = C.c_uint16
+        o.oracle_csum_fold.argtypes = [u32]
+        o.oracle_csum_fold.restype = C.c_uint16
+        o.oracle_csum_tcpudp_nofold.argtypes = [u32, u32, u32, C.c_uint8, u32]
+        o.oracle_csum_tcpudp_nofold.restype = u32
+        o.oracle_csum_tcpudp_magic.argtypes = [u32, u32, u32, C.c_uint8, u32]
+        o.oracle_csum_tcpudp_magic.restype = C.c_uint16
+        o.oracle_udp_csum.argtypes = [u32, u32, u32, C.c_uint8, vp]
+        o.oracle_udp_csum.restype = C.c_uint16
+        o.oracle_csum_ipv6_magic.argtypes = [vp, vp, u32, C.c_uint8, u32]
+        o.oracle_csum_ipv6_magic.restype = C.c_uint16
+        o.oracle_csum_replace2.argtypes = [C.c_uint16, C.c_uint16, C.c_uint16]
+        o.oracle_csum_replace2.restype = C.c_uint16
+        o.oracle_jhash.argtypes = [vp, u32, u32]
+        o.oracle_jhash.restype = u32
+        o.oracle_jhash2.argtypes = [vp, u32, u32]
+        o.oracle_jhash2.restype = u32
+        o.oracle_jhash_3words.argtypes = [u32, u32, u32, u32]
+        o.oracle_jhash_3words.restype = u32
+        o.oracle_process.argtypes = [vp, u64, vp, u32, u32, u32, u32, vp, vp,
+                                     vp, C.POINTER(OStats)]
+        o.oracle_bench.argtypes = [vp, u64, vp, u32, u32, u32, u32, vp, vp,
+                                   vp, u32, u32]
+        o.oracle_bench.restype = C.c_double
+        del u8p
+        _o = o
+    return _o
+
+
+def ref_lib() -> Optional[C.CDLL]:
+    """The reference headers compiled in place, or None off this container."""
+    global _r
+    if _r is None:
+        if not os.path.exists(REF_SO):
+            if os.path.isdir("/root/reference"):
+                build()
+            if not os.path.exists(REF_SO):
+                return None
+        r = C.CDLL(REF_SO)
+        vp, u32 = C.c_void_p, C.c_uint32
+        r.ref_do_csum.argtypes = [vp, C.c_int]
+        r.ref_do_csum.restype = u32
+        r.ref_ip_fast_csum.argtypes = [vp, C.c_uint]
+        r.ref_ip_fast_csum.restype = C.c_uint16
+        r.ref_csum_fold.argtypes = [u32]
+        r.ref_csum_fold.restype = C.c_uint16
+        r.ref_csum_tcpudp_nofold.argtypes = [u32, u32, u32, C.c_uint8, u32]
+        r.ref_csum_tcpudp_nofold.restype = u32
+        r.ref_csum_tcpudp_magic.argtypes = [u32, u32, u32, C.c_uint8, u32]
+        r.ref_csum_tcpudp_magic.restype = C.c_uint16
+        r.ref_udp_csum.argtypes = [u32, u32, u32, C.c_uint8, vp]
+        r.ref_udp_csum.restype = C.c_uint16
+        r.ref_memset32_htonl.argtypes = [vp, u32, u32]
+        r.ref_memset32_htonl.restype = None
+        for name, n in (("ref_jhash", 3), ("ref_jhash2", 3)):
+            f = getattr(r, name)
+            f.argtypes = [vp, u32, u32]
+            f.restype = u32
+        r.ref_jhash_3words.argtypes = [u32, u32, u32, u32]
+        r.ref_jhash_3words.restype = u32
+        r.ref_jhash_2words.argtypes = [u32, u32, u32]
+        r.ref_jhash_2words.restype = u32
+        r.ref_jhash_1word.argtypes = [u32, u32]
+        r.ref_jhash_1word.restype = u32
+        _r = r
+    return _r
+
+
+def buf(b: bytes):
+    """A ctypes buffer holding b (kept alive by the caller)."""
+    return C.create_string_buffer(bytes(b), len(b) + 8)
+
+
+def process(umem: np.ndarray, descs: np.ndarray, flags: int = 0x5,
+            initval: int = 0, tuple_fmt: int = 1):
+    """Run the oracle pipeline: returns (verdict, res, tuples bytes, stats).
+
+    umem is modified in place only for ICMPv6 echo rewrites (flag 0x2)."""
+    o = lib()
+    descs = np.ascontiguousarray(descs, DESC_DTYPE)
+    n = len(descs)
+    verdict = np.zeros(n, np.uint8)
+    res = np.zeros(n, RESULT_DTYPE)
+    tb = TUPLE_BYTES[tuple_fmt]
+    tup = np.zeros(n * tb if tb else 1, np.uint8)
+    st = OStats()
+    rc = o.oracle_process(umem.ctypes.data, umem.nbytes, descs.ctypes.data, n,
+                          flags, initval & 0xffffffff, tuple_fmt,
+                          verdict.ctypes.data, res.ctypes.data,
+                          tup.ctypes.data if tb else None, C.byref(st))
+    if rc:
+        raise RuntimeError(f"oracle_process rc={rc}")
+    stats = {"frames": st.frames, "bytes": st.bytes,
+             "verdict": list(st.verdict), "l3_bad": st.l3_bad,
+             "l4_bad": st.l4_bad, "l4_absent": st.l4_absent, "frag": st.frag}
+    return verdict, res, (tup[: n * tb] if tb else None), stats
+
+
+def bench(umem: np.ndarray, descs: np.ndarray, threads: int, reps: int,
+          flags: int = 0x1, initval: int = 0, tuple_fmt: int = 1) -> float:
+    """Wall seconds for `reps` passes of the oracle over descs on `threads`."""
+    o = lib()
+    descs = np.ascontiguousarray(descs, DESC_DTYPE)
+    n = len(descs)
+    verdict = np.zeros(n, np.uint8)
+    res = np.zeros(n, RESULT_DTYPE)
+    tb = TUPLE_BYTES[tuple_fmt]
+    tup = np.zeros(max(1, n * tb), np.uint8)
+    return o.oracle_bench(umem.ctypes.data, umem.nbytes, descs.ctypes.data, n,
+                          flags, initval, tuple_fmt, verdict.ctypes.data,
+                          res.ctypes.data, tup.ctypes.data, threads, reps)

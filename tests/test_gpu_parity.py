@@ -1,0 +1,219 @@
+# SPDX-License-Identifier: GPL-2.0
+"""GPU parity: the HIP path (through the C ABI) against the committed golden
+vectors and the oracle, bit-exact, on the same inputs.  Runs on the MI355X
+box (`pytest -m gpu`)."""
+import numpy as np
+import pytest
+
+import oracle
+import xdpgpu
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+CFG_FLAGS = {"verify": 0x5, "echo_net": 0x7, "noverify": 0x4}
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need the MI355X"
+    assert xdpgpu.device_count() > 0
+    return torch.device("cuda:0")
+
+
+def to_dev(a: np.ndarray, pad: int = 64):
+    t = torch.zeros(a.nbytes + pad, dtype=torch.uint8, device="cuda:0")
+    t[: a.nbytes].copy_(torch.from_numpy(a.view(np.uint8).reshape(-1)))
+    return t
+
+
+def run_dev(umem, descs, flags=0x5, initval=0, fmt=1, window=64):
+    """Device-resident path; returns verdict, res, tuples, umem after, stats."""
+    n = len(descs)
+    ctx = xdpgpu.XdpGpu(0, flags | xdpgpu.CFG_STATS, initval, fmt, window)
+    d_umem = to_dev(umem)
+    d_desc = to_dev(np.ascontiguousarray(descs, xdpgpu.DESC_DTYPE), 16)
+    d_v = torch.full((max(n, 1),), 0xEE, dtype=torch.uint8, device="cuda:0")
+    d_res = torch.full((max(n, 1) * 16,), 0xEE, dtype=torch.uint8, device="cuda:0")
+    tb = xdpgpu.TUPLE_BYTES[fmt]
+    d_tup = torch.full((max(n * tb, 1),), 0xEE, dtype=torch.uint8, device="cuda:0") \
+        if tb else None
+    s = torch.cuda.current_stream()
+    ctx.process_dev(d_umem, umem.nbytes, d_desc, n, d_v, d_res, d_tup, stream=s)
+    torch.cuda.synchronize()
+    st = ctx.stats()
+    ctx.close()
+    v = d_v.cpu().numpy()[:n]
+    res = d_res.cpu().numpy()[: n * 16].view(xdpgpu.RESULT_DTYPE)
+    tup = d_tup.cpu().numpy()[: n * tb] if tb else None
+    um = d_umem.cpu().numpy()[: umem.nbytes]
+    return v, res, tup, um, st
+
+
+def assert_same(got, want, what):
+    gv, gres, gtup, gum = got
+    wv, wres, wtup, wum = want
+    bad = np.nonzero(gv != wv)[0]
+    assert len(bad) == 0, f"{what}: verdict mismatch at {bad[:8]}: {gv[bad[:8]]} vs {wv[bad[:8]]}"
+    gr, wr = gres.view(np.uint8).reshape(-1, 16), wres.view(np.uint8).reshape(-1, 16)
+    bad = np.nonzero((gr != wr).any(1))[0]
+    assert len(bad) == 0, f"{what}: result mismatch at {bad[:8]}:\n{gres[bad[:4]]}\n{wres[bad[:4]]}"
+    if wtup is not None:
+        tb = len(wtup) // max(len(wv), 1)
+        gt, wt = gtup.reshape(-1, tb), wtup.reshape(-1, tb)
+        bad = np.nonzero((gt != wt).any(1))[0]
+        assert len(bad) == 0, f"{what}: tuple mismatch at {bad[:8]}"
+    if gum is not None and wum is not None:
+        assert np.array_equal(gum, wum), f"{what}: UMEM after differs"
+
+
+def oracle_stats_match(st, ost):
+    assert st["frames"] == ost["frames"] and st["bytes"] == ost["bytes"]
+    assert [st["verdict"][n] for n in xdpgpu.VERDICT_NAMES] == ost["verdict"]
+    for k in ("l3_bad", "l4_bad", "l4_absent", "frag"):
+        assert st[k] == ost[k], k
+
+
+# ---------------------------------------------------------------- golden
+@pytest.mark.parametrize("window", [64, 128])
+@pytest.mark.parametrize("cfg", ["verify", "echo_net", "noverify"])
+def test_golden_fixtures_device(dev, golden, cfg, window):
+    fx, meta = golden
+    flags, iv, fmt = meta["cfgs"][cfg]
+    descs = fx["descs"].view(xdpgpu.DESC_DTYPE)
+    v, res, tup, um, st = run_dev(fx["umem"], descs, flags, iv, fmt, window)
+    want = (fx[f"{cfg}_verdict"], fx[f"{cfg}_res"].view(xdpgpu.RESULT_DTYPE),
+            fx[f"{cfg}_tup"], fx[f"{cfg}_umem_after"])
+    assert_same((v, res, tup, um), want, f"golden/{cfg}/w{window}")
+    ws = fx[f"{cfg}_stats"]
+    assert st["frames"] == ws[0] and st["bytes"] == ws[1]
+    assert [st["verdict"][n] for n in xdpgpu.VERDICT_NAMES] == list(ws[2:7])
+    assert [st["l3_bad"], st["l4_bad"], st["l4_absent"], st["frag"]] == list(ws[7:11])
+
+
+@pytest.mark.parametrize("cfg", ["verify", "echo_net"])
+def test_golden_fixtures_host_path(dev, golden, cfg):
+    """xdpgpu_process on host buffers (pinned UMEM, span copy, D2H)."""
+    fx, meta = golden
+    flags, iv, fmt = meta["cfgs"][cfg]
+    umem = fx["umem"].copy()
+    descs = fx["descs"].view(xdpgpu.DESC_DTYPE).copy()
+    with xdpgpu.XdpGpu(0, flags, iv, fmt) as ctx:
+        ctx.register_umem(umem)
+        v, res, tup = ctx.process(descs)
+    assert_same((v, res, tup.view(np.uint8).reshape(-1), umem),
+                (fx[f"{cfg}_verdict"], fx[f"{cfg}_res"].view(xdpgpu.RESULT_DTYPE),
+                 fx[f"{cfg}_tup"], fx[f"{cfg}_umem_after"]), f"host/{cfg}")
+
+
+# ---------------------------------------------------------------- pools
+POOLS = [
+    ("udp4_64", xdpgpu.POOL_UDP4, 64, 0x5EED0002, 1 << 20, {}),
+    ("udp4_1500", xdpgpu.POOL_UDP4, 1500, 0x5EED0002, 100000, {}),
+    ("imix", xdpgpu.POOL_IMIX, 64, 0x5EED0003, 300000, {}),
+    ("udp4_64_odd_addr", xdpgpu.POOL_UDP4, 64, 7, 100000, dict(headroom=1, stride=128)),
+    ("imix_4mod16", xdpgpu.POOL_IMIX, 64, 8, 50000, dict(headroom=4, stride=2048)),
+    ("echo6", xdpgpu.POOL_UDP4, 128, 9, 100000, dict(ppm_echo6=200000)),
+]
+
+
+@pytest.mark.parametrize("window", [64, 128])
+@pytest.mark.parametrize("name,kind,size,seed,n,kw", POOLS, ids=[p[0] for p in POOLS])
+def test_pool_vs_oracle(dev, name, kind, size, seed, n, kw, window):
+    umem, descs, expect = xdpgpu.pool_generate(n, kind, size, seed, **kw)
+    for flags, iv, fmt in ((0x5, 0, 1), (0x7, 0x9E3779B9, 2)):
+        ou = umem.copy()
+        ov, ores, otup, ost = oracle.process(ou, descs, flags, iv, fmt)
+        v, res, tup, um, st = run_dev(umem, descs, flags, iv, fmt, window)
+        assert_same((v, res, tup, um), (ov, ores, otup, ou), f"{name}/w{window}/{flags:#x}")
+        oracle_stats_match(st, ost)
+        if flags == 0x5:
+            np.testing.assert_array_equal(v, expect)
+
+
+def test_unaligned_encoded_descriptors(dev):
+    """Unaligned-chunk addresses (offset << 48 | base, if_xdp.h:104-106)."""
+    umem, descs, _ = xdpgpu.pool_generate(50000, xdpgpu.POOL_IMIX, 64, 11)
+    enc = descs.copy()
+    base = enc["addr"] & ~np.uint64(0xFFF)
+    enc["addr"] = ((enc["addr"] - base) << np.uint64(48)) | base
+    ov, ores, otup, _ = oracle.process(umem.copy(), descs, 0x5, 0, 1)
+    v, res, tup, um, _ = run_dev(umem, enc, 0x5, 0, 1)
+    assert_same((v, res, tup, None), (ov, ores, otup, None), "encoded")
+
+
+def test_full_size_config2(dev):
+    """BASELINE config 2 at full size: 16 M x 64 B.  Bit-exact against the
+    oracle for every frame, and the generator's intended verdicts."""
+    n = 16 << 20
+    umem, descs, expect = xdpgpu.pool_generate(n, xdpgpu.POOL_UDP4, 64, 0x5EED0002)
+    v, res, tup, _, st = run_dev(umem, descs, 0x5, 0, 1)
+    np.testing.assert_array_equal(v, expect)
+    ov, ores, otup, ost = oracle.process(umem, descs, 0x5, 0, 1)
+    assert_same((v, res, tup, None), (ov, ores, otup, None), "config2-16M")
+    oracle_stats_match(st, ost)
+
+
+def test_empty_batch(dev):
+    umem, descs, _ = xdpgpu.pool_generate(4, xdpgpu.POOL_UDP4, 64, 1)
+    v, res, tup, um, st = run_dev(umem, descs[:0], 0x5, 0, 1)
+    assert len(v) == 0 and st["frames"] == 0
+
+
+def test_host_double_buffer(dev):
+    """xdpgpu_submit/xdpgpu_wait on both slots, batches of an RX loop."""
+    umem, descs, expect = xdpgpu.pool_generate(200000, xdpgpu.POOL_IMIX, 64, 12)
+    ov, ores, otup, _ = oracle.process(umem.copy(), descs, 0x5, 0, 1)
+    B = 4096
+    with xdpgpu.XdpGpu(0, 0x5, 0, 1, max_batch=B) as ctx:
+        ctx.register_umem(umem)
+        v = np.zeros(len(descs), np.uint8)
+        res = np.zeros(len(descs), xdpgpu.RESULT_DTYPE)
+        tup = np.zeros(len(descs), xdpgpu.TUPLE4_DTYPE)
+        pending = [None, None]
+        for k, lo in enumerate(range(0, len(descs), B)):
+            slot = k & 1
+            if pending[slot] is not None:
+                ctx.wait(slot)
+            hi = min(lo + B, len(descs))
+            d = np.ascontiguousarray(descs[lo:hi])
+            pending[slot] = d
+            ctx.submit(slot, d, v[lo:hi], res[lo:hi], tup[lo:hi])
+        ctx.wait(0)
+        ctx.wait(1)
+        st = ctx.stats()
+    assert_same((v, res, tup.view(np.uint8).reshape(-1), None),
+                (ov, ores, otup, None), "double-buffer")
+    assert st["frames"] == len(descs)
+
+
+# ---------------------------------------------------------------- primitives
+def test_jhash_primitive_vectors(dev):
+    import os
+    vec = np.load(os.path.join(os.path.dirname(__file__), "golden", "jhash_vectors.npz"))
+    keys, klen, iv, want = vec["keys"], vec["klen"], vec["initval"], vec["jhash"]
+    ctx = xdpgpu.XdpGpu(0)
+    d_keys = to_dev(np.ascontiguousarray(keys))
+    out = torch.zeros(len(klen), dtype=torch.int32, device="cuda:0")
+    for L in np.unique(klen):
+        idx = np.nonzero(klen == L)[0]
+        for k in idx:
+            ctx.jhash_dev(d_keys.data_ptr() + int(k) * 64, int(L), 64, 1, int(iv[k]),
+                          out.data_ptr() + 4 * int(k))
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(got, want)
+    ctx.close()
+
+
+def test_ip_fast_csum_primitive_vectors(dev):
+    import os
+    vec = np.load(os.path.join(os.path.dirname(__file__), "golden", "csum_vectors.npz"))
+    hdrs = np.ascontiguousarray(vec["hdrs"])
+    ctx = xdpgpu.XdpGpu(0)
+    d = to_dev(hdrs)
+    out = torch.zeros(len(hdrs), dtype=torch.int16, device="cuda:0")
+    ctx.ip_fast_csum_dev(d, 60, len(hdrs), out)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint16), vec["ip_fast_csum"])
+    ctx.close()
