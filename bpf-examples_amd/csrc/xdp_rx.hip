@@ -81,6 +81,25 @@ __device__ __forceinline__ uint32_t keep_mask(uint64_t o, uint64_t lo,
 	return (0xffffffffu >> (32 - 8 * nb)) << (8 * (uint32_t)st);
 }
 
+/* Byte masks of the four dwords of the 16-byte chunk at p keeping the bytes
+ * in [lo, hi): 32-bit arithmetic on the chunk-relative bounds. */
+__device__ __forceinline__ uint4 chunk_keep(uint64_t p, uint64_t lo, uint64_t hi)
+{
+	const int32_t a0 = lo > p ? (int32_t)(lo - p < 16 ? lo - p : 16) : 0;
+	const int32_t b0 = hi > p ? (int32_t)(hi - p < 16 ? hi - p : 16) : 0;
+	uint32_t m[4];
+#pragma unroll
+	for (int j = 0; j < 4; j++) {
+		int32_t st = a0 - 4 * j, en = b0 - 4 * j;
+		st = st < 0 ? 0 : st > 4 ? 4 : st;
+		en = en < 0 ? 0 : en > 4 ? 4 : en;
+		const uint32_t fe = en ? (0xffffffffu >> ((32 - 8 * en) & 31)) : 0u;
+		const uint32_t fs = st ? (0xffffffffu >> ((32 - 8 * st) & 31)) : 0u;
+		m[j] = fe & ~fs;
+	}
+	return make_uint4(m[0], m[1], m[2], m[3]);
+}
+
 /* af_xdp_user.c:590-606 csum16_add / csum16_sub / csum_replace2 */
 __device__ __forceinline__ uint32_t c16_add(uint32_t csum, uint32_t addend)
 {
@@ -144,143 +163,189 @@ __device__ __forceinline__ uint32_t jhash_key44(const uint32_t k[11],
 /* ------------------------------------------------------------------ */
 /* frame byte access: LDS window first, global beyond it                */
 
-template <int WIN>
+template <int WIN, bool DEEP>
 struct FrameView {
-	const uint32_t *w;  /* this lane's LDS row (dword aligned)   */
-	const uint8_t *g;   /* umem + eff                             */
-	uint64_t gleft;     /* umem bytes from eff to the end         */
+	const uint32_t *w;    /* this lane's LDS row (dword aligned) */
+	const uint8_t *umem;  /* UMEM base (wave uniform)            */
+	uint64_t eff;         /* this frame's UMEM offset             */
+	uint64_t usize;
+	/* common path (DEEP false): set when a byte past the window was
+	 * wanted; the lane is then parsed again with DEEP true, which reads
+	 * such bytes from global memory */
+	uint32_t deep;
 
-	__device__ __forceinline__ uint32_t b8(uint32_t off) const
+	__device__ __forceinline__ uint32_t gbyte(uint32_t off) const
 	{
-		if (off < (uint32_t)WIN)
-			return (w[off >> 2] >> ((off & 3) * 8)) & 0xff;
-		return off < gleft ? g[off] : 0;
+		const uint64_t at = eff + off;
+		return at < usize ? umem[at] : 0;
 	}
-	/* network-order 16-bit field */
-	__device__ __forceinline__ uint32_t be16(uint32_t off) const
+	__device__ __forceinline__ uint32_t wd(uint32_t off)
 	{
-		if (off + 1 < (uint32_t)WIN && !(off & 1)) {
-			uint32_t d = w[off >> 2];
-			uint32_t h = (off & 2) ? (d >> 16) : (d & 0xffff);
-			return bswap16(h);
+		if constexpr (!DEEP)
+			deep |= off >= (uint32_t)WIN;
+		return w[(off >> 2) & (WIN / 4 - 1)];
+	}
+	__device__ __forceinline__ uint32_t b8(uint32_t off)
+	{
+		if constexpr (DEEP) {
+			if (off >= (uint32_t)WIN)
+				return gbyte(off);
 		}
-		return (b8(off) << 8) | b8(off + 1);
+		return (wd(off) >> ((off & 3) * 8)) & 0xff;
+	}
+	/* network-order 16-bit field at an even offset (every L2/L3/L4
+	 * field position is even: tags are 4 B, header lengths 4 B units) */
+	__device__ __forceinline__ uint32_t be16(uint32_t off)
+	{
+		if constexpr (DEEP) {
+			if (off + 1 >= (uint32_t)WIN || (off & 1))
+				return (b8(off) << 8) | b8(off + 1);
+		}
+		const uint32_t d = wd(off);
+		return bswap16((off & 2) ? (d >> 16) : (d & 0xffff));
 	}
 	/* 16 bits as a little-endian load of the wire bytes */
-	__device__ __forceinline__ uint32_t le16(uint32_t off) const
+	__device__ __forceinline__ uint32_t le16(uint32_t off)
 	{
 		return bswap16(be16(off));
 	}
-	__device__ __forceinline__ uint32_t le32(uint32_t off) const
+	__device__ __forceinline__ uint32_t le32(uint32_t off)
 	{
 		return le16(off) | (le16(off + 2) << 16);
 	}
-	/* Sum of LE u16 words (frame-relative parity) of the bytes in
-	 * [lo, hi) with [x, x+2) treated as zero, window part only. */
-	__device__ __forceinline__ uint32_t win_sum(uint32_t lo, uint32_t hi,
-						    uint32_t x) const
+	/*
+	 * Exact integer sum of the bytes in [lo, min(hi, WIN)) weighted as
+	 * little-endian dwords at frame-relative positions: byte r counts
+	 * 2^(8*(r&3)).  Congruent mod 0xffff to the lib_checksum.h sum of LE
+	 * 16-bit words, and 0 only if every byte is 0.  Masks touch only the
+	 * first and last dword.
+	 */
+	__device__ __forceinline__ uint64_t win_sum(uint32_t lo, uint32_t hi) const
 	{
-		uint32_t h = hi < (uint32_t)WIN ? hi : (uint32_t)WIN;
-		uint32_t s = 0;
-		for (uint32_t o = lo & ~3u; o < h; o += 4) {
-			uint32_t d = w[o >> 2];
-			d &= keep_mask(o, lo, h) & ~keep_mask(o, x, x + 2);
-			s += halves(d);
-		}
-		return s;
+		const uint32_t h = hi < (uint32_t)WIN ? hi : (uint32_t)WIN;
+		if (lo >= h)
+			return 0;
+		const uint32_t o0 = lo & ~3u, oL = (h - 1) & ~3u;
+		uint64_t s = 0;
+		for (uint32_t o = o0; o <= oL; o += 4)
+			s += w[o >> 2];
+		const uint32_t head = w[o0 >> 2] & ~(0xffffffffu << (8 * (lo & 3)));
+		const uint32_t tb = h - oL;          /* 1..4 bytes kept */
+		const uint32_t tail = tb >= 4 ? 0u :
+				      (w[oL >> 2] & (0xffffffffu << (8 * tb)));
+		return s - head - tail;
 	}
-	/* Same, bytes past the window, one lane on its own (rare: deep
-	 * headers only). */
-	__device__ uint32_t glob_sum(uint32_t lo, uint32_t hi, uint32_t x) const
+	/* The same weighting for the bytes of [lo, hi) past the window. */
+	__device__ uint64_t glob_sum(uint32_t lo, uint32_t hi)
 	{
-		uint32_t s = 0;
-		for (uint32_t o = lo > (uint32_t)WIN ? lo : (uint32_t)WIN; o < hi;
-		     o++) {
-			uint32_t v = o < gleft ? g[o] : 0;
-			if (o - x < 2)
-				v = 0;
-			s += (o & 1) ? (v << 8) : v;
+		if constexpr (!DEEP) {
+			deep |= hi > (uint32_t)WIN;
+			return 0;
 		}
+		uint64_t s = 0;
+		for (uint32_t o = lo > (uint32_t)WIN ? lo : (uint32_t)WIN; o < hi; o++)
+			s += (uint64_t)gbyte(o) << (8 * (o & 3));
 		return s;
 	}
 };
 
+/* weight of the 16-bit word at even frame position x in the sums above */
+__device__ __forceinline__ uint64_t word_weight(uint32_t x, uint32_t v)
+{
+	return (x & 2) ? ((uint64_t)v << 16) : (uint64_t)v;
+}
+
 /* ------------------------------------------------------------------ */
-/* per-lane parse state                                                 */
+/* per-lane parse state, packed: it stays live across the wave's
+ * cooperative payload loop, so it is kept to eight registers            */
 
 enum : uint32_t { ST_ABORT = 0, ST_PASS = 2, ST_GO = 0xff };
 
 struct Lane {
-	uint32_t st;
-	uint32_t l3, l4, nvlan, vid;
-	uint32_t ipv4, ipv6, nh;
-	uint32_t frag, has_l4, has_csum;
-	uint32_t cl, chk;       /* L4 checksum length, check offset      */
-	uint32_t rhi;           /* end of the summed L4 range (+over-read) */
-	uint32_t s3, c3;        /* IPv4 header sum (check zeroed), stored */
-	uint32_t s4, c4;        /* L4 sum window part (check zeroed)      */
-	uint32_t sa[4], da[4];
-	uint32_t sp, dp;
+	uint32_t m;      /* [7:0] state  [15:8] L4 proto / next header
+			  * [23:16] l3 offset  [25:24] VLAN tags  26 ipv4
+			  * 27 ipv6  28 frag  29 has_l4  30 has_csum  31 over-read */
+	uint32_t l4cl;   /* [15:0] l4 offset  [31:16] L4 checksum length  */
+	uint32_t chkvid; /* [15:0] L4 check offset  [27:16] outer VLAN id  */
+	uint32_t cks;    /* [15:0] stored IPv4 check  [31:16] stored L4 check */
+	uint32_t sums;   /* [15:0] IPv4 header sum  [31:16] L4 window sum;
+			  * folded to 16 bits (residue and zero-ness kept),
+			  * check words excluded */
+	uint32_t sa, da; /* IPv4 addresses: LE loads of the wire bytes */
+	uint32_t ports;  /* sport | dport << 16: LE loads of the wire bytes */
+
+	__device__ __forceinline__ uint32_t st() const { return m & 0xff; }
+	__device__ __forceinline__ uint32_t nh() const { return (m >> 8) & 0xff; }
+	__device__ __forceinline__ uint32_t l3() const { return (m >> 16) & 0xff; }
+	__device__ __forceinline__ uint32_t nvlan() const { return (m >> 24) & 3; }
+	__device__ __forceinline__ bool ipv4() const { return (m >> 26) & 1; }
+	__device__ __forceinline__ bool ipv6() const { return (m >> 27) & 1; }
+	__device__ __forceinline__ bool frag() const { return (m >> 28) & 1; }
+	__device__ __forceinline__ bool has_l4() const { return (m >> 29) & 1; }
+	__device__ __forceinline__ bool has_csum() const { return (m >> 30) & 1; }
+	__device__ __forceinline__ uint32_t over() const { return m >> 31; }
+	__device__ __forceinline__ uint32_t l4() const { return l4cl & 0xffff; }
+	__device__ __forceinline__ uint32_t cl() const { return l4cl >> 16; }
+	__device__ __forceinline__ uint32_t rhi() const { return l4() + cl() + over(); }
+	__device__ __forceinline__ uint32_t chk() const { return chkvid & 0xffff; }
+	__device__ __forceinline__ uint32_t vid() const { return chkvid >> 16; }
+	__device__ __forceinline__ uint32_t c3() const { return cks & 0xffff; }
+	__device__ __forceinline__ uint32_t c4() const { return cks >> 16; }
+	__device__ __forceinline__ uint32_t s3() const { return sums & 0xffff; }
+	__device__ __forceinline__ uint32_t s4() const { return sums >> 16; }
 };
 
 /* The pipeline of oracle/xdp_oracle.c frame_pipeline(), up to the sums. */
-template <int WIN>
-__device__ __forceinline__ void parse_lane(const FrameView<WIN> &F,
-					   uint32_t end, Lane &L)
+template <int WIN, bool DEEP>
+__device__ __forceinline__ Lane parse_lane(FrameView<WIN, DEEP> &F,
+					   uint32_t end)
 {
-	L.st = ST_ABORT;
-	L.l3 = L.l4 = L.nvlan = L.vid = 0;
-	L.ipv4 = L.ipv6 = L.nh = 0;
-	L.frag = L.has_l4 = L.has_csum = 0;
-	L.cl = L.chk = L.rhi = 0;
-	L.s3 = L.c3 = L.s4 = L.c4 = 0;
-	L.sp = L.dp = 0;
-#pragma unroll
-	for (int j = 0; j < 4; j++)
-		L.sa[j] = L.da[j] = 0;
+	Lane L;
+	L.m = ST_ABORT;
+	L.l4cl = L.chkvid = L.cks = L.sums = 0;
+	L.sa = L.da = L.ports = 0;
 
 	/* parse_ethhdr_vlan, parsing_helpers.h:86-129, VLAN_MAX_DEPTH 2 */
 	if (end < 14)
-		return;
+		return L;
 	uint32_t proto = F.be16(12);
-	uint32_t c = 14;
+	uint32_t l3 = 14, nvlan = 0, vid = 0;
 #pragma unroll
 	for (int i = 0; i < 2; i++) {
 		if (proto != 0x8100 && proto != 0x88A8)
 			break;
-		if (c + 4 > end)
+		if (l3 + 4 > end)
 			break;
 		if (i == 0)
-			L.vid = F.be16(c) & 0x0fff;
-		proto = F.be16(c + 2);
-		c += 4;
-		L.nvlan++;
+			vid = F.be16(l3) & 0x0fff;
+		proto = F.be16(l3 + 2);
+		l3 += 4;
+		nvlan++;
 	}
-	L.l3 = c;
-	const uint32_t l3 = c;
 
 	/* af_xdp_kern.c:114-148 parse_pkt__is_ARP_or_NDP */
 	if (proto == 0x0806) {
-		L.st = ST_PASS;
-		return;
+		L.m = ST_PASS;
+		return L;
 	}
-	L.ipv4 = (proto == 0x0800);
-	L.ipv6 = (proto == 0x86DD);
-	uint32_t ip_end = 0, nonfirst = 0;
-	int frag_at = -1;
+	const bool ipv4 = proto == 0x0800;
+	const bool ipv6 = proto == 0x86DD;
+	uint32_t ip_end = 0, nonfirst = 0, frag = 0, nh = 0, l4 = 0;
+	uint32_t s3 = 0, c3 = 0;
 
-	if (L.ipv6) {
+	if (ipv6) {
 		/* parse_ip6hdr :174-194 + skip_ip6hdrext :139-172 */
 		if (l3 + 40 > end)
-			return;
+			return L;
 		if ((F.b8(l3) >> 4) != 6)
-			return;
+			return L;
 		uint32_t cur = l3 + 40;
-		uint32_t nh = F.b8(l3 + 6);
+		nh = F.b8(l3 + 6);
+		int frag_at = -1;
 		bool found = false;
 		for (int i = 0; i < 6; i++) {
 			if (cur + 2 > end)
-				return;
+				return L;
 			if (nh == 0 || nh == 60 || nh == 43 || nh == 135) {
 				uint32_t hl = F.b8(cur + 1);
 				nh = F.b8(cur);
@@ -299,143 +364,137 @@ __device__ __forceinline__ void parse_lane(const FrameView<WIN> &F,
 			}
 		}
 		if (!found)
-			return;
-		L.nh = nh;
-		L.l4 = cur;
+			return L;
+		l4 = cur;
 		if (nh == 58) {
 			/* parse_icmp6hdr :224-237; NDP 133..137 -> PASS */
 			if (cur + 8 > end)
-				return;
-			uint32_t t = F.b8(cur);
+				return L;
+			const uint32_t t = F.b8(cur);
 			if (t >= 133 && t <= 137) {
-				L.st = ST_PASS;
-				return;
+				L.m = ST_PASS;
+				return L;
 			}
 		}
 		ip_end = l3 + 40 + F.be16(l3 + 4);
 		if (ip_end > end || cur > ip_end)
-			return;
+			return L;
 		if (frag_at >= 0) {
-			L.frag = 1;
+			frag = 1;
 			if (F.be16((uint32_t)frag_at + 2) >> 3)
 				nonfirst = 1;
 		}
-#pragma unroll
-		for (int j = 0; j < 4; j++) {
-			L.sa[j] = F.le32(l3 + 8 + 4 * j);
-			L.da[j] = F.le32(l3 + 24 + 4 * j);
-		}
-	} else if (L.ipv4) {
+	} else if (ipv4) {
 		/* parse_iphdr :196-222 */
 		if (l3 + 20 > end)
-			return;
-		uint32_t vihl = F.b8(l3);
+			return L;
+		const uint32_t vihl = F.b8(l3);
 		if ((vihl >> 4) != 4)
-			return;
-		uint32_t hl = (vihl & 0xf) * 4;
+			return L;
+		const uint32_t hl = (vihl & 0xf) * 4;
 		if (hl < 20)
-			return;
+			return L;
 		if (l3 + hl > end)
-			return;
-		L.nh = F.b8(l3 + 9);
-		uint32_t tot = F.be16(l3 + 2);
+			return L;
+		nh = F.b8(l3 + 9);
+		const uint32_t tot = F.be16(l3 + 2);
 		if (tot < hl || l3 + tot > end)
-			return;
+			return L;
 		ip_end = l3 + tot;
-		L.l4 = l3 + hl;
-		uint32_t fo = F.be16(l3 + 6) & 0x3fff;
+		l4 = l3 + hl;
+		const uint32_t fo = F.be16(l3 + 6) & 0x3fff;
 		if (fo) {
-			L.frag = 1;
+			frag = 1;
 			if (fo & 0x1fff)
 				nonfirst = 1;
 		}
-		/* header sum with the check word zeroed (af_xdp_user.c:664) */
-		L.c3 = F.le16(l3 + 10);
-		L.s3 = F.win_sum(l3, l3 + hl, l3 + 10);
+		/* header sum with the check word zeroed (af_xdp_user.c:664):
+		 * exact integer sum minus the check's own term */
+		c3 = F.le16(l3 + 10);
+		uint64_t s = F.win_sum(l3, l3 + hl);
 		if (l3 + hl > (uint32_t)WIN)
-			L.s3 += F.glob_sum(l3, l3 + hl, l3 + 10);
-		L.sa[0] = F.le32(l3 + 12);
-		L.da[0] = F.le32(l3 + 16);
+			s += F.glob_sum(l3, l3 + hl);
+		s3 = fold16(s - word_weight(l3 + 10, c3));
+		L.sa = F.le32(l3 + 12);
+		L.da = F.le32(l3 + 16);
 	}
 
-	if ((L.ipv4 || L.ipv6) && !nonfirst) {
-		const uint32_t l4 = L.l4;
-		const uint32_t nh = L.nh;
+	uint32_t has_l4 = 0, has_csum = 0, cl = 0, chk = 0;
+	if ((ipv4 || ipv6) && !nonfirst) {
 		if (nh == 17) {
 			/* parse_udphdr :272-290 */
 			if (l4 + 8 > end)
-				return;
-			uint32_t ulen = F.be16(l4 + 4);
+				return L;
+			const uint32_t ulen = F.be16(l4 + 4);
 			if (ulen < 8)
-				return;
-			L.has_l4 = 1;
-			if (!L.frag) {
+				return L;
+			has_l4 = 1;
+			if (!frag) {
 				if (l4 + ulen > ip_end)
-					return;
-				L.cl = ulen;
-				L.chk = l4 + 6;
-				L.has_csum = 1;
+					return L;
+				cl = ulen;
+				chk = l4 + 6;
+				has_csum = 1;
 			}
 		} else if (nh == 6) {
 			/* parse_tcphdr :295-318 */
 			if (l4 + 20 > end)
-				return;
-			uint32_t thl = (F.b8(l4 + 12) >> 4) * 4;
+				return L;
+			const uint32_t thl = (F.b8(l4 + 12) >> 4) * 4;
 			if (thl < 20 || l4 + thl > end)
-				return;
-			L.has_l4 = 1;
-			if (!L.frag) {
-				uint32_t cl = ip_end - l4;
+				return L;
+			has_l4 = 1;
+			if (!frag) {
+				cl = ip_end - l4;
 				if (cl < thl)
-					return;
-				L.cl = cl;
-				L.chk = l4 + 16;
-				L.has_csum = 1;
+					return L;
+				chk = l4 + 16;
+				has_csum = 1;
 			}
-		} else if ((nh == 1 && L.ipv4) || (nh == 58 && L.ipv6)) {
+		} else if ((nh == 1 && ipv4) || (nh == 58 && ipv6)) {
 			/* parse_icmphdr / parse_icmp6hdr :224-252 */
 			if (l4 + 8 > end)
-				return;
-			L.has_l4 = 1;
-			if (!L.frag) {
-				uint32_t cl = ip_end - l4;
+				return L;
+			has_l4 = 1;
+			if (!frag) {
+				cl = ip_end - l4;
 				if (cl < 8)
-					return;
-				L.cl = cl;
-				L.chk = l4 + 2;
-				L.has_csum = 1;
+					return L;
+				chk = l4 + 2;
+				has_csum = 1;
 			}
 		}
-		if (L.has_l4 && (nh == 6 || nh == 17)) {
-			L.sp = F.le16(l4);
-			L.dp = F.le16(l4 + 2);
-		}
+		if (has_l4 && (nh == 6 || nh == 17))
+			L.ports = F.le16(l4) | (F.le16(l4 + 2) << 16);
 	}
 
-	if (L.has_csum) {
+	uint32_t over = 0, c4 = 0, s4 = 0;
+	if (has_csum) {
 		/* udp_csum over-reads one byte for an odd length
 		 * (lib_checksum.h:175-176); csum_partial zero-pads (ICMP, v6) */
-		uint32_t over = (L.ipv4 && L.nh != 1) ? (L.cl & 1) : 0;
-		L.rhi = L.l4 + L.cl + over;
-		L.c4 = F.le16(L.chk);
-		L.s4 = F.win_sum(L.l4, L.rhi, L.chk);
+		over = (ipv4 && nh != 1) ? (cl & 1) : 0;
+		c4 = F.le16(chk);
+		uint64_t s = F.win_sum(l4, l4 + cl + over);
+		if (chk < (uint32_t)WIN)      /* else removed in the wave pass */
+			s -= word_weight(chk, c4);
+		s4 = fold16(s);
 	}
-	L.st = ST_GO;
+	L.m = ST_GO | (nh << 8) | (l3 << 16) | (nvlan << 24) |
+	      ((uint32_t)ipv4 << 26) | ((uint32_t)ipv6 << 27) | (frag << 28) |
+	      (has_l4 << 29) | (has_csum << 30) | (over << 31);
+	L.l4cl = l4 | (cl << 16);
+	L.chkvid = chk | (vid << 16);
+	L.cks = c3 | (c4 << 16);
+	L.sums = s3 | (s4 << 16);
+	return L;
 }
 
 /* ------------------------------------------------------------------ */
 /* wave helpers                                                         */
 
-__device__ __forceinline__ uint32_t shfl32(uint32_t v, int src)
+__device__ __forceinline__ uint32_t readlane32(uint32_t v, int src)
 {
-	return (uint32_t)__shfl((int)v, src, kWave);
-}
-
-__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src)
-{
-	uint32_t lo = shfl32((uint32_t)v, src);
-	uint32_t hi = shfl32((uint32_t)(v >> 32), src);
-	return ((uint64_t)hi << 32) | lo;
+	return (uint32_t)__builtin_amdgcn_readlane((int)v, src);
 }
 
 __device__ __forceinline__ uint32_t wave_sum32(uint32_t v)
@@ -457,21 +516,407 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v)
 	return v;
 }
 
+__device__ __forceinline__ uint4 load_desc(const xdpgpu_desc *d, uint64_t i,
+					   uint32_t n)
+{
+	if (i < n)
+		return *reinterpret_cast<const uint4 *>(d + i);
+	return make_uint4(0, 0, 0, 0);
+}
+
+/* Issue the transposed 16-byte window loads of one tile into registers.
+ * In load k, lane l fetches chunk (64k + l) % CPF of frame (64k + l) / CPF,
+ * so a packed pool is read as contiguous 1 KiB wave-instructions.  Returns
+ * true (and issues nothing) when a frame of the tile is not 16-byte
+ * aligned: the caller then stages bytes per lane. */
+template <int WIN>
+__device__ __forceinline__ bool issue_window(const RxArgs &a, uint4 dv,
+					     int lane, uint64_t *dtab,
+					     uint4 *fv)
+{
+	constexpr int CPF = WIN / 16;
+	const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
+	const uint32_t len = dv.z;
+	const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
+	const bool valid = (dv.x | dv.y | dv.z) != 0 && (uint64_t)len <= a.usize &&
+			   eff <= a.usize - len;
+	if (__ballot(valid && (eff & 15)))
+		return true;
+	/* per-frame staging word: eff << 8 | chunks to load (those starting
+	 * at or before len: the udp_csum over-read byte included) */
+	uint32_t nch = (len >> 4) + 1;
+	if (nch > (uint32_t)CPF)
+		nch = CPF;
+	dtab[lane] = valid ? ((eff << 8) | nch) : 0ull;
+	__builtin_amdgcn_wave_barrier();
+#pragma unroll
+	for (int k = 0; k < CPF; k++) {
+		const int q = k * kWave + lane;
+		const uint64_t e = dtab[q / CPF];
+		const int ch = q % CPF;
+		const uint64_t src = (e >> 8) + 16ull * ch;
+		uint4 v = make_uint4(0, 0, 0, 0);
+		if ((uint32_t)ch < (uint32_t)(e & 0xff) && src < a.usize) {
+			v = *reinterpret_cast<const uint4 *>(a.umem + src);
+			if (src + 16 > a.usize) {
+				const uint4 m = chunk_keep(src, src, a.usize);
+				v.x &= m.x;
+				v.y &= m.y;
+				v.z &= m.z;
+				v.w &= m.w;
+			}
+		}
+		fv[k] = v;
+	}
+	return false;
+}
+
+/* Write the chunks loaded by issue_window into the per-frame LDS rows. */
+template <int WIN>
+__device__ __forceinline__ void commit_window(uint32_t *win, const uint4 *fv,
+					      int lane)
+{
+	constexpr int CPF = WIN / 16;
+	constexpr int SDW = WIN / 4 + 1;
+#pragma unroll
+	for (int k = 0; k < CPF; k++) {
+		const int q = k * kWave + lane;
+		uint32_t *dst = win + (q / CPF) * SDW + (q % CPF) * 4;
+		dst[0] = fv[k].x;
+		dst[1] = fv[k].y;
+		dst[2] = fv[k].z;
+		dst[3] = fv[k].w;
+	}
+}
+
 /* ------------------------------------------------------------------ */
 /* the RX kernel                                                        */
 
+/* Wave counters (wave-uniform, scalar registers) */
+struct Counters {
+	uint32_t c[CNT_FRAG + 1];
+	uint64_t bytes; /* per lane */
+};
+
+/*
+ * L4 bytes past the header window, summed by the whole wave: for every lane
+ * in `need` the wave streams that frame's range in 1 KiB coalesced steps and
+ * reduces the 64 partial sums.  Returns, in the owning lane, the folded sum
+ * (frame-relative parity; check word removed if it lies in the range).
+ */
 template <int WIN>
-__global__ __launch_bounds__(kBlock) void xdp_rx_kernel(RxArgs a)
+__device__ __forceinline__ uint32_t ext_sums(const RxArgs &a, bool need,
+					     uint64_t eff, uint32_t l4,
+					     uint32_t rhi, uint32_t chk,
+					     uint32_t c4, int lane)
 {
-	constexpr int CPF = WIN / 16;      /* 16-B chunks per frame window */
-	constexpr int SDW = WIN / 4 + 1;   /* LDS row stride in dwords      */
-	__shared__ uint32_t lds[kWavesPerBlock * kWave * SDW];
+	uint64_t mask = __ballot(need);
+	uint32_t out = 0;
+	while (mask) {
+		const int src = __builtin_ctzll(mask);
+		mask &= mask - 1;
+		const uint64_t seff =
+			((uint64_t)readlane32((uint32_t)(eff >> 32), src) << 32) |
+			readlane32((uint32_t)eff, src);
+		const uint32_t sl4 = readlane32(l4, src);
+		const uint32_t srhi = readlane32(rhi, src);
+		const uint32_t schk = readlane32(chk, src);
+		const uint64_t lo = seff + (sl4 > (uint32_t)WIN ? sl4 : (uint32_t)WIN);
+		const uint64_t hi = seff + srhi;
+		const uint64_t lim = hi < a.usize ? hi : a.usize;
+		uint32_t acc = 0;
+		for (uint64_t p = (lo & ~15ull) + 16ull * lane; p < lim;
+		     p += 16ull * kWave) {
+			uint4 v = *reinterpret_cast<const uint4 *>(a.umem + p);
+			if (p < lo || p + 16 > lim) {
+				const uint4 m = chunk_keep(p, lo, lim);
+				v.x &= m.x;
+				v.y &= m.y;
+				v.z &= m.z;
+				v.w &= m.w;
+			}
+			acc += halves(v.x) + halves(v.y) + halves(v.z) + halves(v.w);
+		}
+		/* exact: the range is at most 64 KiB, so the raw sum of 16-bit
+		 * halves fits 32 bits */
+		acc = wave_sum32(acc);
+		if (schk >= (uint32_t)WIN) {
+			const uint32_t c = readlane32(c4, src);
+			acc -= (seff & 1) ? bswap16(c) : c;
+		}
+		uint32_t s = fold16(acc);
+		if (seff & 1)        /* absolute vs frame-relative parity */
+			s = bswap16(s);
+		if (lane == src)
+			out = s;
+	}
+	return out;
+}
+
+/*
+ * The generic pipeline on up to 64 frames (one per lane): any descriptor,
+ * any alignment, any header stack the oracle knows.  Used for the frames
+ * the fast path defers.  Writes verdict, result and tuple of each frame.
+ */
+template <int WIN>
+__device__ __forceinline__ void generic_batch(const RxArgs &a, uint32_t *win,
+					      uint64_t *dtab, int lane,
+					      uint64_t i, bool active,
+					      uint32_t (&cnt)[CNT_FRAG + 1],
+					      uint64_t &my_bytes)
+{
+	constexpr int SDW = WIN / 4 + 1;
+	const uint4 dv = active ? *reinterpret_cast<const uint4 *>(a.desc + i)
+				: make_uint4(0, 0, 0, 0);
+	const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
+	const uint32_t len = dv.z;
+	const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
+	const bool valid = active && (uint64_t)len <= a.usize &&
+			   eff <= a.usize - len;
+
+	/* stage the header windows */
+	uint4 cv[WIN / 16];
+	const bool misaligned = issue_window<WIN>(a, dv, lane, dtab, cv);
+	if (!misaligned) {
+		commit_window<WIN>(win, cv, lane);
+	} else {
+		/* unaligned-chunk UMEM: per-lane byte staging */
+		for (int d = 0; d < WIN / 4; d++) {
+			uint32_t wv = 0;
+#pragma unroll
+			for (int b = 0; b < 4; b++) {
+				const uint32_t off = 4 * d + b;
+				if (valid && off <= len && eff + off < a.usize)
+					wv |= (uint32_t)a.umem[eff + off] << (8 * b);
+			}
+			win[lane * SDW + d] = wv;
+		}
+	}
+	__builtin_amdgcn_wave_barrier();
+
+	/* parse: branch-free window reads; frames whose headers reach past
+	 * the window are parsed again with global-memory reads */
+	FrameView<WIN, false> F;
+	F.w = win + lane * SDW;
+	F.umem = a.umem;
+	F.eff = eff;
+	F.usize = a.usize;
+	F.deep = 0;
+	Lane L = parse_lane<WIN, false>(F, valid ? len : 0u); /* 0: ABORTED */
+	if (__ballot(F.deep)) {
+		if (F.deep) {
+			FrameView<WIN, true> G;
+			G.w = F.w;
+			G.umem = a.umem;
+			G.eff = eff;
+			G.usize = a.usize;
+			G.deep = 0;
+			L = parse_lane<WIN, true>(G, valid ? len : 0u);
+		}
+	}
+
+	const uint32_t ext_sum = ext_sums<WIN>(
+		a, L.st() == ST_GO && L.has_csum() && L.rhi() > (uint32_t)WIN,
+		eff, L.l4(), L.rhi(), L.chk(), L.c4(), lane);
+
+	/* checksums, flow key, verdict */
+	uint32_t verdict = L.st() == ST_PASS ? XDPGPU_PASS : XDPGPU_ABORTED;
+	uint4 rec = make_uint4(0, 0, 0, 0);
+	uint32_t key[11];
+#pragma unroll
+	for (int j = 0; j < 11; j++)
+		key[j] = 0;
+	uint32_t l3_bad = 0, l4_bad = 0, absent = 0;
+	if (L.st() == ST_GO) {
+		const bool ip = L.ipv4() || L.ipv6();
+		const uint32_t nh = L.nh(), cl = L.cl(), c4 = L.c4();
+		uint32_t flags = 0, l3c = 0, l4c = 0, l3_ok = 1, l4_ok = 0;
+		if (L.ipv4()) {
+			/* ip_fast_csum, lib_checksum.h:103-106 */
+			l3c = ~L.s3() & 0xffff;
+			l3_ok = fold16((uint64_t)L.s3() + L.c3()) == 0xffff;
+		}
+		if (L.has_csum()) {
+			const uint64_t body = (uint64_t)L.s4() + ext_sum;
+			uint64_t ph = 0;
+			if (L.ipv4() && nh != 1) {
+				/* udp_csum -> csum_tcpudp_magic,
+				 * lib_checksum.h:142-179 */
+				ph = (uint64_t)L.sa + L.da + ((uint64_t)(nh + cl) << 8);
+			} else if (L.ipv6()) {
+				/* csum_ipv6_magic, xdp_synproxy_kern.c:149-172 */
+				ph = (uint64_t)__builtin_bswap32(cl) +
+				     __builtin_bswap32(nh) +
+				     F.win_sum(L.l3() + 8, L.l3() + 40);
+			}
+			/* ICMPv4: no pseudo header, ~do_csum(msg) */
+			l4c = ~fold16(body + ph) & 0xffff;
+			l4_ok = (~fold16(body + c4 + ph) & 0xffff) == 0;
+			if (L.ipv4() && nh == 17 && c4 == 0) {
+				absent = 1;
+				l4_ok = 1;
+			}
+		}
+		if (L.nvlan())
+			flags |= XDPGPU_F_VLAN;
+		if (ip) {
+			flags |= XDPGPU_F_IP;
+			if (L.ipv6())
+				flags |= XDPGPU_F_IPV6;
+			if (l3_ok)
+				flags |= XDPGPU_F_L3_OK;
+			if (L.frag())
+				flags |= XDPGPU_F_FRAG;
+			if (L.has_l4())
+				flags |= XDPGPU_F_L4;
+			if (L.has_csum() && l4_ok)
+				flags |= XDPGPU_F_L4_OK;
+			if (absent)
+				flags |= XDPGPU_F_L4_ABSENT;
+			/* flow key: pping.h:120-139, v4 mapped as in
+			 * pping_kern.c:212-217 */
+			if (L.ipv4()) {
+				key[2] = 0xffff0000u;
+				key[3] = L.sa;
+				key[7] = 0xffff0000u;
+				key[8] = L.da;
+			} else {
+#pragma unroll
+				for (int j = 0; j < 4; j++) {
+					key[j] = F.le32(L.l3() + 8 + 4 * j);
+					key[5 + j] = F.le32(L.l3() + 24 + 4 * j);
+				}
+			}
+			key[4] = L.ports & 0xffff;
+			key[9] = L.ports >> 16;
+			key[10] = nh | ((L.ipv4() ? 2u : 10u) << 16);
+		}
+		rec.x = jhash_key44(key, a.initval);
+		l3_bad = L.ipv4() && !l3_ok;
+		l4_bad = L.has_csum() && !l4_ok;
+		rec.y = l3c | (l4c << 16);
+		rec.z = flags | ((ip ? nh : 0u) << 8) | (L.l3() << 16) |
+			(L.nvlan() << 24);
+		rec.w = ip ? (L.l4() | ((L.has_csum() ? cl : 0u) << 16)) : 0u;
+
+		verdict = XDPGPU_REDIRECT;
+		if ((a.flags & XDPGPU_CFG_VERIFY_CSUM) && (l3_bad || l4_bad)) {
+			verdict = XDPGPU_DROP;
+		} else if ((a.flags & XDPGPU_CFG_ICMP6_ECHO) &&
+			   L.nvlan() == 0 && L.ipv6() && len >= 62 &&
+			   F.b8(20) == 58 && F.b8(54) == 128) {
+			verdict = XDPGPU_TX;   /* rewritten below */
+		}
+	}
+	/* af_xdp_user.c:968-1040 echo responder, one frame at a time by the
+	 * whole wave: lane j writes byte j of the reply (MACs swapped, IPv6
+	 * addresses swapped, type 129, csum_replace2) */
+	uint64_t tx_mask = __ballot(verdict == XDPGPU_TX);
+	while (tx_mask) {
+		const int src = __builtin_ctzll(tx_mask);
+		tx_mask &= tx_mask - 1;
+		const uint64_t seff =
+			((uint64_t)readlane32((uint32_t)(eff >> 32), src) << 32) |
+			readlane32((uint32_t)eff, src);
+		const uint32_t *srow = win + src * SDW;
+		auto sb = [&](int j) -> uint32_t {
+			return (srow[j >> 2] >> ((j & 3) * 8)) & 0xff;
+		};
+		const int j = lane;
+		int from = -1;
+		uint32_t val = 0;
+		if (j < 6)
+			from = j + 6;
+		else if (j < 12)
+			from = j - 6;
+		else if (j >= 22 && j < 38)
+			from = j + 16;
+		else if (j >= 38 && j < 54)
+			from = j - 16;
+		if (from >= 0)
+			val = sb(from);
+		if (j == 54)
+			val = 129;
+		if (j == 56 || j == 57) {
+			const uint32_t ck = csum_replace2(sb(56) | (sb(57) << 8),
+							  0x0080, 0x0081);
+			val = (j == 56) ? (ck & 0xff) : (ck >> 8);
+		}
+		if (from >= 0 || j == 54 || j == 56 || j == 57)
+			a.umem[seff + j] = (uint8_t)val;
+	}
+	const bool rec_live = verdict != XDPGPU_ABORTED && verdict != XDPGPU_PASS;
+
+	/* outputs */
+	if (active) {
+		a.verdict[i] = (uint8_t)verdict;
+		if (a.res)
+			*reinterpret_cast<uint4 *>(a.res + i) = rec;
+		if (a.tup) {
+			if (a.tuple_fmt == XDPGPU_TUPLE_V4) {
+				uint4 tv = make_uint4(0, 0, 0, 0);
+				if (rec_live) {
+					const bool ip = L.ipv4() || L.ipv6();
+					tv.x = L.ipv4() ? L.sa : 0u;
+					tv.y = L.ipv4() ? L.da : 0u;
+					tv.z = L.ports;
+					tv.w = (ip ? L.nh() : 0u) |
+					       ((ip ? (L.ipv4() ? 2u : 10u) : 0u) << 8) |
+					       (L.vid() << 16);
+				}
+				*reinterpret_cast<uint4 *>(a.tup + 16 * i) = tv;
+			} else if (a.tuple_fmt == XDPGPU_TUPLE_NET) {
+				uint32_t *tp = reinterpret_cast<uint32_t *>(a.tup + 44 * i);
+#pragma unroll
+				for (int j = 0; j < 11; j++)
+					tp[j] = rec_live ? key[j] : 0u;
+			}
+		}
+	}
+
+	/* counters: ballot + popcount */
+	if (a.stats) {
+		cnt[CNT_FRAMES] += __popcll(__ballot(active));
+#pragma unroll
+		for (int v = 0; v < 5; v++)
+			cnt[CNT_VERDICT0 + v] +=
+				__popcll(__ballot(active && verdict == (uint32_t)v));
+		cnt[CNT_L3_BAD] += __popcll(__ballot(rec_live && l3_bad));
+		cnt[CNT_L4_BAD] += __popcll(__ballot(rec_live && l4_bad));
+		cnt[CNT_L4_ABSENT] += __popcll(__ballot(rec_live && absent));
+		cnt[CNT_FRAG] += __popcll(__ballot(rec_live && L.frag()));
+	}
+	my_bytes += active ? len : 0;
+}
+
+/* LE 16-bit loads of the VLAN TPIDs 0x8100 / 0x88A8 (parsing_helpers.h:75) */
+__device__ __forceinline__ bool le_is_vlan(uint32_t v)
+{
+	return v == 0x0081u || v == 0xa888u;
+}
+
+/* mask of the first nb (0..4) bytes of a dword */
+__device__ __forceinline__ uint32_t first_bytes(int32_t nb)
+{
+	nb = nb < 0 ? 0 : nb > 4 ? 4 : nb;
+	return nb ? (0xffffffffu >> ((32 - 8 * nb) & 31)) : 0u;
+}
+
+template <int WIN, int MINW, bool PF>
+__global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
+{
+	constexpr int SDW = WIN / 4 + 1;   /* LDS row stride in dwords */
+	constexpr int XQ = 2 * kWave;      /* exception queue per wave  */
+	__shared__ uint32_t lds[kWavesPerBlock * kWave * SDW + 8];
+	__shared__ uint64_t dtab_all[kWavesPerBlock * kWave];
+	__shared__ uint32_t xq_all[kWavesPerBlock * XQ];
 	__shared__ unsigned long long blk_cnt[CNT_SLOT];
 
 	const int lane = threadIdx.x & (kWave - 1);
 	const int wid = threadIdx.x / kWave;
 	uint32_t *win = lds + wid * kWave * SDW;
-	const uint32_t *row = win + lane * SDW;
+	uint64_t *dtab = dtab_all + wid * kWave;
+	uint32_t *xq = xq_all + wid * XQ;
 
 	if (threadIdx.x < CNT_SLOT)
 		blk_cnt[threadIdx.x] = 0;
@@ -479,282 +924,314 @@ __global__ __launch_bounds__(kBlock) void xdp_rx_kernel(RxArgs a)
 
 	const uint64_t ntiles = ((uint64_t)a.n + kWave - 1) / kWave;
 	const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
-	uint64_t cnt_frames = 0, cnt_v[5] = {0, 0, 0, 0, 0};
-	uint64_t cnt_l3 = 0, cnt_l4 = 0, cnt_abs = 0, cnt_frag = 0;
+	uint32_t cnt[CNT_FRAG + 1] = {};   /* wave-uniform */
 	uint64_t my_bytes = 0;
+	uint32_t xq_n = 0;                 /* deferred frames queued (uniform) */
+	uint32_t xout = 0;                 /* deferred frames flushed (uniform) */
+	const uint64_t wgid = (uint64_t)blockIdx.x * kWavesPerBlock + wid;
+	uint32_t *xl = a.xlist + wgid * a.xregion;
 
-	for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + wid;
-	     t < ntiles; t += nwaves) {
+	uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + wid;
+	uint4 dcur = load_desc(a.desc, t * kWave + lane, a.n);
+	uint4 dnext = dcur;
+	uint4 fv[PF ? WIN / 16 : 1];
+	bool mis_cur = false;
+	if constexpr (PF) {
+		/* software pipeline: the window loads of tile t+1 are in flight
+		 * while tile t is processed */
+		if (t < ntiles)
+			mis_cur = issue_window<WIN>(a, dcur, lane, dtab, fv);
+		dnext = load_desc(a.desc, (t + nwaves) * kWave + lane, a.n);
+	}
+	for (; t < ntiles; t += nwaves) {
 		const uint64_t i = t * kWave + lane;
 		const bool active = i < a.n;
 
-		/* 1. descriptor */
-		uint64_t addr = 0;
-		uint32_t len = 0;
-		if (active) {
-			uint4 dv = *reinterpret_cast<const uint4 *>(a.desc + i);
-			addr = ((uint64_t)dv.y << 32) | dv.x;
-			len = dv.z;
+		/* 1. descriptor (prefetched one tile ahead) */
+		uint4 dv;
+		if constexpr (PF) {
+			dv = dcur;
+		} else {
+			dv = dnext;
+			dnext = load_desc(a.desc, (t + nwaves) * kWave + lane, a.n);
 		}
+		const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
+		const uint32_t len = dv.z;
 		const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
 		const bool valid = active && (uint64_t)len <= a.usize &&
 				   eff <= a.usize - len;
 
-		/* 2. stage the header window into LDS */
-		const uint64_t misaligned = __ballot(valid && (eff & 15));
-		if (misaligned == 0) {
-#pragma unroll
-			for (int k = 0; k < CPF; k++) {
-				const int q = k * kWave + lane;
-				const int f = q / CPF;
-				const int ch = q % CPF;
-				const uint64_t feff = shfl64(eff, f);
-				const uint32_t flen = shfl32(len, f);
-				const uint32_t fval = shfl32(valid ? 1u : 0u, f);
-				const uint64_t src = feff + 16ull * ch;
-				uint4 v = make_uint4(0, 0, 0, 0);
-				if (fval && 16u * ch <= flen && src < a.usize) {
-					v = *reinterpret_cast<const uint4 *>(a.umem + src);
-					if (src + 16 > a.usize) {
-						v.x &= keep_mask(src, src, a.usize);
-						v.y &= keep_mask(src + 4, src, a.usize);
-						v.z &= keep_mask(src + 8, src, a.usize);
-						v.w &= keep_mask(src + 12, src, a.usize);
-					}
-				}
-				uint32_t *dst = win + f * SDW + ch * 4;
-				dst[0] = v.x;
-				dst[1] = v.y;
-				dst[2] = v.z;
-				dst[3] = v.w;
-			}
+		/* 2. stage the header windows (transposed 16-B loads); a tile
+		 * with an unaligned frame goes to the generic path whole */
+		bool misaligned;
+		if constexpr (PF) {
+			misaligned = mis_cur;
+			if (!misaligned)
+				commit_window<WIN>(win, fv, lane);
 		} else {
-			/* unaligned-chunk UMEM: per-lane byte staging */
-			for (int d = 0; d < WIN / 4; d++) {
-				uint32_t wv = 0;
-#pragma unroll
-				for (int b = 0; b < 4; b++) {
-					const uint32_t off = 4 * d + b;
-					if (valid && off <= len && eff + off < a.usize)
-						wv |= (uint32_t)a.umem[eff + off] << (8 * b);
-				}
-				win[lane * SDW + d] = wv;
-			}
+			uint4 cv[WIN / 16];
+			misaligned = issue_window<WIN>(a, dv, lane, dtab, cv);
+			if (!misaligned)
+				commit_window<WIN>(win, cv, lane);
 		}
 		__builtin_amdgcn_wave_barrier();
-
-		/* 3. per-lane parse */
-		FrameView<WIN> F;
-		F.w = row;
-		F.g = a.umem + eff;
-		F.gleft = a.usize - (valid ? eff : a.usize);
-		Lane L;
-		parse_lane<WIN>(F, valid ? len : 0u, L);   /* end 0 -> ABORTED */
-
-		/* 4. cooperative sum of L4 bytes past the window */
-		const bool need_ext = L.st == ST_GO && L.has_csum &&
-				      L.rhi > (uint32_t)WIN;
-		uint64_t ext_mask = __ballot(need_ext);
-		uint32_t ext_sum = 0;
-		while (ext_mask) {
-			const int src = __builtin_ctzll(ext_mask);
-			ext_mask &= ext_mask - 1;
-			const uint64_t seff = shfl64(eff, src);
-			const uint32_t sl4 = shfl32(L.l4, src);
-			const uint32_t srhi = shfl32(L.rhi, src);
-			const uint32_t schk = shfl32(L.chk, src);
-			const uint64_t lo = seff + (sl4 > (uint32_t)WIN ? sl4 : (uint32_t)WIN);
-			const uint64_t hi = seff + srhi;
-			const uint64_t x = seff + schk;
-			const uint64_t lim = hi < a.usize ? hi : a.usize;
-			uint32_t acc = 0;
-			for (uint64_t p = (lo & ~15ull) + 16ull * lane; p < lim;
-			     p += 16ull * kWave) {
-				uint4 v = *reinterpret_cast<const uint4 *>(a.umem + p);
-				v.x &= keep_mask(p, lo, lim) & ~keep_mask(p, x, x + 2);
-				v.y &= keep_mask(p + 4, lo, lim) & ~keep_mask(p + 4, x, x + 2);
-				v.z &= keep_mask(p + 8, lo, lim) & ~keep_mask(p + 8, x, x + 2);
-				v.w &= keep_mask(p + 12, lo, lim) & ~keep_mask(p + 12, x, x + 2);
-				acc += halves(v.x) + halves(v.y) + halves(v.z) + halves(v.w);
-			}
-			acc = wave_sum32(fold16(acc));
-			uint32_t s = fold16(acc);
-			if (seff & 1)        /* absolute vs frame-relative parity */
-				s = bswap16(s);
-			if (lane == src)
-				ext_sum = s;
+		if constexpr (PF) {
+			dcur = dnext;
+			if (t + nwaves < ntiles)
+				mis_cur = issue_window<WIN>(a, dcur, lane, dtab, fv);
+			dnext = load_desc(a.desc, (t + 2 * nwaves) * kWave + lane, a.n);
 		}
 
-		/* 5. checksums, flow key, verdict */
-		uint32_t verdict = L.st == ST_PASS ? XDPGPU_PASS : XDPGPU_ABORTED;
-		uint4 rec = make_uint4(0, 0, 0, 0);
-		uint32_t key[11];
-#pragma unroll
-		for (int j = 0; j < 11; j++)
-			key[j] = 0;
-		uint32_t l3_bad = 0, l4_bad = 0, absent = 0;
-		if (L.st == ST_GO) {
-			const bool ip = L.ipv4 || L.ipv6;
-			uint32_t flags = 0, l3c = 0, l4c = 0, l3_ok = 1, l4_ok = 0;
-			if (L.ipv4) {
-				/* ip_fast_csum, lib_checksum.h:103-106 */
-				l3c = ~fold16(L.s3) & 0xffff;
-				l3_ok = fold16((uint64_t)L.s3 + L.c3) == 0xffff;
-			}
-			if (L.has_csum) {
-				const uint64_t body = (uint64_t)L.s4 + ext_sum;
-				if (L.ipv4 && L.nh != 1) {
-					/* udp_csum -> csum_tcpudp_magic,
-					 * lib_checksum.h:142-179 */
-					const uint64_t ph = (uint64_t)L.sa[0] + L.da[0] +
-						((uint64_t)(L.nh + L.cl) << 8);
-					l4c = ~fold16(body + ph) & 0xffff;
-					l4_ok = (~fold16(body + L.c4 + ph) & 0xffff) == 0;
-					if (L.nh == 17 && L.c4 == 0) {
-						absent = 1;
-						l4_ok = 1;
-					}
-				} else if (L.ipv4) {
-					/* ICMP: ~do_csum(msg) */
-					l4c = ~fold16(body) & 0xffff;
-					l4_ok = (~fold16(body + L.c4) & 0xffff) == 0;
-				} else {
-					/* csum_ipv6_magic, xdp_synproxy_kern.c:149-172 */
-					uint64_t ph = (uint64_t)__builtin_bswap32(L.cl) +
-						      __builtin_bswap32(L.nh);
-#pragma unroll
-					for (int j = 0; j < 4; j++)
-						ph += (uint64_t)L.sa[j] + L.da[j];
-					l4c = ~fold16(body + ph) & 0xffff;
-					l4_ok = (~fold16(body + L.c4 + ph) & 0xffff) == 0;
-				}
-			}
-			if (L.nvlan)
-				flags |= XDPGPU_F_VLAN;
-			if (ip) {
-				flags |= XDPGPU_F_IP;
-				if (L.ipv6)
-					flags |= XDPGPU_F_IPV6;
-				if (l3_ok)
-					flags |= XDPGPU_F_L3_OK;
-				if (L.frag)
-					flags |= XDPGPU_F_FRAG;
-				if (L.has_l4)
-					flags |= XDPGPU_F_L4;
-				if (L.has_csum && l4_ok)
-					flags |= XDPGPU_F_L4_OK;
-				if (absent)
-					flags |= XDPGPU_F_L4_ABSENT;
-				/* flow key: pping.h:120-139, v4 mapped as in
-				 * pping_kern.c:212-217 */
-				if (L.ipv4) {
-					key[2] = 0xffff0000u;
-					key[3] = L.sa[0];
-					key[7] = 0xffff0000u;
-					key[8] = L.da[0];
-				} else {
-					key[0] = L.sa[0]; key[1] = L.sa[1];
-					key[2] = L.sa[2]; key[3] = L.sa[3];
-					key[5] = L.da[0]; key[6] = L.da[1];
-					key[7] = L.da[2]; key[8] = L.da[3];
-				}
-				key[4] = L.sp;
-				key[9] = L.dp;
-				key[10] = L.nh | ((L.ipv4 ? 2u : 10u) << 16);
-			}
-			const uint32_t hash = jhash_key44(key, a.initval);
-			l3_bad = L.ipv4 && !l3_ok;
-			l4_bad = L.has_csum && !l4_ok;
-			rec.x = hash;
-			rec.y = l3c | (l4c << 16);
-			rec.z = flags | ((ip ? L.nh : 0u) << 8) | (L.l3 << 16) |
-				(L.nvlan << 24);
-			rec.w = ip ? (L.l4 | ((L.has_csum ? L.cl : 0u) << 16)) : 0u;
+		/* 3. fast path: Ethernet + 0..2 VLAN tags + IPv4 (ihl 5, not a
+		 * fragment) + UDP/TCP, everything at fixed offsets from the L2
+		 * end.  Frames of any other shape are deferred (below).  The
+		 * results are those of the generic pipeline for such frames. */
+		const uint32_t *w = win + lane * SDW;
+		const uint32_t w3 = w[3], w4 = w[4];
+		uint32_t nv = 0;
+		if (le_is_vlan(w3 & 0xffff)) {
+			nv = 1;
+			if (le_is_vlan(w4 & 0xffff))
+				nv = 2;
+		}
+		const uint32_t *r = w + nv;        /* frame offsets shifted by 4*nv */
+		const uint32_t r3 = r[3], r4 = r[4], r5 = r[5], r6 = r[6];
+		const uint32_t r7 = r[7], r8 = r[8], r9 = r[9], r10 = r[10];
+		const uint32_t r11 = r[11], r12 = r[12];
+		const uint32_t l3 = 14 + 4 * nv, l4 = l3 + 20;
+		const uint32_t tot = bswap16(r4 & 0xffff);
+		const uint32_t proto = r5 >> 24;
+		const bool udp = proto == 17;
+		uint32_t cl;
+		bool fast = !a.force_generic && !misaligned && valid &&
+			    (r3 & 0x00ffffffu) == 0x00450008u &&
+			    (r5 & 0xff3fu) == 0 && (udp || proto == 6) &&
+			    tot >= 20 && l3 + tot <= len;
+		if (udp) {
+			cl = bswap16(r9 >> 16);
+			fast = fast && len >= l4 + 8 && cl >= 8 && l4 + cl <= l3 + tot;
+		} else {
+			const uint32_t thl = ((r11 >> 20) & 0xf) * 4;
+			cl = tot - 20;
+			fast = fast && len >= l4 + 20 && thl >= 20 && l4 + thl <= len &&
+			       cl >= thl;
+		}
 
-			verdict = XDPGPU_REDIRECT;
-			if ((a.flags & XDPGPU_CFG_VERIFY_CSUM) && (l3_bad || l4_bad)) {
-				verdict = XDPGPU_DROP;
-			} else if ((a.flags & XDPGPU_CFG_ICMP6_ECHO) &&
-				   L.nvlan == 0 && L.ipv6 && len >= 62 &&
-				   F.b8(20) == 58 && F.b8(54) == 128) {
-				/* af_xdp_user.c:968-1040 echo responder */
-				uint8_t *g = a.umem + eff;
-				for (int j = 0; j < 6; j++) {
-					uint8_t t0 = (uint8_t)F.b8(j);
-					g[j] = (uint8_t)F.b8(6 + j);
-					g[6 + j] = t0;
-				}
-				for (int j = 0; j < 16; j++) {
-					uint8_t t0 = (uint8_t)F.b8(22 + j);
-					g[22 + j] = (uint8_t)F.b8(38 + j);
-					g[38 + j] = t0;
-				}
-				g[54] = 129;
-				uint32_t ck = csum_replace2(F.le16(56), 0x0080, 0x0081);
-				g[56] = (uint8_t)ck;
-				g[57] = (uint8_t)(ck >> 8);
-				verdict = XDPGPU_TX;
+		/* 4. defer the other frames to this wave's region of the
+		 * exception list (LDS queue, flushed 64 at a time); the generic
+		 * kernel processes them after this launch */
+		const uint64_t dm = __ballot(active && !fast);
+		if (dm) {
+			const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+				(uint32_t)(dm >> 32),
+				__builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0));
+			if (active && !fast)
+				xq[xq_n + rank] = (uint32_t)i;
+			xq_n += (uint32_t)__popcll(dm);
+			if (xq_n >= (uint32_t)kWave) {
+				__builtin_amdgcn_wave_barrier();
+				xl[xout + lane] = xq[lane];
+				xout += kWave;
+				const uint32_t rest = xq[kWave + lane];
+				__builtin_amdgcn_wave_barrier();
+				xq[lane] = rest;
+				xq_n -= kWave;
 			}
 		}
-		const bool rec_live = verdict != XDPGPU_ABORTED && verdict != XDPGPU_PASS;
 
-		/* 6. outputs */
-		if (active) {
-			a.verdict[i] = (uint8_t)verdict;
-			if (a.res)
-				*reinterpret_cast<uint4 *>(a.res + i) = rec;
+		/* 5. fast frames: flow key, hash and tuple first (they do not
+		 * depend on the payload), then the checksums */
+		const uint32_t sa = (r6 >> 16) | (r7 << 16);
+		const uint32_t da = (r7 >> 16) | (r8 << 16);
+		const uint32_t ports = (r8 >> 16) | (r9 << 16);
+		uint32_t hash = 0;
+		if (fast) {
+			uint32_t key[11] = {0, 0, 0xffff0000u, sa, ports & 0xffff,
+					    0, 0, 0xffff0000u, da, ports >> 16,
+					    proto | (2u << 16)};
+			hash = jhash_key44(key, a.initval);
 			if (a.tup) {
 				if (a.tuple_fmt == XDPGPU_TUPLE_V4) {
-					uint4 tv = make_uint4(0, 0, 0, 0);
-					if (rec_live) {
-						tv.x = L.ipv4 ? L.sa[0] : 0u;
-						tv.y = L.ipv4 ? L.da[0] : 0u;
-						tv.z = L.sp | (L.dp << 16);
-						tv.w = ((L.ipv4 || L.ipv6) ? L.nh : 0u) |
-						       (((L.ipv4 || L.ipv6) ? (L.ipv4 ? 2u : 10u) : 0u) << 8) |
-						       (L.vid << 16);
-					}
-					*reinterpret_cast<uint4 *>(a.tup + 16 * i) = tv;
+					const uint32_t vid =
+						nv ? (bswap16(w3 >> 16) & 0x0fff) : 0u;
+					*reinterpret_cast<uint4 *>(a.tup + 16 * i) =
+						make_uint4(sa, da, ports,
+							   proto | (2u << 8) | (vid << 16));
 				} else if (a.tuple_fmt == XDPGPU_TUPLE_NET) {
 					uint32_t *tp = reinterpret_cast<uint32_t *>(a.tup + 44 * i);
 #pragma unroll
 					for (int j = 0; j < 11; j++)
-						tp[j] = rec_live ? key[j] : 0u;
+						tp[j] = key[j];
 				}
 			}
+			my_bytes += len;
 		}
-
-		/* 7. counters (scalar: ballot + popcount) */
-		cnt_frames += __popcll(__ballot(active));
+		/* IPv4 header sum, check word (r6 low half) excluded */
+		const uint64_t s3 = (uint64_t)(r3 & 0xffff0000u) + r4 + r5 +
+				    (r6 & 0xffff0000u) + r7 + (r8 & 0xffffu);
+		const uint32_t c3 = r6 & 0xffff;
+		const uint32_t l3c = ~fold16(s3) & 0xffff;
+		const bool l3_ok = fold16(s3 + c3) == 0xffff;
+		const uint32_t c4 = udp ? (r10 & 0xffff) : (r12 >> 16);
+		/* L4 window sum over [34, end) in the shifted frame, check word
+		 * excluded; udp_csum's odd-length over-read byte included;
+		 * pseudo header folded in */
+		const uint32_t over = cl & 1;
+		const int32_t e = (int32_t)(34 + cl + over) <
+				  (int32_t)(WIN - 4 * nv) ?
+				  (int32_t)(34 + cl + over) : (int32_t)(WIN - 4 * nv);
+		uint64_t s4 = (uint64_t)(r8 & 0xffff0000u) + sa + da +
+			      ((uint64_t)(proto + cl) << 8);
 #pragma unroll
-		for (int v = 0; v < 5; v++)
-			cnt_v[v] += __popcll(__ballot(active && verdict == (uint32_t)v));
-		cnt_l3 += __popcll(__ballot(rec_live && l3_bad));
-		cnt_l4 += __popcll(__ballot(rec_live && l4_bad));
-		cnt_abs += __popcll(__ballot(rec_live && absent));
-		cnt_frag += __popcll(__ballot(rec_live && L.frag));
-		my_bytes += active ? len : 0;
+		for (int j = 9; j < WIN / 4; j++) {
+			uint32_t m = first_bytes(e - 4 * j);
+			if (j == 10)
+				m &= udp ? 0xffff0000u : 0xffffffffu;
+			if (j == 12)
+				m &= udp ? 0xffffffffu : 0x0000ffffu;
+			s4 += r[j] & m;
+		}
+		const uint32_t sum4 = fold16(s4);
+		const uint32_t rhi = l4 + cl + over;      /* frame relative */
+		const uint32_t ext = ext_sums<WIN>(a, fast && rhi > (uint32_t)WIN,
+						   eff, l4, rhi, udp ? l4 + 6 : l4 + 16,
+						   c4, lane);
+		const uint64_t body = (uint64_t)sum4 + ext;
+		const uint32_t l4c = ~fold16(body) & 0xffff;
+		const bool absent = udp && c4 == 0;
+		const bool l4_ok = absent || (~fold16(body + c4) & 0xffff) == 0;
+		const bool drop = (a.flags & XDPGPU_CFG_VERIFY_CSUM) && (!l3_ok || !l4_ok);
+		if (fast) {
+			uint4 rec;
+			rec.x = hash;
+			rec.y = l3c | (l4c << 16);
+			rec.z = XDPGPU_F_IP | XDPGPU_F_L4 | (nv ? XDPGPU_F_VLAN : 0u) |
+				(l3_ok ? XDPGPU_F_L3_OK : 0u) |
+				(l4_ok ? XDPGPU_F_L4_OK : 0u) |
+				(absent ? XDPGPU_F_L4_ABSENT : 0u) |
+				(proto << 8) | (l3 << 16) | (nv << 24);
+			rec.w = l4 | (cl << 16);
+			a.verdict[i] = (uint8_t)(drop ? XDPGPU_DROP : XDPGPU_REDIRECT);
+			if (a.res)
+				*reinterpret_cast<uint4 *>(a.res + i) = rec;
+		}
+		if (a.stats) {
+			cnt[CNT_FRAMES] += __popcll(__ballot(fast));
+			cnt[CNT_VERDICT0 + XDPGPU_DROP] += __popcll(__ballot(fast && drop));
+			cnt[CNT_VERDICT0 + XDPGPU_REDIRECT] += __popcll(__ballot(fast && !drop));
+			cnt[CNT_L3_BAD] += __popcll(__ballot(fast && !l3_ok));
+			cnt[CNT_L4_BAD] += __popcll(__ballot(fast && !l4_ok));
+			cnt[CNT_L4_ABSENT] += __popcll(__ballot(fast && absent));
+		}
 	}
+	__builtin_amdgcn_wave_barrier();
+	if ((uint32_t)lane < xq_n)
+		xl[xout + lane] = xq[lane];
+	if (lane == 0 && a.xcount)
+		a.xcount[wgid] = xout + xq_n;
 
 	if (a.stats) {
 		const uint64_t bytes = wave_sum64(my_bytes);
 		if (lane == 0) {
-			atomicAdd(&blk_cnt[CNT_FRAMES], (unsigned long long)cnt_frames);
 			atomicAdd(&blk_cnt[CNT_BYTES], (unsigned long long)bytes);
 #pragma unroll
-			for (int v = 0; v < 5; v++)
-				atomicAdd(&blk_cnt[CNT_VERDICT0 + v],
-					  (unsigned long long)cnt_v[v]);
-			atomicAdd(&blk_cnt[CNT_L3_BAD], (unsigned long long)cnt_l3);
-			atomicAdd(&blk_cnt[CNT_L4_BAD], (unsigned long long)cnt_l4);
-			atomicAdd(&blk_cnt[CNT_L4_ABSENT], (unsigned long long)cnt_abs);
-			atomicAdd(&blk_cnt[CNT_FRAG], (unsigned long long)cnt_frag);
+			for (int k = 0; k <= CNT_FRAG; k++)
+				if (k != CNT_BYTES)
+					atomicAdd(&blk_cnt[k], (unsigned long long)cnt[k]);
 		}
 		__syncthreads();
 		if (threadIdx.x < CNT_SLOT)
 			a.stats[(uint64_t)blockIdx.x * CNT_SLOT + threadIdx.x] +=
 				blk_cnt[threadIdx.x];
 	}
+}
+
+
+/* Exception kernel: the generic pipeline on the frames the fast kernel
+ * deferred, one wave per fast-kernel wave region, 64 frames per batch. */
+template <int WIN>
+__global__ __launch_bounds__(kBlock) void xdp_rx_generic_kernel(RxArgs a)
+{
+	constexpr int SDW = WIN / 4 + 1;
+	__shared__ uint32_t lds[kWavesPerBlock * kWave * SDW + 8];
+	__shared__ uint64_t dtab_all[kWavesPerBlock * kWave];
+	__shared__ unsigned long long blk_cnt[CNT_SLOT];
+
+	const int lane = threadIdx.x & (kWave - 1);
+	const int wid = threadIdx.x / kWave;
+	uint32_t *win = lds + wid * kWave * SDW;
+	uint64_t *dtab = dtab_all + wid * kWave;
+	if (threadIdx.x < CNT_SLOT)
+		blk_cnt[threadIdx.x] = 0;
+	__syncthreads();
+
+	const uint64_t wgid = (uint64_t)blockIdx.x * kWavesPerBlock + wid;
+	const uint32_t count = a.xcount[wgid];
+	const uint32_t *xl = a.xlist + wgid * a.xregion;
+	uint32_t cnt[CNT_FRAG + 1] = {};
+	uint64_t my_bytes = 0;
+	for (uint32_t b = 0; b < count; b += kWave) {
+		const bool act = b + lane < count;
+		const uint64_t i = act ? xl[b + lane] : 0;
+		generic_batch<WIN>(a, win, dtab, lane, i, act, cnt, my_bytes);
+	}
+
+	if (a.stats) {
+		const uint64_t bytes = wave_sum64(my_bytes);
+		if (lane == 0) {
+			atomicAdd(&blk_cnt[CNT_BYTES], (unsigned long long)bytes);
+#pragma unroll
+			for (int k = 0; k <= CNT_FRAG; k++)
+				if (k != CNT_BYTES)
+					atomicAdd(&blk_cnt[k], (unsigned long long)cnt[k]);
+		}
+		__syncthreads();
+		if (threadIdx.x < CNT_SLOT)
+			a.stats[(uint64_t)blockIdx.x * CNT_SLOT + threadIdx.x] +=
+				blk_cnt[threadIdx.x];
+	}
+}
+
+/* Memory ceiling for the RX traffic pattern (diagnostic): the same
+ * descriptor, transposed 64-byte window loads and 33 bytes of stores per
+ * frame, with no parse.  Its bandwidth is what the RX kernel can approach. */
+__global__ __launch_bounds__(kBlock) void xdp_ceiling_kernel(RxArgs a)
+{
+	__shared__ uint64_t dtab_all[kWavesPerBlock * kWave];
+	const int lane = threadIdx.x & (kWave - 1);
+	const int wid = threadIdx.x / kWave;
+	uint64_t *dtab = dtab_all + wid * kWave;
+	const uint64_t ntiles = ((uint64_t)a.n + kWave - 1) / kWave;
+	const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+	for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + wid; t < ntiles;
+	     t += nwaves) {
+		const uint64_t i = t * kWave + lane;
+		const uint4 dv = load_desc(a.desc, i, a.n);
+		dtab[lane] = ((uint64_t)dv.y << 32) | dv.x;
+		__builtin_amdgcn_wave_barrier();
+		uint32_t x = dv.z;
+#pragma unroll
+		for (int k = 0; k < 4; k++) {
+			const int q = k * kWave + lane;
+			const uint64_t src = dtab[q >> 2] + 16ull * (q & 3);
+			if (src + 16 <= a.usize) {
+				uint4 v = *reinterpret_cast<const uint4 *>(a.umem + src);
+				x ^= v.x ^ v.y ^ v.z ^ v.w;
+			}
+		}
+		if (i < a.n) {
+			a.verdict[i] = (uint8_t)x;
+			*reinterpret_cast<uint4 *>(a.res + i) = make_uint4(x, x, x, x);
+			*reinterpret_cast<uint4 *>(a.tup + 16 * i) = make_uint4(x, 0, x, 0);
+		}
+	}
+}
+
+hipError_t launch_ceiling(const RxArgs &a, uint32_t blocks, hipStream_t stream)
+{
+	hipLaunchKernelGGL(xdp_ceiling_kernel, dim3(blocks), dim3(kBlock), 0,
+			   stream, a);
+	return hipGetLastError();
 }
 
 uint32_t rx_grid_blocks(uint32_t n, uint32_t max_blocks)
@@ -770,16 +1247,76 @@ uint32_t rx_grid_blocks(uint32_t n, uint32_t max_blocks)
 	return (uint32_t)blocks;
 }
 
-hipError_t launch_rx(const RxArgs &a, uint32_t window, uint32_t blocks,
-		     hipStream_t stream)
+/* Kernel variants selectable by cfg.tune (diagnostic A/B): bits 0-7 =
+ * waves per SIMD the register allocator is held to (0 = compiler's
+ * choice), bit 8 = software-pipelined window loads. */
+template <int WIN, int MINW, bool PF>
+static uint32_t resident_blocks()
 {
-	if (window == 128)
-		hipLaunchKernelGGL(xdp_rx_kernel<128>, dim3(blocks), dim3(kBlock),
-				   0, stream, a);
-	else
-		hipLaunchKernelGGL(xdp_rx_kernel<64>, dim3(blocks), dim3(kBlock),
-				   0, stream, a);
+	static uint32_t cached = 0;
+	if (!cached) {
+		int per_cu = 0, dev = 0;
+		hipDeviceProp_t prop;
+		if (hipGetDevice(&dev) != hipSuccess ||
+		    hipGetDeviceProperties(&prop, dev) != hipSuccess ||
+		    hipOccupancyMaxActiveBlocksPerMultiprocessor(
+			    &per_cu, xdp_rx_kernel<WIN, MINW, PF>, kBlock, 0) != hipSuccess ||
+		    per_cu <= 0)
+			return kMaxRxBlocks;
+		cached = (uint32_t)per_cu * (uint32_t)prop.multiProcessorCount;
+	}
+	return cached;
+}
+
+/* Launch the fast kernel on a grid of resident blocks (no partial second
+ * round), then the exception kernel on the same grid.  a.xlist must hold
+ * rx_xlist_entries(a.n, blocks) entries. */
+template <int WIN, int MINW, bool PF>
+static hipError_t launch_sized(RxArgs a, uint32_t max_blocks,
+			       hipStream_t stream)
+{
+	uint32_t cap = resident_blocks<WIN, MINW, PF>();
+	if (cap < max_blocks)
+		max_blocks = cap;
+	const uint32_t blocks = rx_grid_blocks(a.n, max_blocks);
+	a.xregion = rx_xregion(a.n, blocks);
+	hipLaunchKernelGGL((xdp_rx_kernel<WIN, MINW, PF>), dim3(blocks),
+			   dim3(kBlock), 0, stream, a);
+	hipError_t e = hipGetLastError();
+	if (e != hipSuccess)
+		return e;
+	hipLaunchKernelGGL((xdp_rx_generic_kernel<WIN>), dim3(blocks),
+			   dim3(kBlock), 0, stream, a);
 	return hipGetLastError();
+}
+
+uint32_t rx_xregion(uint32_t n, uint32_t blocks)
+{
+	const uint64_t ntiles = ((uint64_t)n + kWave - 1) / kWave;
+	const uint64_t nwaves = (uint64_t)blocks * kWavesPerBlock;
+	return (uint32_t)(((ntiles + nwaves - 1) / nwaves) * kWave);
+}
+
+hipError_t launch_rx(const RxArgs &a, uint32_t window, uint32_t max_blocks,
+		     hipStream_t stream, uint32_t tune)
+{
+	const uint32_t waves = tune & 0xff;
+	const bool pf = (tune >> 8) & 1;
+	if (window == 128) {
+		if (pf)
+			return launch_sized<128, 1, true>(a, max_blocks, stream);
+		return launch_sized<128, 1, false>(a, max_blocks, stream);
+	}
+	if (pf) {
+		if (waves == 6)
+			return launch_sized<64, 6, true>(a, max_blocks, stream);
+		return launch_sized<64, 1, true>(a, max_blocks, stream);
+	}
+	if (waves == 6)
+		return launch_sized<64, 6, false>(a, max_blocks, stream);
+	if (waves == 8)
+		return launch_sized<64, 8, false>(a, max_blocks, stream);
+	return launch_sized<64, 1, false>(a, max_blocks, stream);
 }
 
 /* ------------------------------------------------------------------ */

@@ -37,6 +37,9 @@ struct Slot {
 	uint8_t *d_verdict = nullptr;
 	xdpgpu_result *d_res = nullptr;
 	uint8_t *d_tup = nullptr;
+	uint32_t *d_xlist = nullptr;  /* exception list (fast -> generic kernel) */
+	uint64_t xcap = 0;
+	uint32_t *d_xcount = nullptr;
 	bool busy = false;
 	/* pending host copies for xdpgpu_wait() */
 	uint32_t n = 0;
@@ -113,6 +116,10 @@ static void free_slot(Slot &s)
 		(void)hipFree(s.d_res);
 	if (s.d_tup)
 		(void)hipFree(s.d_tup);
+	if (s.d_xlist)
+		(void)hipFree(s.d_xlist);
+	if (s.d_xcount)
+		(void)hipFree(s.d_xcount);
 	if (s.done)
 		(void)hipEventDestroy(s.done);
 	if (s.stream)
@@ -243,12 +250,38 @@ static int ensure_slot_buffers(xdpgpu_ctx *ctx, Slot &s, uint32_t n)
 	return 0;
 }
 
-static int enqueue_rx(xdpgpu_ctx *ctx, uint8_t *d_umem, uint64_t usize,
-		      const xdpgpu_desc *d_desc, uint32_t n, uint8_t *d_verdict,
-		      xdpgpu_result *d_res, uint8_t *d_tup,
-		      unsigned long long *d_stats, hipStream_t stream)
+/* Exception-list scratch for a launch of n frames (any grid up to
+ * kMaxRxBlocks): per-wave regions of whole tiles. */
+static int ensure_xlist(xdpgpu_ctx *ctx, Slot &s, uint32_t n)
 {
+	const uint64_t need = (uint64_t)n + 64ull * 4 * kMaxRxBlocks + 64;
+	if (!s.d_xcount &&
+	    hipMalloc(&s.d_xcount, (size_t)kMaxRxBlocks * 4 * sizeof(uint32_t)) != hipSuccess)
+		return set_err(ctx, -ENOMEM, "exception counts");
+	if (s.xcap >= need)
+		return 0;
+	if (s.d_xlist) {
+		(void)hipDeviceSynchronize();
+		(void)hipFree(s.d_xlist);
+		s.d_xlist = nullptr;
+		s.xcap = 0;
+	}
+	if (hipMalloc(&s.d_xlist, need * sizeof(uint32_t)) != hipSuccess)
+		return set_err(ctx, -ENOMEM, "exception list of %llu entries",
+			       (unsigned long long)need);
+	s.xcap = need;
+	return 0;
+}
+
+static int enqueue_rx(xdpgpu_ctx *ctx, Slot &s, uint8_t *d_umem, uint64_t usize,
+		      const xdpgpu_desc *d_desc, uint32_t n, uint8_t *d_verdict,
+		      xdpgpu_result *d_res, uint8_t *d_tup, hipStream_t stream)
+{
+	int rc = ensure_xlist(ctx, s, n);
+	if (rc)
+		return rc;
 	RxArgs a;
+	memset(&a, 0, sizeof(a));
 	a.umem = d_umem;
 	a.usize = usize;
 	a.desc = d_desc;
@@ -259,9 +292,12 @@ static int enqueue_rx(xdpgpu_ctx *ctx, uint8_t *d_umem, uint64_t usize,
 	a.tup = d_tup;
 	a.flags = ctx->cfg.flags;
 	a.initval = ctx->cfg.jhash_initval;
-	a.stats = (ctx->cfg.flags & XDPGPU_CFG_STATS) ? d_stats : nullptr;
-	uint32_t blocks = rx_grid_blocks(n, ctx->max_blocks);
-	HIP_TRY(ctx, launch_rx(a, ctx->cfg.window, blocks, stream));
+	a.stats = (ctx->cfg.flags & XDPGPU_CFG_STATS) ? s.d_stats : nullptr;
+	a.xlist = s.d_xlist;
+	a.xcount = s.d_xcount;
+	a.force_generic = (ctx->cfg.tune >> 9) & 1;
+	HIP_TRY(ctx, launch_rx(a, ctx->cfg.window, ctx->max_blocks, stream,
+			       ctx->cfg.tune));
 	return 0;
 }
 
@@ -275,9 +311,30 @@ int xdpgpu_process_dev(xdpgpu_ctx *ctx, void *d_umem, uint64_t umem_size,
 	if (n == 0)
 		return 0;
 	hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
-	return enqueue_rx(ctx, (uint8_t *)d_umem, umem_size, d_descs, n,
-			  d_verdict, d_res, (uint8_t *)d_tuples,
-			  ctx->slot[0].d_stats, st);
+	return enqueue_rx(ctx, ctx->slot[0], (uint8_t *)d_umem, umem_size,
+			  d_descs, n, d_verdict, d_res, (uint8_t *)d_tuples, st);
+}
+
+int xdpgpu_ceiling_dev(xdpgpu_ctx *ctx, const void *d_umem, uint64_t umem_size,
+		       const xdpgpu_desc *d_descs, uint32_t n, uint8_t *d_verdict,
+		       void *d_res, void *d_tuples, void *stream)
+{
+	if (!ctx || !d_umem || !d_descs || !d_verdict || !d_res || !d_tuples)
+		return -EINVAL;
+	if (n == 0)
+		return 0;
+	RxArgs a;
+	memset(&a, 0, sizeof(a));
+	a.umem = (uint8_t *)d_umem;
+	a.usize = umem_size;
+	a.desc = d_descs;
+	a.n = n;
+	a.verdict = d_verdict;
+	a.res = (xdpgpu_result *)d_res;
+	a.tup = (uint8_t *)d_tuples;
+	hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
+	HIP_TRY(ctx, launch_ceiling(a, rx_grid_blocks(n, ctx->max_blocks), st));
+	return 0;
 }
 
 int xdpgpu_submit(xdpgpu_ctx *ctx, uint32_t slot, const xdpgpu_desc *descs,
@@ -333,8 +390,8 @@ int xdpgpu_submit(xdpgpu_ctx *ctx, uint32_t slot, const xdpgpu_desc *descs,
 	HIP_TRY(ctx, hipMemcpyAsync(s.d_desc, descs, (size_t)n * sizeof(*descs),
 				    hipMemcpyHostToDevice, s.stream));
 	uint8_t *d_tup = (tuples && ctx->cfg.tuple_fmt) ? s.d_tup : nullptr;
-	rc = enqueue_rx(ctx, kumem, ctx->umem_size, s.d_desc, n, s.d_verdict,
-			res ? s.d_res : nullptr, d_tup, s.d_stats, s.stream);
+	rc = enqueue_rx(ctx, s, kumem, ctx->umem_size, s.d_desc, n, s.d_verdict,
+			res ? s.d_res : nullptr, d_tup, s.stream);
 	if (rc)
 		return rc;
 	HIP_TRY(ctx, hipMemcpyAsync(verdict, s.d_verdict, n,

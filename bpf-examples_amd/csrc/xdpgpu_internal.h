@@ -38,11 +38,17 @@ struct RxArgs {
 	uint32_t flags;
 	uint32_t initval;
 	unsigned long long *stats; /* [kMaxRxBlocks][CNT_SLOT] or null */
+	uint32_t *xlist;           /* deferred-frame list, xregion per wave */
+	uint32_t *xcount;          /* deferred frames per wave              */
+	uint32_t xregion;          /* set by the launcher                   */
+	uint32_t force_generic;    /* 1: defer every frame (diagnostic)     */
 };
 
-hipError_t launch_rx(const RxArgs &a, uint32_t window, uint32_t blocks,
-		     hipStream_t stream);
+hipError_t launch_rx(const RxArgs &a, uint32_t window, uint32_t max_blocks,
+		     hipStream_t stream, uint32_t tune);
 uint32_t rx_grid_blocks(uint32_t n, uint32_t max_blocks);
+uint32_t rx_xregion(uint32_t n, uint32_t blocks);
+hipError_t launch_ceiling(const RxArgs &a, uint32_t blocks, hipStream_t stream);
 
 hipError_t launch_jhash(const uint8_t *keys, uint32_t key_len,
 			uint32_t stride, uint32_t n, uint32_t initval,

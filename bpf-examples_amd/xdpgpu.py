@@ -74,7 +74,7 @@ class Cfg(C.Structure):
     _fields_ = [("device", C.c_int32), ("flags", C.c_uint32),
                 ("max_batch", C.c_uint32), ("jhash_initval", C.c_uint32),
                 ("tuple_fmt", C.c_uint32), ("window", C.c_uint32),
-                ("rsvd", C.c_uint32 * 2)]
+                ("tune", C.c_uint32), ("rsvd", C.c_uint32)]
 
 
 class Stats(C.Structure):
@@ -115,7 +115,7 @@ EXPORTS = (
     "xdpgpu_init", "xdpgpu_fini", "xdpgpu_register_umem", "xdpgpu_process",
     "xdpgpu_submit", "xdpgpu_wait", "xdpgpu_process_dev", "xdpgpu_stats",
     "xdpgpu_stats_reset", "xdpgpu_jhash_dev", "xdpgpu_ip_fast_csum_dev",
-    "xdpgpu_sync", "xdpgpu_device_count", "xdpgpu_last_error",
+    "xdpgpu_sync", "xdpgpu_ceiling_dev", "xdpgpu_device_count", "xdpgpu_last_error",
     "xdpgpu_abi_version", "xdpgpu_pool_size", "xdpgpu_pool_generate",
     "xdpgpu_pool_spec_default",
 )
@@ -144,6 +144,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.xdpgpu_jhash_dev.argtypes = [vp, vp, u32, u32, u32, u32, vp, vp]
     lib.xdpgpu_ip_fast_csum_dev.argtypes = [vp, vp, u32, u32, vp, vp]
     lib.xdpgpu_sync.argtypes = [vp, vp]
+    lib.xdpgpu_ceiling_dev.argtypes = [vp, vp, u64, vp, u32, vp, vp, vp, vp]
     lib.xdpgpu_device_count.argtypes = []
     lib.xdpgpu_last_error.argtypes = [vp]
     lib.xdpgpu_last_error.restype = C.c_char_p
@@ -186,11 +187,11 @@ class XdpGpu:
 
     def __init__(self, device: int = 0, flags: int = CFG_DEFAULT,
                  initval: int = 0, tuple_fmt: int = TUPLE_V4,
-                 window: int = 64, max_batch: int = 0):
+                 window: int = 64, max_batch: int = 0, tune: int = 0):
         self.lib = load_library()
         cfg = Cfg(device=device, flags=flags, max_batch=max_batch,
                   jhash_initval=initval & 0xffffffff, tuple_fmt=tuple_fmt,
-                  window=window)
+                  window=window, tune=tune)
         h = C.c_void_p()
         rc = self.lib.xdpgpu_init(C.byref(cfg), C.byref(h))
         if rc:
@@ -267,6 +268,13 @@ class XdpGpu:
         self._check(self.lib.xdpgpu_process_dev(
             self.h, _ptr(umem), umem_size, _ptr(descs), n, _ptr(verdict),
             _ptr(res), _ptr(tup), _stream_handle(stream)), "xdpgpu_process_dev")
+
+    def ceiling_dev(self, umem, umem_size: int, descs, n: int, verdict, res,
+                    tup, stream=None) -> None:
+        """Diagnostic memory-ceiling kernel (same traffic, no parse)."""
+        self._check(self.lib.xdpgpu_ceiling_dev(
+            self.h, _ptr(umem), umem_size, _ptr(descs), n, _ptr(verdict),
+            _ptr(res), _ptr(tup), _stream_handle(stream)), "xdpgpu_ceiling_dev")
 
     def jhash_dev(self, keys, key_len: int, key_stride: int, n: int,
                   initval: int, out, stream=None) -> None:

@@ -121,7 +121,10 @@ struct xdpgpu_cfg {
 	uint32_t jhash_initval; /* initval of jhash (CLI option, default 0)    */
 	uint32_t tuple_fmt;     /* XDPGPU_TUPLE_*                              */
 	uint32_t window;        /* header bytes staged in LDS: 64 or 128 (0: 64) */
-	uint32_t rsvd[2];
+	uint32_t tune;          /* kernel variant (diagnostic): bits 0-7 waves per
+				 * SIMD, bit 8 pipelined loads, bit 9 generic
+				 * path only; 0 = default */
+	uint32_t rsvd;
 };
 
 /* UMEM registration flags (headers/linux/if_xdp.h:31) */
@@ -194,6 +197,15 @@ int xdpgpu_jhash_dev(struct xdpgpu_ctx *ctx, const void *d_keys,
 int xdpgpu_ip_fast_csum_dev(struct xdpgpu_ctx *ctx, const void *d_hdrs,
 			    uint32_t hdr_stride, uint32_t n, uint16_t *d_out,
 			    void *stream);
+
+/* Diagnostic: the RX kernel's memory traffic (descriptor, 64-byte header
+ * window, 16 B result + 16 B tuple + verdict stores) with no parse, to
+ * measure the achievable bandwidth ceiling of that access pattern.  Outputs
+ * are meaningless. */
+int xdpgpu_ceiling_dev(struct xdpgpu_ctx *ctx, const void *d_umem,
+		       uint64_t umem_size, const struct xdpgpu_desc *d_descs,
+		       uint32_t n, uint8_t *d_verdict, void *d_res,
+		       void *d_tuples, void *stream);
 
 /* Wait for all work of the context (or of stream if non-NULL). */
 int xdpgpu_sync(struct xdpgpu_ctx *ctx, void *stream);

@@ -27,10 +27,15 @@ def to_dev(a: np.ndarray, pad: int = 64):
     return t
 
 
-def run_dev(umem, descs, flags=0x5, initval=0, fmt=1, window=64):
+# kernel variants (cfg.tune): default fast+exception kernels, every frame
+# through the generic kernel, software-pipelined window loads
+TUNES = [0, 512, 256]
+
+
+def run_dev(umem, descs, flags=0x5, initval=0, fmt=1, window=64, tune=0):
     """Device-resident path; returns verdict, res, tuples, umem after, stats."""
     n = len(descs)
-    ctx = xdpgpu.XdpGpu(0, flags | xdpgpu.CFG_STATS, initval, fmt, window)
+    ctx = xdpgpu.XdpGpu(0, flags | xdpgpu.CFG_STATS, initval, fmt, window, tune=tune)
     d_umem = to_dev(umem)
     d_desc = to_dev(np.ascontiguousarray(descs, xdpgpu.DESC_DTYPE), 16)
     d_v = torch.full((max(n, 1),), 0xEE, dtype=torch.uint8, device="cuda:0")
@@ -75,13 +80,14 @@ def oracle_stats_match(st, ost):
 
 
 # ---------------------------------------------------------------- golden
+@pytest.mark.parametrize("tune", TUNES)
 @pytest.mark.parametrize("window", [64, 128])
 @pytest.mark.parametrize("cfg", ["verify", "echo_net", "noverify"])
-def test_golden_fixtures_device(dev, golden, cfg, window):
+def test_golden_fixtures_device(dev, golden, cfg, window, tune):
     fx, meta = golden
     flags, iv, fmt = meta["cfgs"][cfg]
     descs = fx["descs"].view(xdpgpu.DESC_DTYPE)
-    v, res, tup, um, st = run_dev(fx["umem"], descs, flags, iv, fmt, window)
+    v, res, tup, um, st = run_dev(fx["umem"], descs, flags, iv, fmt, window, tune)
     want = (fx[f"{cfg}_verdict"], fx[f"{cfg}_res"].view(xdpgpu.RESULT_DTYPE),
             fx[f"{cfg}_tup"], fx[f"{cfg}_umem_after"])
     assert_same((v, res, tup, um), want, f"golden/{cfg}/w{window}")
@@ -117,14 +123,15 @@ POOLS = [
 ]
 
 
+@pytest.mark.parametrize("tune", TUNES)
 @pytest.mark.parametrize("window", [64, 128])
 @pytest.mark.parametrize("name,kind,size,seed,n,kw", POOLS, ids=[p[0] for p in POOLS])
-def test_pool_vs_oracle(dev, name, kind, size, seed, n, kw, window):
+def test_pool_vs_oracle(dev, name, kind, size, seed, n, kw, window, tune):
     umem, descs, expect = xdpgpu.pool_generate(n, kind, size, seed, **kw)
     for flags, iv, fmt in ((0x5, 0, 1), (0x7, 0x9E3779B9, 2)):
         ou = umem.copy()
         ov, ores, otup, ost = oracle.process(ou, descs, flags, iv, fmt)
-        v, res, tup, um, st = run_dev(umem, descs, flags, iv, fmt, window)
+        v, res, tup, um, st = run_dev(umem, descs, flags, iv, fmt, window, tune)
         assert_same((v, res, tup, um), (ov, ores, otup, ou), f"{name}/w{window}/{flags:#x}")
         oracle_stats_match(st, ost)
         if flags == 0x5:

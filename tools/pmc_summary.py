@@ -1,0 +1,44 @@
+#!/usr/bin/env python3
+# SPDX-License-Identifier: GPL-2.0
+"""Summarise rocprofv3 --pmc passes (tools/pmc_profile.sh) per kernel:
+average counter value per dispatch.  HBM traffic per launch is
+2 * FETCH_SIZE + WRITE_SIZE (KiB -> bytes): on gfx950 FETCH_SIZE reads half
+the bytes of a wide coalesced stream (MI355X_MICROARCH.md §HBM)."""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def main(out):
+    acc = defaultdict(lambda: defaultdict(list))
+    for f in glob.glob(os.path.join(out, "p*", "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                k = row.get("Kernel_Name", "?")
+                if "xdp_" not in k:
+                    continue
+                name = row.get("Counter_Name")
+                val = float(row.get("Counter_Value", 0))
+                disp = row.get("Dispatch_Id")
+                acc[k][name].append((disp, val))
+    summary = {}
+    for k, ctrs in acc.items():
+        s = {}
+        for name, vals in ctrs.items():
+            per = defaultdict(float)
+            for d, v in vals:
+                per[d] += v
+            s[name] = sum(per.values()) / max(len(per), 1)
+        if "FETCH_SIZE" in s and "WRITE_SIZE" in s:
+            s["hbm_bytes_per_launch"] = (2 * s["FETCH_SIZE"] + s["WRITE_SIZE"]) * 1024
+        summary[k] = s
+    print(json.dumps(summary, indent=1))
+    with open(os.path.join(out, "summary.json"), "w") as fh:
+        json.dump(summary, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc")
