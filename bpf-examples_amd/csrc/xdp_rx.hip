@@ -610,45 +610,75 @@ __device__ __forceinline__ uint32_t ext_sums(const RxArgs &a, bool need,
 					     uint32_t rhi, uint32_t chk,
 					     uint32_t c4, int lane)
 {
+	constexpr int G = 4;   /* frames whose 1 KiB steps are in flight together */
 	uint64_t mask = __ballot(need);
 	uint32_t out = 0;
 	while (mask) {
-		const int src = __builtin_ctzll(mask);
-		mask &= mask - 1;
-		const uint64_t seff =
-			((uint64_t)readlane32((uint32_t)(eff >> 32), src) << 32) |
-			readlane32((uint32_t)eff, src);
-		const uint32_t sl4 = readlane32(l4, src);
-		const uint32_t srhi = readlane32(rhi, src);
-		const uint32_t schk = readlane32(chk, src);
-		const uint64_t lo = seff + (sl4 > (uint32_t)WIN ? sl4 : (uint32_t)WIN);
-		const uint64_t hi = seff + srhi;
-		const uint64_t lim = hi < a.usize ? hi : a.usize;
-		uint32_t acc = 0;
-		for (uint64_t p = (lo & ~15ull) + 16ull * lane; p < lim;
-		     p += 16ull * kWave) {
-			uint4 v = *reinterpret_cast<const uint4 *>(a.umem + p);
-			if (p < lo || p + 16 > lim) {
-				const uint4 m = chunk_keep(p, lo, lim);
-				v.x &= m.x;
-				v.y &= m.y;
-				v.z &= m.z;
-				v.w &= m.w;
+		int src[G];
+		uint64_t lo[G], lim[G], seff[G];
+		uint32_t acc[G];
+		int nf = 0;
+		uint64_t steps = 0;   /* 1 KiB steps of the longest frame */
+#pragma unroll
+		for (int k = 0; k < G; k++) {
+			src[k] = 0;
+			lo[k] = lim[k] = seff[k] = 0;
+			acc[k] = 0;
+			if (mask) {
+				const int sl = __builtin_ctzll(mask);
+				mask &= mask - 1;
+				src[k] = sl;
+				seff[k] = ((uint64_t)readlane32((uint32_t)(eff >> 32), sl) << 32) |
+					  readlane32((uint32_t)eff, sl);
+				const uint32_t sl4 = readlane32(l4, sl);
+				const uint64_t hi = seff[k] + readlane32(rhi, sl);
+				lo[k] = seff[k] + (sl4 > (uint32_t)WIN ? sl4 : (uint32_t)WIN);
+				lim[k] = hi < a.usize ? hi : a.usize;
+				const uint64_t st = (lim[k] - (lo[k] & ~15ull) + 1023) / 1024;
+				steps = st > steps ? st : steps;
+				nf = k + 1;
 			}
-			acc += halves(v.x) + halves(v.y) + halves(v.z) + halves(v.w);
 		}
-		/* exact: the range is at most 64 KiB, so the raw sum of 16-bit
-		 * halves fits 32 bits */
-		acc = wave_sum32(acc);
-		if (schk >= (uint32_t)WIN) {
-			const uint32_t c = readlane32(c4, src);
-			acc -= (seff & 1) ? bswap16(c) : c;
+		for (uint64_t s = 0; s < steps; s++) {
+			uint4 v[G];
+			uint64_t p[G];
+#pragma unroll
+			for (int k = 0; k < G; k++) {
+				p[k] = (lo[k] & ~15ull) + 1024 * s + 16ull * lane;
+				v[k] = make_uint4(0, 0, 0, 0);
+				if (k < nf && p[k] < lim[k])
+					v[k] = *reinterpret_cast<const uint4 *>(a.umem + p[k]);
+			}
+#pragma unroll
+			for (int k = 0; k < G; k++) {
+				if (p[k] < lo[k] || p[k] + 16 > lim[k]) {
+					const uint4 m = chunk_keep(p[k], lo[k], lim[k]);
+					v[k].x &= m.x;
+					v[k].y &= m.y;
+					v[k].z &= m.z;
+					v[k].w &= m.w;
+				}
+				acc[k] += halves(v[k].x) + halves(v[k].y) +
+					  halves(v[k].z) + halves(v[k].w);
+			}
 		}
-		uint32_t s = fold16(acc);
-		if (seff & 1)        /* absolute vs frame-relative parity */
-			s = bswap16(s);
-		if (lane == src)
-			out = s;
+#pragma unroll
+		for (int k = 0; k < G; k++) {
+			if (k >= nf)
+				break;
+			/* exact: a range is at most 64 KiB, so the raw sum of
+			 * 16-bit halves fits 32 bits */
+			uint32_t t = wave_sum32(acc[k]);
+			if (readlane32(chk, src[k]) >= (uint32_t)WIN) {
+				const uint32_t c = readlane32(c4, src[k]);
+				t -= (seff[k] & 1) ? bswap16(c) : c;
+			}
+			uint32_t f = fold16(t);
+			if (seff[k] & 1)     /* absolute vs frame-relative parity */
+				f = bswap16(f);
+			if (lane == src[k])
+				out = f;
+		}
 	}
 	return out;
 }
@@ -902,19 +932,44 @@ __device__ __forceinline__ uint32_t first_bytes(int32_t nb)
 	return nb ? (0xffffffffu >> ((32 - 8 * nb) & 31)) : 0u;
 }
 
-template <int WIN, int MINW, bool PF>
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+/* non-temporal 16-byte store (streamed outputs, written once) */
+typedef unsigned int v4u_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_nt16(void *p, uint4 r)
+{
+	v4u_t v = {r.x, r.y, r.z, r.w};
+	__builtin_nontemporal_store(v, reinterpret_cast<v4u_t *>(p));
+}
+
+/*
+ * Fast kernel, 64-byte header windows staged by LDS-DMA.
+ *
+ * Per wave and tile of 64 frames: the 256 16-byte chunks of the windows go
+ * straight from HBM into LDS with four global_load_lds_dwordx4 (nt); in
+ * load k lane l fetches chunk c of frame f = 16k + l/4, and slot 64k + l of
+ * the tile buffer receives it, with c = (l & 3) ^ ((f >> 2) & 3): frame f's
+ * chunk c then sits in slot 4f + (c ^ ((f >> 2) & 3)), which makes the four
+ * ds_read_b128 each lane issues for its own frame bank-conflict free.  The
+ * DMA of tile t+1 is issued as soon as tile t is in registers, so it runs
+ * under tile t's parse.  Descriptors are prefetched two tiles ahead.
+ *
+ * Frames of the fast shape (Ethernet + 0..2 VLAN tags + IPv4 ihl 5, not a
+ * fragment, + UDP/TCP whose checksum range lies in the window) are finished
+ * here; every other frame is deferred to the exception kernel.
+ */
+template <int MINW>
 __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 {
-	constexpr int SDW = WIN / 4 + 1;   /* LDS row stride in dwords */
-	constexpr int XQ = 2 * kWave;      /* exception queue per wave  */
-	__shared__ uint32_t lds[kWavesPerBlock * kWave * SDW + 8];
+	constexpr int XQ = 2 * kWave;      /* exception queue per wave */
+	__shared__ uint4 buf_all[kWavesPerBlock * 4 * kWave];
 	__shared__ uint64_t dtab_all[kWavesPerBlock * kWave];
 	__shared__ uint32_t xq_all[kWavesPerBlock * XQ];
 	__shared__ unsigned long long blk_cnt[CNT_SLOT];
 
 	const int lane = threadIdx.x & (kWave - 1);
 	const int wid = threadIdx.x / kWave;
-	uint32_t *win = lds + wid * kWave * SDW;
+	uint4 *buf = buf_all + wid * 4 * kWave;
 	uint64_t *dtab = dtab_all + wid * kWave;
 	uint32_t *xq = xq_all + wid * XQ;
 
@@ -924,102 +979,123 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 
 	const uint64_t ntiles = ((uint64_t)a.n + kWave - 1) / kWave;
 	const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
-	uint32_t cnt[CNT_FRAG + 1] = {};   /* wave-uniform */
-	uint64_t my_bytes = 0;
-	uint32_t xq_n = 0;                 /* deferred frames queued (uniform) */
-	uint32_t xout = 0;                 /* deferred frames flushed (uniform) */
 	const uint64_t wgid = (uint64_t)blockIdx.x * kWavesPerBlock + wid;
 	uint32_t *xl = a.xlist + wgid * a.xregion;
+	uint32_t cnt[CNT_FRAG + 1] = {};   /* wave-uniform */
+	uint64_t my_bytes = 0;
+	uint32_t xq_n = 0, xout = 0;       /* queued / flushed deferrals (uniform) */
 
-	uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + wid;
-	uint4 dcur = load_desc(a.desc, t * kWave + lane, a.n);
-	uint4 dnext = dcur;
-	uint4 fv[PF ? WIN / 16 : 1];
-	bool mis_cur = false;
-	if constexpr (PF) {
-		/* software pipeline: the window loads of tile t+1 are in flight
-		 * while tile t is processed */
-		if (t < ntiles)
-			mis_cur = issue_window<WIN>(a, dcur, lane, dtab, fv);
-		dnext = load_desc(a.desc, (t + nwaves) * kWave + lane, a.n);
+	/* the DMA of an invalid frame reads the UMEM's first 64 bytes */
+	const bool dma = !a.force_generic && a.usize >= 64;
+	/* descriptor of frame t*64+lane, index clamped to the batch so the
+	 * prefetch is an unconditional load (lanes past the end are inactive) */
+	auto ld_desc = [&](uint64_t tt) -> uint4 {
+		uint64_t i = tt * kWave + lane;
+		i = i < a.n ? i : a.n - 1;
+		return *reinterpret_cast<const uint4 *>(a.desc + i);
+	};
+	/* DMA the 64-byte windows of a tile into buf: frames that are not
+	 * valid, 16-byte aligned and whole inside the UMEM load the UMEM's
+	 * first chunks instead (their lanes are deferred) */
+	auto issue = [&](uint4 dv) {
+		const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
+		const uint32_t len = dv.z;
+		const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
+		const bool ok = dma && len >= 14 && (uint64_t)len <= a.usize &&
+				eff <= a.usize - len && !(eff & 15) &&
+				eff + 64 <= ((a.usize + 15) & ~15ull);
+		dtab[lane] = ok ? eff : 0ull;
+		__builtin_amdgcn_wave_barrier();
+#pragma unroll
+		for (int k = 0; k < 4; k++) {
+			const int f = 16 * k + (lane >> 2);
+			const int c = (lane & 3) ^ ((f >> 2) & 3);
+			__builtin_amdgcn_global_load_lds(
+				(const void *)(a.umem + dtab[f] + 16 * c),
+				(lds_void_t *)(buf + kWave * k), 16, 0, 2 /* nt */);
+		}
+	};
+
+	uint64_t t = wgid;
+	uint4 dcur = make_uint4(0, 0, 0, 0), dnext = dcur;
+	if (t < ntiles) {
+		dcur = ld_desc(t);
+		dnext = ld_desc(t + nwaves);
+		if (dma)
+			issue(dcur);
 	}
 	for (; t < ntiles; t += nwaves) {
 		const uint64_t i = t * kWave + lane;
 		const bool active = i < a.n;
+		const uint4 dv = dcur;
 
-		/* 1. descriptor (prefetched one tile ahead) */
-		uint4 dv;
-		if constexpr (PF) {
-			dv = dcur;
-		} else {
-			dv = dnext;
-			dnext = load_desc(a.desc, (t + nwaves) * kWave + lane, a.n);
+		/* 1. this lane's window out of LDS (4 conflict-free b128 reads),
+		 * then the next tile's DMA and descriptors */
+		uint32_t F[18];
+		{
+			const int sw = (lane >> 2) & 3;
+#pragma unroll
+			for (int c = 0; c < 4; c++) {
+				const uint4 v = buf[4 * lane + (c ^ sw)];
+				F[4 * c] = v.x;
+				F[4 * c + 1] = v.y;
+				F[4 * c + 2] = v.z;
+				F[4 * c + 3] = v.w;
+			}
+			F[16] = F[17] = 0;
 		}
+		__builtin_amdgcn_s_waitcnt(0xc07f);   /* lgkmcnt(0): buf read */
+		__builtin_amdgcn_wave_barrier();
+		if (t + nwaves < ntiles) {
+			dcur = dnext;
+			if (dma)
+				issue(dcur);
+			dnext = ld_desc(t + 2 * nwaves);
+		}
+
 		const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
 		const uint32_t len = dv.z;
 		const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
-		const bool valid = active && (uint64_t)len <= a.usize &&
-				   eff <= a.usize - len;
+		const bool staged = dma && active && len >= 14 && (uint64_t)len <= a.usize &&
+				    eff <= a.usize - len && !(eff & 15) &&
+				    eff + 64 <= ((a.usize + 15) & ~15ull);
 
-		/* 2. stage the header windows (transposed 16-B loads); a tile
-		 * with an unaligned frame goes to the generic path whole */
-		bool misaligned;
-		if constexpr (PF) {
-			misaligned = mis_cur;
-			if (!misaligned)
-				commit_window<WIN>(win, fv, lane);
-		} else {
-			uint4 cv[WIN / 16];
-			misaligned = issue_window<WIN>(a, dv, lane, dtab, cv);
-			if (!misaligned)
-				commit_window<WIN>(win, cv, lane);
-		}
-		__builtin_amdgcn_wave_barrier();
-		if constexpr (PF) {
-			dcur = dnext;
-			if (t + nwaves < ntiles)
-				mis_cur = issue_window<WIN>(a, dcur, lane, dtab, fv);
-			dnext = load_desc(a.desc, (t + 2 * nwaves) * kWave + lane, a.n);
-		}
-
-		/* 3. fast path: Ethernet + 0..2 VLAN tags + IPv4 (ihl 5, not a
-		 * fragment) + UDP/TCP, everything at fixed offsets from the L2
-		 * end.  Frames of any other shape are deferred (below).  The
-		 * results are those of the generic pipeline for such frames. */
-		const uint32_t *w = win + lane * SDW;
-		const uint32_t w3 = w[3], w4 = w[4];
+		/* 2. fast-shape classification.  r[j] = frame dword j + nv */
 		uint32_t nv = 0;
-		if (le_is_vlan(w3 & 0xffff)) {
+		if (le_is_vlan(F[3] & 0xffff)) {
 			nv = 1;
-			if (le_is_vlan(w4 & 0xffff))
+			if (le_is_vlan(F[4] & 0xffff))
 				nv = 2;
 		}
-		const uint32_t *r = w + nv;        /* frame offsets shifted by 4*nv */
-		const uint32_t r3 = r[3], r4 = r[4], r5 = r[5], r6 = r[6];
-		const uint32_t r7 = r[7], r8 = r[8], r9 = r[9], r10 = r[10];
-		const uint32_t r11 = r[11], r12 = r[12];
+		uint32_t r[16];
+#pragma unroll
+		for (int j = 3; j < 16; j++)
+			r[j] = nv == 0 ? F[j] : nv == 1 ? F[j + 1] : F[j + 2];
 		const uint32_t l3 = 14 + 4 * nv, l4 = l3 + 20;
-		const uint32_t tot = bswap16(r4 & 0xffff);
-		const uint32_t proto = r5 >> 24;
+		const uint32_t tot = bswap16(r[4] & 0xffff);
+		const uint32_t proto = r[5] >> 24;
 		const bool udp = proto == 17;
 		uint32_t cl;
-		bool fast = !a.force_generic && !misaligned && valid &&
-			    (r3 & 0x00ffffffu) == 0x00450008u &&
-			    (r5 & 0xff3fu) == 0 && (udp || proto == 6) &&
+		bool fast = !a.force_generic && staged &&
+			    (r[3] & 0x00ffffffu) == 0x00450008u &&
+			    (r[5] & 0xff3fu) == 0 && (udp || proto == 6) &&
 			    tot >= 20 && l3 + tot <= len;
 		if (udp) {
-			cl = bswap16(r9 >> 16);
+			cl = bswap16(r[9] >> 16);
 			fast = fast && len >= l4 + 8 && cl >= 8 && l4 + cl <= l3 + tot;
 		} else {
-			const uint32_t thl = ((r11 >> 20) & 0xf) * 4;
+			const uint32_t thl = ((r[11] >> 20) & 0xf) * 4;
 			cl = tot - 20;
 			fast = fast && len >= l4 + 20 && thl >= 20 && l4 + thl <= len &&
 			       cl >= thl;
 		}
+		/* the L4 checksum range (with udp_csum's odd over-read byte) must
+		 * lie in the window; larger frames go to the exception kernel,
+		 * whose payload sums stream from HBM */
+		fast = fast && l4 + cl + (cl & 1) <= 64u;
 
-		/* 4. defer the other frames to this wave's region of the
-		 * exception list (LDS queue, flushed 64 at a time); the generic
-		 * kernel processes them after this launch */
+		/* 3. defer the other frames to this wave's region of the
+		 * exception list (LDS queue, flushed 64 at a time) */
 		const uint64_t dm = __ballot(active && !fast);
 		if (dm) {
 			const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
@@ -1039,51 +1115,23 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 			}
 		}
 
-		/* 5. fast frames: flow key, hash and tuple first (they do not
-		 * depend on the payload), then the checksums */
-		const uint32_t sa = (r6 >> 16) | (r7 << 16);
-		const uint32_t da = (r7 >> 16) | (r8 << 16);
-		const uint32_t ports = (r8 >> 16) | (r9 << 16);
-		uint32_t hash = 0;
-		if (fast) {
-			uint32_t key[11] = {0, 0, 0xffff0000u, sa, ports & 0xffff,
-					    0, 0, 0xffff0000u, da, ports >> 16,
-					    proto | (2u << 16)};
-			hash = jhash_key44(key, a.initval);
-			if (a.tup) {
-				if (a.tuple_fmt == XDPGPU_TUPLE_V4) {
-					const uint32_t vid =
-						nv ? (bswap16(w3 >> 16) & 0x0fff) : 0u;
-					*reinterpret_cast<uint4 *>(a.tup + 16 * i) =
-						make_uint4(sa, da, ports,
-							   proto | (2u << 8) | (vid << 16));
-				} else if (a.tuple_fmt == XDPGPU_TUPLE_NET) {
-					uint32_t *tp = reinterpret_cast<uint32_t *>(a.tup + 44 * i);
-#pragma unroll
-					for (int j = 0; j < 11; j++)
-						tp[j] = key[j];
-				}
-			}
-			my_bytes += len;
-		}
+		/* 4. fast frames: flow key, hash, tuple, checksums, verdict */
+		const uint32_t sa = (r[6] >> 16) | (r[7] << 16);
+		const uint32_t da = (r[7] >> 16) | (r[8] << 16);
+		const uint32_t ports = (r[8] >> 16) | (r[9] << 16);
 		/* IPv4 header sum, check word (r6 low half) excluded */
-		const uint64_t s3 = (uint64_t)(r3 & 0xffff0000u) + r4 + r5 +
-				    (r6 & 0xffff0000u) + r7 + (r8 & 0xffffu);
-		const uint32_t c3 = r6 & 0xffff;
-		const uint32_t l3c = ~fold16(s3) & 0xffff;
-		const bool l3_ok = fold16(s3 + c3) == 0xffff;
-		const uint32_t c4 = udp ? (r10 & 0xffff) : (r12 >> 16);
-		/* L4 window sum over [34, end) in the shifted frame, check word
-		 * excluded; udp_csum's odd-length over-read byte included;
-		 * pseudo header folded in */
-		const uint32_t over = cl & 1;
-		const int32_t e = (int32_t)(34 + cl + over) <
-				  (int32_t)(WIN - 4 * nv) ?
-				  (int32_t)(34 + cl + over) : (int32_t)(WIN - 4 * nv);
-		uint64_t s4 = (uint64_t)(r8 & 0xffff0000u) + sa + da +
+		const uint64_t s3 = (uint64_t)(r[3] & 0xffff0000u) + r[4] + r[5] +
+				    (r[6] & 0xffff0000u) + r[7] + (r[8] & 0xffffu);
+		const uint32_t c3 = r[6] & 0xffff;
+		const uint32_t c4 = udp ? (r[10] & 0xffff) : (r[12] >> 16);
+		/* L4 sum over [34, end) of the shifted frame with the pseudo
+		 * header, check word excluded; udp_csum's odd-length over-read
+		 * byte included (lib_checksum.h:142-179) */
+		const int32_t e = (int32_t)(34 + cl + (cl & 1));
+		uint64_t s4 = (uint64_t)(r[8] & 0xffff0000u) + sa + da +
 			      ((uint64_t)(proto + cl) << 8);
 #pragma unroll
-		for (int j = 9; j < WIN / 4; j++) {
+		for (int j = 9; j < 16; j++) {
 			uint32_t m = first_bytes(e - 4 * j);
 			if (j == 10)
 				m &= udp ? 0xffff0000u : 0xffffffffu;
@@ -1091,19 +1139,19 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 				m &= udp ? 0xffffffffu : 0x0000ffffu;
 			s4 += r[j] & m;
 		}
+		const uint32_t l3c = ~fold16(s3) & 0xffff;
+		const bool l3_ok = fold16(s3 + c3) == 0xffff;
 		const uint32_t sum4 = fold16(s4);
-		const uint32_t rhi = l4 + cl + over;      /* frame relative */
-		const uint32_t ext = ext_sums<WIN>(a, fast && rhi > (uint32_t)WIN,
-						   eff, l4, rhi, udp ? l4 + 6 : l4 + 16,
-						   c4, lane);
-		const uint64_t body = (uint64_t)sum4 + ext;
-		const uint32_t l4c = ~fold16(body) & 0xffff;
+		const uint32_t l4c = ~sum4 & 0xffff;
 		const bool absent = udp && c4 == 0;
-		const bool l4_ok = absent || (~fold16(body + c4) & 0xffff) == 0;
+		const bool l4_ok = absent || (~fold16((uint64_t)sum4 + c4) & 0xffff) == 0;
 		const bool drop = (a.flags & XDPGPU_CFG_VERIFY_CSUM) && (!l3_ok || !l4_ok);
 		if (fast) {
+			uint32_t key[11] = {0, 0, 0xffff0000u, sa, ports & 0xffff,
+					    0, 0, 0xffff0000u, da, ports >> 16,
+					    proto | (2u << 16)};
 			uint4 rec;
-			rec.x = hash;
+			rec.x = jhash_key44(key, a.initval);
 			rec.y = l3c | (l4c << 16);
 			rec.z = XDPGPU_F_IP | XDPGPU_F_L4 | (nv ? XDPGPU_F_VLAN : 0u) |
 				(l3_ok ? XDPGPU_F_L3_OK : 0u) |
@@ -1113,8 +1161,24 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 			rec.w = l4 | (cl << 16);
 			a.verdict[i] = (uint8_t)(drop ? XDPGPU_DROP : XDPGPU_REDIRECT);
 			if (a.res)
-				*reinterpret_cast<uint4 *>(a.res + i) = rec;
+				st_nt16(a.res + i, rec);
+			if (a.tup) {
+				if (a.tuple_fmt == XDPGPU_TUPLE_V4) {
+					const uint32_t vid =
+						nv ? (bswap16(F[3] >> 16) & 0x0fff) : 0u;
+					st_nt16(a.tup + 16 * i,
+						make_uint4(sa, da, ports,
+							   proto | (2u << 8) | (vid << 16)));
+				} else if (a.tuple_fmt == XDPGPU_TUPLE_NET) {
+					uint32_t *tp = reinterpret_cast<uint32_t *>(a.tup + 44 * i);
+#pragma unroll
+					for (int j = 0; j < 11; j++)
+						tp[j] = key[j];
+				}
+			}
+			my_bytes += len;
 		}
+		/* counters (wave-uniform: ballots outside divergent code) */
 		if (a.stats) {
 			cnt[CNT_FRAMES] += __popcll(__ballot(fast));
 			cnt[CNT_VERDICT0 + XDPGPU_DROP] += __popcll(__ballot(fast && drop));
@@ -1248,9 +1312,9 @@ uint32_t rx_grid_blocks(uint32_t n, uint32_t max_blocks)
 }
 
 /* Kernel variants selectable by cfg.tune (diagnostic A/B): bits 0-7 =
- * waves per SIMD the register allocator is held to (0 = compiler's
- * choice), bit 8 = software-pipelined window loads. */
-template <int WIN, int MINW, bool PF>
+ * waves per SIMD the fast kernel's register allocation is held to (0 =
+ * compiler's choice), bit 9 = every frame through the exception kernel. */
+template <int MINW>
 static uint32_t resident_blocks()
 {
 	static uint32_t cached = 0;
@@ -1260,7 +1324,7 @@ static uint32_t resident_blocks()
 		if (hipGetDevice(&dev) != hipSuccess ||
 		    hipGetDeviceProperties(&prop, dev) != hipSuccess ||
 		    hipOccupancyMaxActiveBlocksPerMultiprocessor(
-			    &per_cu, xdp_rx_kernel<WIN, MINW, PF>, kBlock, 0) != hipSuccess ||
+			    &per_cu, xdp_rx_kernel<MINW>, kBlock, 0) != hipSuccess ||
 		    per_cu <= 0)
 			return kMaxRxBlocks;
 		cached = (uint32_t)per_cu * (uint32_t)prop.multiProcessorCount;
@@ -1271,16 +1335,16 @@ static uint32_t resident_blocks()
 /* Launch the fast kernel on a grid of resident blocks (no partial second
  * round), then the exception kernel on the same grid.  a.xlist must hold
  * rx_xlist_entries(a.n, blocks) entries. */
-template <int WIN, int MINW, bool PF>
+template <int WIN, int MINW>
 static hipError_t launch_sized(RxArgs a, uint32_t max_blocks,
 			       hipStream_t stream)
 {
-	uint32_t cap = resident_blocks<WIN, MINW, PF>();
+	uint32_t cap = resident_blocks<MINW>();
 	if (cap < max_blocks)
 		max_blocks = cap;
 	const uint32_t blocks = rx_grid_blocks(a.n, max_blocks);
 	a.xregion = rx_xregion(a.n, blocks);
-	hipLaunchKernelGGL((xdp_rx_kernel<WIN, MINW, PF>), dim3(blocks),
+	hipLaunchKernelGGL((xdp_rx_kernel<MINW>), dim3(blocks),
 			   dim3(kBlock), 0, stream, a);
 	hipError_t e = hipGetLastError();
 	if (e != hipSuccess)
@@ -1301,22 +1365,13 @@ hipError_t launch_rx(const RxArgs &a, uint32_t window, uint32_t max_blocks,
 		     hipStream_t stream, uint32_t tune)
 {
 	const uint32_t waves = tune & 0xff;
-	const bool pf = (tune >> 8) & 1;
-	if (window == 128) {
-		if (pf)
-			return launch_sized<128, 1, true>(a, max_blocks, stream);
-		return launch_sized<128, 1, false>(a, max_blocks, stream);
-	}
-	if (pf) {
-		if (waves == 6)
-			return launch_sized<64, 6, true>(a, max_blocks, stream);
-		return launch_sized<64, 1, true>(a, max_blocks, stream);
-	}
+	if (window == 128)
+		return launch_sized<128, 1>(a, max_blocks, stream);
 	if (waves == 6)
-		return launch_sized<64, 6, false>(a, max_blocks, stream);
+		return launch_sized<64, 6>(a, max_blocks, stream);
 	if (waves == 8)
-		return launch_sized<64, 8, false>(a, max_blocks, stream);
-	return launch_sized<64, 1, false>(a, max_blocks, stream);
+		return launch_sized<64, 8>(a, max_blocks, stream);
+	return launch_sized<64, 1>(a, max_blocks, stream);
 }
 
 /* ------------------------------------------------------------------ */

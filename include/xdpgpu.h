@@ -120,10 +120,11 @@ struct xdpgpu_cfg {
 	uint32_t max_batch;     /* max descriptors per host-path call (0: 2^20) */
 	uint32_t jhash_initval; /* initval of jhash (CLI option, default 0)    */
 	uint32_t tuple_fmt;     /* XDPGPU_TUPLE_*                              */
-	uint32_t window;        /* header bytes staged in LDS: 64 or 128 (0: 64) */
+	uint32_t window;        /* header bytes the exception path stages in
+				 * LDS: 64 or 128 (0: 64) */
 	uint32_t tune;          /* kernel variant (diagnostic): bits 0-7 waves per
-				 * SIMD, bit 8 pipelined loads, bit 9 generic
-				 * path only; 0 = default */
+				 * SIMD, bit 8 reserved, bit 9 exception path
+				 * only; 0 = default */
 	uint32_t rsvd;
 };
 

@@ -1,0 +1,298 @@
+// SPDX-License-Identifier: GPL-2.0
+/*
+ * hbm_probe.hip - achievable HBM bandwidth on this MI355X for the access
+ * shapes of the RX kernel (diagnostic; not part of the product).
+ *
+ *   read      : dwordx4 streaming reads, grid-stride
+ *   read_nt   : the same with non-temporal loads
+ *   write     : dwordx4 streaming stores
+ *   copy      : read + write of equal size
+ *   rx_mix    : 80 B read + 33 B written per 64-B frame, as the RX kernel
+ *               (16 B descriptor + 64 B frame; 16 B + 16 B + 1 B stores)
+ *   rx_mix_nt : the same with non-temporal loads and stores
+ *
+ * Build: hipcc --offload-arch=gfx950 -O3 -o tools/hbm_probe tools/hbm_probe.hip
+ */
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ntl(const uint4 *p)
+{
+	v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(p));
+	return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void nts(uint4 r, uint4 *p)
+{
+	v4u v = {r.x, r.y, r.z, r.w};
+	__builtin_nontemporal_store(v, reinterpret_cast<v4u *>(p));
+}
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
+	fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
+
+template <bool NT>
+__global__ __launch_bounds__(256) void k_read(const uint4 *p, size_t n, uint32_t *out)
+{
+	uint32_t x = 0;
+	for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+		uint4 v = NT ? ntl(p + i) : p[i];
+		x ^= v.x ^ v.y ^ v.z ^ v.w;
+	}
+	if (x == 0x12345678u)
+		out[0] = x;
+}
+
+__global__ __launch_bounds__(256) void k_write(uint4 *p, size_t n)
+{
+	for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+		p[i] = make_uint4((uint32_t)i, 1, 2, 3);
+}
+
+__global__ __launch_bounds__(256) void k_copy(const uint4 *s, uint4 *d, size_t n)
+{
+	for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+		d[i] = s[i];
+}
+
+/* per frame: desc (16 B) + frame (64 B) read, 16 + 16 + 1 B written */
+template <bool NT, int UNROLL>
+__global__ __launch_bounds__(256) void k_rxmix(const uint4 *desc, const uint4 *frames,
+					       uint4 *res, uint4 *tup, uint8_t *verd,
+					       size_t nframes)
+{
+	const size_t tiles = nframes / 64;
+	const int lane = threadIdx.x & 63;
+	const size_t wave = blockIdx.x * 4ull + (threadIdx.x >> 6);
+	const size_t nw = (size_t)gridDim.x * 4;
+	for (size_t t = wave * UNROLL; t < tiles; t += nw * UNROLL) {
+		uint4 d[UNROLL], f[UNROLL][4];
+#pragma unroll
+		for (int u = 0; u < UNROLL; u++) {
+			const size_t i = (t + u) * 64 + lane;
+			d[u] = NT ? ntl(desc + i) : desc[i];
+#pragma unroll
+			for (int k = 0; k < 4; k++) {
+				const size_t c = (t + u) * 256 + k * 64 + lane;  /* transposed */
+				f[u][k] = NT ? ntl(frames + c) : frames[c];
+			}
+		}
+#pragma unroll
+		for (int u = 0; u < UNROLL; u++) {
+			const size_t i = (t + u) * 64 + lane;
+			uint32_t x = d[u].x ^ d[u].z;
+#pragma unroll
+			for (int k = 0; k < 4; k++)
+				x ^= f[u][k].x ^ f[u][k].y ^ f[u][k].z ^ f[u][k].w;
+			const uint4 r = make_uint4(x, x + 1, x + 2, x + 3);
+			if (NT) {
+				nts(r, res + i);
+				nts(r, tup + i);
+			} else {
+				res[i] = r;
+				tup[i] = r;
+			}
+			verd[i] = (uint8_t)x;
+		}
+	}
+}
+
+/* the same traffic, but each lane loads its own frame's four 16-B chunks
+ * (stride 64 B across lanes) straight into registers */
+template <bool NT, int UNROLL>
+__global__ __launch_bounds__(256) void k_rxdirect(const uint4 *desc, const uint4 *frames,
+						  uint4 *res, uint4 *tup, uint8_t *verd,
+						  size_t nframes)
+{
+	const size_t tiles = nframes / 64;
+	const int lane = threadIdx.x & 63;
+	const size_t wave = blockIdx.x * 4ull + (threadIdx.x >> 6);
+	const size_t nw = (size_t)gridDim.x * 4;
+	for (size_t t = wave * UNROLL; t < tiles; t += nw * UNROLL) {
+		uint4 d[UNROLL], f[UNROLL][4];
+#pragma unroll
+		for (int u = 0; u < UNROLL; u++) {
+			const size_t i = (t + u) * 64 + lane;
+			d[u] = NT ? ntl(desc + i) : desc[i];
+			const uint4 *fp = frames + (d[u].x & 0) + i * 4;
+#pragma unroll
+			for (int k = 0; k < 4; k++)
+				f[u][k] = NT ? ntl(fp + k) : fp[k];
+		}
+#pragma unroll
+		for (int u = 0; u < UNROLL; u++) {
+			const size_t i = (t + u) * 64 + lane;
+			uint32_t x = d[u].x ^ d[u].z;
+#pragma unroll
+			for (int k = 0; k < 4; k++)
+				x ^= f[u][k].x ^ f[u][k].y ^ f[u][k].z ^ f[u][k].w;
+			const uint4 r = make_uint4(x, x + 1, x + 2, x + 3);
+			if (NT) {
+				nts(r, res + i);
+				nts(r, tup + i);
+			} else {
+				res[i] = r;
+				tup[i] = r;
+			}
+			verd[i] = (uint8_t)x;
+		}
+	}
+}
+
+/* LDS-DMA staging: the transposed 16-B chunks of a tile go straight into
+ * LDS (global_load_lds_dwordx4 nt), slot(f, c) = 4f + (c ^ ((f >> 2) & 3))
+ * so that each lane's four ds_read_b128 of its own frame are conflict-free;
+ * the DMA of tile t+1 is in flight while tile t is processed. */
+typedef __attribute__((address_space(3))) void lds_void;
+__global__ __launch_bounds__(256) void k_rxlds(const uint4 *desc, const uint8_t *frames,
+					       uint4 *res, uint4 *tup, uint8_t *verd,
+					       size_t nframes)
+{
+	__shared__ uint4 buf_all[4 * 256];
+	__shared__ uint64_t dtab_all[4 * 64];
+	const int lane = threadIdx.x & 63;
+	const int wid = threadIdx.x >> 6;
+	uint4 *buf = buf_all + wid * 256;
+	uint64_t *dtab = dtab_all + wid * 64;
+	const size_t tiles = nframes / 64;
+	const size_t nw = (size_t)gridDim.x * 4;
+	size_t t = blockIdx.x * 4ull + wid;
+	auto issue = [&](uint4 dv) {
+		dtab[lane] = ((uint64_t)dv.y << 32) | dv.x;
+		__builtin_amdgcn_wave_barrier();
+#pragma unroll
+		for (int k = 0; k < 4; k++) {
+			const int f = 16 * k + (lane >> 2);
+			const int c = (lane & 3) ^ ((f >> 2) & 3);
+			const uint8_t *src = frames + dtab[f] + 16 * c;
+			__builtin_amdgcn_global_load_lds((const void *)src,
+				(lds_void *)(buf + 64 * k), 16, 0, 2);
+		}
+	};
+	if (t >= tiles)
+		return;
+	uint4 dcur = desc[t * 64 + lane];
+	issue(dcur);
+	auto ld = [&](size_t tt) { return desc[(tt < tiles ? tt : tiles - 1) * 64 + lane]; };
+	uint4 dnext = ld(t + nw);
+	for (; t < tiles; t += nw) {
+		const size_t i = t * 64 + lane;
+		uint4 f[4];
+#pragma unroll
+		for (int c = 0; c < 4; c++)
+			f[c] = buf[4 * lane + (c ^ ((lane >> 2) & 3))];
+		__builtin_amdgcn_s_waitcnt(0xc07f);   /* lgkmcnt(0) */
+		__builtin_amdgcn_wave_barrier();
+		const uint4 dv = dcur;
+		if (t + nw < tiles) {
+			dcur = dnext;
+			issue(dcur);
+			dnext = ld(t + 2 * nw);
+		}
+		uint32_t x = dv.x ^ dv.z;
+#pragma unroll
+		for (int k = 0; k < 4; k++)
+			x ^= f[k].x ^ f[k].y ^ f[k].z ^ f[k].w;
+		const uint4 r = make_uint4(x, x + 1, x + 2, x + 3);
+		nts(r, res + i);
+		nts(r, tup + i);
+		verd[i] = (uint8_t)x;
+	}
+}
+
+static float time_it(void (*fn)(void *), void *arg, int reps)
+{
+	hipEvent_t a, b;
+	CK(hipEventCreate(&a));
+	CK(hipEventCreate(&b));
+	fn(arg);
+	CK(hipDeviceSynchronize());
+	CK(hipEventRecord(a, 0));
+	for (int r = 0; r < reps; r++)
+		fn(arg);
+	CK(hipEventRecord(b, 0));
+	CK(hipEventSynchronize(b));
+	float ms = 0;
+	CK(hipEventElapsedTime(&ms, a, b));
+	return ms / reps;
+}
+
+struct Ctx {
+	uint4 *a, *b, *desc, *res, *tup;
+	uint8_t *verd;
+	uint32_t *out;
+	size_t n16, frames;
+	int grid;
+};
+
+static Ctx C;
+static void run_read(void *) { hipLaunchKernelGGL(k_read<false>, dim3(C.grid), dim3(256), 0, 0, C.a, C.n16, C.out); }
+static void run_read_nt(void *) { hipLaunchKernelGGL(k_read<true>, dim3(C.grid), dim3(256), 0, 0, C.a, C.n16, C.out); }
+static void run_write(void *) { hipLaunchKernelGGL(k_write, dim3(C.grid), dim3(256), 0, 0, C.b, C.n16); }
+static void run_copy(void *) { hipLaunchKernelGGL(k_copy, dim3(C.grid), dim3(256), 0, 0, C.a, C.b, C.n16 / 2); }
+static uint4 *descs_real;
+static void run_lds(void *) { hipLaunchKernelGGL(k_rxlds, dim3(C.grid), dim3(256), 0, 0, descs_real, (const uint8_t *)C.a, C.res, C.tup, C.verd, C.frames); }
+template <bool NT, int U>
+static void run_direct(void *) { hipLaunchKernelGGL((k_rxdirect<NT, U>), dim3(C.grid), dim3(256), 0, 0, C.desc, C.a, C.res, C.tup, C.verd, C.frames); }
+template <bool NT, int U>
+static void run_mix(void *) { hipLaunchKernelGGL((k_rxmix<NT, U>), dim3(C.grid), dim3(256), 0, 0, C.desc, C.a, C.res, C.tup, C.verd, C.frames); }
+
+int main(int argc, char **argv)
+{
+	const size_t frames = 16ull << 20;
+	C.frames = frames;
+	C.n16 = frames * 64 / 16;              /* 1 GiB */
+	CK(hipMalloc(&C.a, C.n16 * 16));
+	CK(hipMalloc(&C.b, C.n16 * 16));
+	CK(hipMalloc(&C.desc, frames * 16));
+	CK(hipMalloc(&C.res, frames * 16));
+	CK(hipMalloc(&C.tup, frames * 16));
+	CK(hipMalloc(&C.verd, frames));
+	CK(hipMalloc(&C.out, 64));
+	CK(hipMemset(C.a, 1, C.n16 * 16));
+	CK(hipMemset(C.desc, 2, frames * 16));
+	{
+		/* real packed descriptors for the LDS-DMA kernel */
+		uint4 *h = (uint4 *)malloc(frames * 16);
+		for (size_t i = 0; i < frames; i++)
+			h[i] = make_uint4((uint32_t)(i * 64), (uint32_t)((i * 64) >> 32), 64, 0);
+		CK(hipMalloc(&descs_real, frames * 16));
+		CK(hipMemcpy(descs_real, h, frames * 16, hipMemcpyHostToDevice));
+		free(h);
+	}
+	const int grids[] = {1024, 2048, 4096, 8192};
+	for (int gi = 0; gi < 4; gi++) {
+		if (argc > 1 && gi < 2) continue;
+		C.grid = grids[gi];
+		const double gb = C.n16 * 16 / 1e9;
+		float t;
+		t = time_it(run_read, 0, 20);
+		printf("grid %5d read      %7.1f GB/s\n", C.grid, gb / t * 1e3);
+		t = time_it(run_read_nt, 0, 20);
+		printf("grid %5d read_nt   %7.1f GB/s\n", C.grid, gb / t * 1e3);
+		t = time_it(run_write, 0, 20);
+		printf("grid %5d write     %7.1f GB/s\n", C.grid, gb / t * 1e3);
+		t = time_it(run_copy, 0, 20);
+		printf("grid %5d copy      %7.1f GB/s\n", C.grid, gb / t * 1e3);
+		const double mixb = frames * 113.0 / 1e9;
+		t = time_it(run_mix<false, 1>, 0, 20);
+		printf("grid %5d rx_mix    %7.1f GB/s  %.4f ms\n", C.grid, mixb / t * 1e3, t);
+		t = time_it(run_mix<true, 1>, 0, 20);
+		printf("grid %5d rx_mix_nt %7.1f GB/s  %.4f ms\n", C.grid, mixb / t * 1e3, t);
+		t = time_it(run_mix<false, 2>, 0, 20);
+		printf("grid %5d rx_mix_u2 %7.1f GB/s  %.4f ms\n", C.grid, mixb / t * 1e3, t);
+		t = time_it(run_mix<true, 2>, 0, 20);
+		printf("grid %5d rx_mix_nt_u2 %7.1f GB/s  %.4f ms\n", C.grid, mixb / t * 1e3, t);
+		t = time_it(run_lds, 0, 20);
+		printf("grid %5d rx_lds       %7.1f GB/s  %.4f ms\n", C.grid, mixb / t * 1e3, t);
+		t = time_it(run_direct<false, 1>, 0, 20);
+		printf("grid %5d rx_direct    %7.1f GB/s  %.4f ms\n", C.grid, mixb / t * 1e3, t);
+		t = time_it(run_direct<true, 1>, 0, 20);
+		printf("grid %5d rx_direct_nt %7.1f GB/s  %.4f ms\n", C.grid, mixb / t * 1e3, t);
+		t = time_it(run_direct<true, 2>, 0, 20);
+		printf("grid %5d rx_direct_nt_u2 %7.1f GB/s  %.4f ms\n", C.grid, mixb / t * 1e3, t);
+	}
+	return 0;
+}
