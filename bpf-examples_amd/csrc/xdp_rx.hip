@@ -955,16 +955,19 @@ __device__ __forceinline__ void st_nt16(void *p, uint4 r)
  * under tile t's parse.  Descriptors are prefetched two tiles ahead.
  *
  * Frames of the fast shape (Ethernet + 0..2 VLAN tags + IPv4 ihl 5, not a
- * fragment, + UDP/TCP whose checksum range lies in the window) are finished
- * here; every other frame is deferred to the exception kernel.
+ * fragment, + UDP/TCP) whose checksum range lies in the window are finished
+ * here.  Fast-shape frames with a longer range get everything but the
+ * payload sum here and go to the bulk list; every other frame is deferred
+ * to the exception kernel.
  */
 template <int MINW>
 __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 {
-	constexpr int XQ = 2 * kWave;      /* exception queue per wave */
+	constexpr int XQ = 2 * kWave;      /* deferral queues per wave */
 	__shared__ uint4 buf_all[kWavesPerBlock * 4 * kWave];
 	__shared__ uint64_t dtab_all[kWavesPerBlock * kWave];
 	__shared__ uint32_t xq_all[kWavesPerBlock * XQ];
+	__shared__ uint32_t bq_all[kWavesPerBlock * XQ];
 	__shared__ unsigned long long blk_cnt[CNT_SLOT];
 
 	const int lane = threadIdx.x & (kWave - 1);
@@ -972,6 +975,7 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 	uint4 *buf = buf_all + wid * 4 * kWave;
 	uint64_t *dtab = dtab_all + wid * kWave;
 	uint32_t *xq = xq_all + wid * XQ;
+	uint32_t *bq = bq_all + wid * XQ;
 
 	if (threadIdx.x < CNT_SLOT)
 		blk_cnt[threadIdx.x] = 0;
@@ -981,9 +985,34 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 	const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
 	const uint64_t wgid = (uint64_t)blockIdx.x * kWavesPerBlock + wid;
 	uint32_t *xl = a.xlist + wgid * a.xregion;
+	uint32_t *bl = a.blist + wgid * a.xregion;
 	uint32_t cnt[CNT_FRAG + 1] = {};   /* wave-uniform */
 	uint64_t my_bytes = 0;
-	uint32_t xq_n = 0, xout = 0;       /* queued / flushed deferrals (uniform) */
+	/* queued / flushed deferrals (uniform): exception and bulk lists */
+	uint32_t xq_n = 0, xout = 0, bq_n = 0, bout = 0;
+
+	/* append the frames of the lanes with want set to a wave's list: LDS
+	 * queue in lane order, flushed to the list 64 entries at a time */
+	auto defer = [&](bool want, uint64_t i, uint32_t *q, uint32_t &qn,
+			 uint32_t *gl, uint32_t &gout) {
+		const uint64_t dm = __ballot(want);
+		if (!dm)
+			return;
+		const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+			(uint32_t)(dm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0));
+		if (want)
+			q[qn + rank] = (uint32_t)i;
+		qn += (uint32_t)__popcll(dm);
+		if (qn >= (uint32_t)kWave) {
+			__builtin_amdgcn_wave_barrier();
+			gl[gout + lane] = q[lane];
+			gout += kWave;
+			const uint32_t rest = q[kWave + lane];
+			__builtin_amdgcn_wave_barrier();
+			q[lane] = rest;
+			qn -= kWave;
+		}
+	};
 
 	/* the DMA of an invalid frame reads the UMEM's first 64 bytes */
 	const bool dma = !a.force_generic && a.usize >= 64;
@@ -1089,31 +1118,16 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 			fast = fast && len >= l4 + 20 && thl >= 20 && l4 + thl <= len &&
 			       cl >= thl;
 		}
-		/* the L4 checksum range (with udp_csum's odd over-read byte) must
-		 * lie in the window; larger frames go to the exception kernel,
-		 * whose payload sums stream from HBM */
-		fast = fast && l4 + cl + (cl & 1) <= 64u;
+		/* a checksum range (with udp_csum's odd over-read byte) that ends
+		 * past the window: the bulk kernel adds the payload sum */
+		const bool shape = fast;
+		fast = shape && l4 + cl + (cl & 1) <= 64u;
+		const bool bulk = shape && !fast && a.res;
 
-		/* 3. defer the other frames to this wave's region of the
-		 * exception list (LDS queue, flushed 64 at a time) */
-		const uint64_t dm = __ballot(active && !fast);
-		if (dm) {
-			const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
-				(uint32_t)(dm >> 32),
-				__builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0));
-			if (active && !fast)
-				xq[xq_n + rank] = (uint32_t)i;
-			xq_n += (uint32_t)__popcll(dm);
-			if (xq_n >= (uint32_t)kWave) {
-				__builtin_amdgcn_wave_barrier();
-				xl[xout + lane] = xq[lane];
-				xout += kWave;
-				const uint32_t rest = xq[kWave + lane];
-				__builtin_amdgcn_wave_barrier();
-				xq[lane] = rest;
-				xq_n -= kWave;
-			}
-		}
+		/* 3. defer the frames of other shapes to the exception list and
+		 * the long ones to the bulk list of this wave */
+		defer(active && !fast && !bulk, i, xq, xq_n, xl, xout);
+		defer(bulk, i, bq, bq_n, bl, bout);
 
 		/* 4. fast frames: flow key, hash, tuple, checksums, verdict */
 		const uint32_t sa = (r[6] >> 16) | (r[7] << 16);
@@ -1126,7 +1140,8 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 		const uint32_t c4 = udp ? (r[10] & 0xffff) : (r[12] >> 16);
 		/* L4 sum over [34, end) of the shifted frame with the pseudo
 		 * header, check word excluded; udp_csum's odd-length over-read
-		 * byte included (lib_checksum.h:142-179) */
+		 * byte included (lib_checksum.h:142-179).  For a bulk frame the
+		 * window part: frame bytes [l4, 64) (F[16], F[17] are zero). */
 		const int32_t e = (int32_t)(34 + cl + (cl & 1));
 		uint64_t s4 = (uint64_t)(r[8] & 0xffff0000u) + sa + da +
 			      ((uint64_t)(proto + cl) << 8);
@@ -1146,20 +1161,24 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 		const bool absent = udp && c4 == 0;
 		const bool l4_ok = absent || (~fold16((uint64_t)sum4 + c4) & 0xffff) == 0;
 		const bool drop = (a.flags & XDPGPU_CFG_VERIFY_CSUM) && (!l3_ok || !l4_ok);
-		if (fast) {
+		if (fast || bulk) {
 			uint32_t key[11] = {0, 0, 0xffff0000u, sa, ports & 0xffff,
 					    0, 0, 0xffff0000u, da, ports >> 16,
 					    proto | (2u << 16)};
+			/* a bulk frame's record carries its window sum in the
+			 * l4_csum field and its check word in l4_off until the
+			 * bulk kernel completes it */
 			uint4 rec;
 			rec.x = jhash_key44(key, a.initval);
-			rec.y = l3c | (l4c << 16);
+			rec.y = l3c | ((fast ? l4c : sum4) << 16);
 			rec.z = XDPGPU_F_IP | XDPGPU_F_L4 | (nv ? XDPGPU_F_VLAN : 0u) |
 				(l3_ok ? XDPGPU_F_L3_OK : 0u) |
-				(l4_ok ? XDPGPU_F_L4_OK : 0u) |
-				(absent ? XDPGPU_F_L4_ABSENT : 0u) |
+				(fast && l4_ok ? XDPGPU_F_L4_OK : 0u) |
+				(fast && absent ? XDPGPU_F_L4_ABSENT : 0u) |
 				(proto << 8) | (l3 << 16) | (nv << 24);
-			rec.w = l4 | (cl << 16);
-			a.verdict[i] = (uint8_t)(drop ? XDPGPU_DROP : XDPGPU_REDIRECT);
+			rec.w = (fast ? l4 : c4) | (cl << 16);
+			if (fast)
+				a.verdict[i] = (uint8_t)(drop ? XDPGPU_DROP : XDPGPU_REDIRECT);
 			if (a.res)
 				st_nt16(a.res + i, rec);
 			if (a.tup) {
@@ -1176,7 +1195,7 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 						tp[j] = key[j];
 				}
 			}
-			my_bytes += len;
+			my_bytes += fast ? len : 0;
 		}
 		/* counters (wave-uniform: ballots outside divergent code) */
 		if (a.stats) {
@@ -1191,8 +1210,12 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 	__builtin_amdgcn_wave_barrier();
 	if ((uint32_t)lane < xq_n)
 		xl[xout + lane] = xq[lane];
-	if (lane == 0 && a.xcount)
+	if ((uint32_t)lane < bq_n)
+		bl[bout + lane] = bq[lane];
+	if (lane == 0) {
 		a.xcount[wgid] = xout + xq_n;
+		a.bcount[wgid] = bout + bq_n;
+	}
 
 	if (a.stats) {
 		const uint64_t bytes = wave_sum64(my_bytes);
@@ -1210,6 +1233,158 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 	}
 }
 
+
+/*
+ * Bulk kernel: completes the fast-shape frames whose L4 checksum range runs
+ * past the 64-byte window, by summing frame bytes [64, end of range) (with
+ * udp_csum's over-read byte; zero past the UMEM) into the window sum the
+ * fast kernel left in the result record.
+ *
+ * Per batch of 64 listed frames the wave works as four quarter-waves: a
+ * quarter streams one frame at a time, 16 lanes x 16 B x 2 = 512 B per
+ * step, and on finishing a frame takes the next unassigned one of the batch
+ * (dynamic, so long and short frames balance).  Per-lane partial sums go to
+ * LDS; lane f then adds frame f's 16 partials and completes its record.
+ * Frames are 16-byte aligned (a fast-shape condition), so absolute and
+ * frame-relative 16-bit words coincide.
+ */
+template <int MINW>
+__global__ __launch_bounds__(kBlock, MINW) void xdp_rx_bulk_kernel(RxArgs a)
+{
+	__shared__ uint4 meta_all[kWavesPerBlock * kWave];
+	__shared__ uint4 part_all[kWavesPerBlock * kWave * 4];
+	__shared__ unsigned long long blk_cnt[CNT_SLOT];
+
+	const int lane = threadIdx.x & (kWave - 1);
+	const int wid = threadIdx.x / kWave;
+	uint4 *meta = meta_all + wid * kWave;
+	uint4 *part4 = part_all + wid * kWave * 4;
+	uint32_t *part = reinterpret_cast<uint32_t *>(part4);
+	if (threadIdx.x < CNT_SLOT)
+		blk_cnt[threadIdx.x] = 0;
+	__syncthreads();
+
+	const uint64_t wgid = (uint64_t)blockIdx.x * kWavesPerBlock + wid;
+	const uint32_t count = a.bcount[wgid];
+	const uint32_t *bl = a.blist + wgid * a.xregion;
+	const uint32_t sub = lane & 15;
+	uint32_t cnt[CNT_FRAG + 1] = {};
+	uint64_t my_bytes = 0;
+	for (uint32_t b = 0; b < count; b += kWave) {
+		const uint32_t nb = count - b < (uint32_t)kWave ? count - b : kWave;
+		const bool act = (uint32_t)lane < nb;
+		const uint64_t i = bl[b + (act ? lane : 0)];
+		const uint4 dv = *reinterpret_cast<const uint4 *>(a.desc + i);
+		uint4 rv = *reinterpret_cast<const uint4 *>(a.res + i);
+		const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
+		const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
+		const uint32_t cl = rv.w >> 16;
+		const uint32_t l4 = ((rv.z >> 16) & 0xff) + 20;
+		uint64_t lim = eff + l4 + cl + (cl & 1);
+		lim = lim < a.usize ? lim : a.usize;
+		const uint64_t lo = eff + 64;
+		meta[lane] = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32),
+					(uint32_t)(lim > lo ? lim - lo : 0), 0);
+		__builtin_amdgcn_wave_barrier();
+
+		/* quarter-wave streaming with dynamic frame assignment */
+		uint32_t k = lane >> 4;            /* this quarter's frame */
+		uint32_t nxt = 4;                  /* next unassigned (uniform) */
+		bool live = k < nb;
+		uint4 m = meta[live ? k : 0];
+		uint64_t flo = ((uint64_t)m.y << 32) | m.x;
+		uint32_t fnb = m.z, o = 0, acc = 0;
+		while (__ballot(live)) {
+			uint4 v[2];
+#pragma unroll
+			for (int u = 0; u < 2; u++) {
+				const uint32_t ou = o + 256 * u + 16 * sub;
+				v[u] = make_uint4(0, 0, 0, 0);
+				if (live && ou < fnb)
+					v[u] = *reinterpret_cast<const uint4 *>(a.umem + flo + ou);
+			}
+#pragma unroll
+			for (int u = 0; u < 2; u++) {
+				const uint32_t ou = o + 256 * u + 16 * sub;
+				if (ou + 16 > fnb && ou < fnb) {
+					const uint4 mk = chunk_keep(ou, 0, fnb);
+					v[u].x &= mk.x;
+					v[u].y &= mk.y;
+					v[u].z &= mk.z;
+					v[u].w &= mk.w;
+				}
+				acc += halves(v[u].x) + halves(v[u].y) + halves(v[u].z) +
+				       halves(v[u].w);
+			}
+			o += 512;
+			const bool done = live && o >= fnb;
+			const uint64_t dq = __ballot(done && sub == 0);
+			if (dq) {
+				if (done) {
+					part[16 * k + sub] = acc;
+					acc = 0;
+					k = nxt + (uint32_t)__popcll(dq & ((1ull << (lane & ~15)) - 1));
+					live = k < nb;
+					m = meta[live ? k : 0];
+					flo = ((uint64_t)m.y << 32) | m.x;
+					fnb = m.z;
+					o = 0;
+				}
+				nxt += (uint32_t)__popcll(dq);
+			}
+		}
+		__builtin_amdgcn_wave_barrier();
+
+		/* lane f completes frame f: exact, a range is < 64 KiB + 64 B so
+		 * the raw sum of 16-bit halves fits 32 bits */
+		uint32_t t = 0;
+#pragma unroll
+		for (int j = 0; j < 4; j++) {
+			const uint4 x = part4[4 * lane + ((j + lane) & 3)];
+			t += x.x + x.y + x.z + x.w;
+		}
+		const uint32_t c4 = rv.w & 0xffff;
+		const uint32_t sum4 = fold16((uint64_t)(rv.y >> 16) + t);
+		const bool udp = ((rv.z >> 8) & 0xff) == 17;
+		const bool l3_ok = rv.z & XDPGPU_F_L3_OK;
+		const bool absent = udp && c4 == 0;
+		const bool l4_ok = absent || (~fold16((uint64_t)sum4 + c4) & 0xffff) == 0;
+		const bool drop = (a.flags & XDPGPU_CFG_VERIFY_CSUM) && (!l3_ok || !l4_ok);
+		if (act) {
+			rv.y = (rv.y & 0xffff) | ((~sum4 & 0xffff) << 16);
+			rv.z |= (l4_ok ? XDPGPU_F_L4_OK : 0u) |
+				(absent ? XDPGPU_F_L4_ABSENT : 0u);
+			rv.w = l4 | (cl << 16);
+			st_nt16(a.res + i, rv);
+			a.verdict[i] = (uint8_t)(drop ? XDPGPU_DROP : XDPGPU_REDIRECT);
+			my_bytes += dv.z;
+		}
+		if (a.stats) {
+			cnt[CNT_FRAMES] += __popcll(__ballot(act));
+			cnt[CNT_VERDICT0 + XDPGPU_DROP] += __popcll(__ballot(act && drop));
+			cnt[CNT_VERDICT0 + XDPGPU_REDIRECT] += __popcll(__ballot(act && !drop));
+			cnt[CNT_L3_BAD] += __popcll(__ballot(act && !l3_ok));
+			cnt[CNT_L4_BAD] += __popcll(__ballot(act && !l4_ok));
+			cnt[CNT_L4_ABSENT] += __popcll(__ballot(act && absent));
+		}
+		__builtin_amdgcn_wave_barrier();
+	}
+
+	if (a.stats) {
+		const uint64_t bytes = wave_sum64(my_bytes);
+		if (lane == 0) {
+			atomicAdd(&blk_cnt[CNT_BYTES], (unsigned long long)bytes);
+#pragma unroll
+			for (int k = 0; k <= CNT_FRAG; k++)
+				if (k != CNT_BYTES)
+					atomicAdd(&blk_cnt[k], (unsigned long long)cnt[k]);
+		}
+		__syncthreads();
+		if (threadIdx.x < CNT_SLOT)
+			a.stats[(uint64_t)blockIdx.x * CNT_SLOT + threadIdx.x] +=
+				blk_cnt[threadIdx.x];
+	}
+}
 
 /* Exception kernel: the generic pipeline on the frames the fast kernel
  * deferred, one wave per fast-kernel wave region, 64 frames per batch. */
@@ -1333,8 +1508,9 @@ static uint32_t resident_blocks()
 }
 
 /* Launch the fast kernel on a grid of resident blocks (no partial second
- * round), then the exception kernel on the same grid.  a.xlist must hold
- * rx_xlist_entries(a.n, blocks) entries. */
+ * round), then the bulk and exception kernels on the same grid (their wave
+ * regions are the fast kernel's).  a.xlist and a.blist must each hold
+ * blocks * kWavesPerBlock * rx_xregion(a.n, blocks) entries. */
 template <int WIN, int MINW>
 static hipError_t launch_sized(RxArgs a, uint32_t max_blocks,
 			       hipStream_t stream)
@@ -1347,6 +1523,11 @@ static hipError_t launch_sized(RxArgs a, uint32_t max_blocks,
 	hipLaunchKernelGGL((xdp_rx_kernel<MINW>), dim3(blocks),
 			   dim3(kBlock), 0, stream, a);
 	hipError_t e = hipGetLastError();
+	if (e != hipSuccess)
+		return e;
+	hipLaunchKernelGGL((xdp_rx_bulk_kernel<8>), dim3(blocks), dim3(kBlock), 0,
+			   stream, a);
+	e = hipGetLastError();
 	if (e != hipSuccess)
 		return e;
 	hipLaunchKernelGGL((xdp_rx_generic_kernel<WIN>), dim3(blocks),

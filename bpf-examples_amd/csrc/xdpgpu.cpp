@@ -250,13 +250,14 @@ static int ensure_slot_buffers(xdpgpu_ctx *ctx, Slot &s, uint32_t n)
 	return 0;
 }
 
-/* Exception-list scratch for a launch of n frames (any grid up to
- * kMaxRxBlocks): per-wave regions of whole tiles. */
+/* Deferred-frame list scratch for a launch of n frames (any grid up to
+ * kMaxRxBlocks): two lists (exception, bulk) of per-wave regions of whole
+ * tiles, xcap entries each, and their per-wave counts. */
 static int ensure_xlist(xdpgpu_ctx *ctx, Slot &s, uint32_t n)
 {
 	const uint64_t need = (uint64_t)n + 64ull * 4 * kMaxRxBlocks + 64;
 	if (!s.d_xcount &&
-	    hipMalloc(&s.d_xcount, (size_t)kMaxRxBlocks * 4 * sizeof(uint32_t)) != hipSuccess)
+	    hipMalloc(&s.d_xcount, (size_t)kMaxRxBlocks * 4 * 2 * sizeof(uint32_t)) != hipSuccess)
 		return set_err(ctx, -ENOMEM, "exception counts");
 	if (s.xcap >= need)
 		return 0;
@@ -266,7 +267,7 @@ static int ensure_xlist(xdpgpu_ctx *ctx, Slot &s, uint32_t n)
 		s.d_xlist = nullptr;
 		s.xcap = 0;
 	}
-	if (hipMalloc(&s.d_xlist, need * sizeof(uint32_t)) != hipSuccess)
+	if (hipMalloc(&s.d_xlist, 2 * need * sizeof(uint32_t)) != hipSuccess)
 		return set_err(ctx, -ENOMEM, "exception list of %llu entries",
 			       (unsigned long long)need);
 	s.xcap = need;
@@ -295,6 +296,8 @@ static int enqueue_rx(xdpgpu_ctx *ctx, Slot &s, uint8_t *d_umem, uint64_t usize,
 	a.stats = (ctx->cfg.flags & XDPGPU_CFG_STATS) ? s.d_stats : nullptr;
 	a.xlist = s.d_xlist;
 	a.xcount = s.d_xcount;
+	a.blist = s.d_xlist + s.xcap;
+	a.bcount = s.d_xcount + kMaxRxBlocks * 4;
 	a.force_generic = (ctx->cfg.tune >> 9) & 1;
 	HIP_TRY(ctx, launch_rx(a, ctx->cfg.window, ctx->max_blocks, stream,
 			       ctx->cfg.tune));

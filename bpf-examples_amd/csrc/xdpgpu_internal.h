@@ -38,8 +38,11 @@ struct RxArgs {
 	uint32_t flags;
 	uint32_t initval;
 	unsigned long long *stats; /* [kMaxRxBlocks][CNT_SLOT] or null */
-	uint32_t *xlist;           /* deferred-frame list, xregion per wave */
-	uint32_t *xcount;          /* deferred frames per wave              */
+	uint32_t *xlist;           /* exception list, xregion per wave      */
+	uint32_t *xcount;          /* exception frames per wave             */
+	uint32_t *blist;           /* bulk list (payload beyond the header
+				    * window), xregion per wave            */
+	uint32_t *bcount;          /* bulk frames per wave                  */
 	uint32_t xregion;          /* set by the launcher                   */
 	uint32_t force_generic;    /* 1: defer every frame (diagnostic)     */
 };
