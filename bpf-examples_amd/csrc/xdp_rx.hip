@@ -942,6 +942,13 @@ __device__ __forceinline__ void st_nt16(void *p, uint4 r)
 	__builtin_nontemporal_store(v, reinterpret_cast<v4u_t *>(p));
 }
 
+/* non-temporal 16-byte load (payload streamed once) */
+__device__ __forceinline__ uint4 ld_nt16(const void *p)
+{
+	const v4u_t v = __builtin_nontemporal_load(reinterpret_cast<const v4u_t *>(p));
+	return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 /*
  * Fast kernel, 64-byte header windows staged by LDS-DMA.
  *
@@ -1234,6 +1241,22 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 }
 
 
+/* Assignment of the fast kernel's wave regions to the waves of a
+ * follow-up kernel: with at least as many waves as regions, m = W / R waves
+ * share a region and take its batches round robin; otherwise waves stride
+ * over regions.  Each wave reads a region's count once. */
+struct RegionWalk {
+	uint32_t first, rstep, bfirst, bstep;
+	__device__ RegionWalk(uint32_t regions, uint32_t waves, uint32_t w)
+	{
+		const uint32_t m = waves >= regions ? waves / regions : 1;
+		first = w / m;
+		rstep = waves / m;
+		bfirst = (w % m) * kWave;
+		bstep = m * kWave;
+	}
+};
+
 /*
  * Bulk kernel: completes the fast-shape frames whose L4 checksum range runs
  * past the 64-byte window, by summing frame bytes [64, end of range) (with
@@ -1241,14 +1264,13 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
  * fast kernel left in the result record.
  *
  * Per batch of 64 listed frames the wave works as four quarter-waves: a
- * quarter streams one frame at a time, 16 lanes x 16 B x 2 = 512 B per
- * step, and on finishing a frame takes the next unassigned one of the batch
+ * quarter streams one frame at a time, 16 lanes x 16 B x U per step, and on finishing a frame takes the next unassigned one of the batch
  * (dynamic, so long and short frames balance).  Per-lane partial sums go to
  * LDS; lane f then adds frame f's 16 partials and completes its record.
  * Frames are 16-byte aligned (a fast-shape condition), so absolute and
  * frame-relative 16-bit words coincide.
  */
-template <int MINW>
+template <int MINW, int U, bool NT>
 __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_bulk_kernel(RxArgs a)
 {
 	__shared__ uint4 meta_all[kWavesPerBlock * kWave];
@@ -1264,13 +1286,15 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_bulk_kernel(RxArgs a)
 		blk_cnt[threadIdx.x] = 0;
 	__syncthreads();
 
-	const uint64_t wgid = (uint64_t)blockIdx.x * kWavesPerBlock + wid;
-	const uint32_t count = a.bcount[wgid];
-	const uint32_t *bl = a.blist + wgid * a.xregion;
+	const uint32_t nwaves = gridDim.x * kWavesPerBlock;
 	const uint32_t sub = lane & 15;
 	uint32_t cnt[CNT_FRAG + 1] = {};
 	uint64_t my_bytes = 0;
-	for (uint32_t b = 0; b < count; b += kWave) {
+	const RegionWalk w(a.nregions, nwaves, blockIdx.x * kWavesPerBlock + wid);
+	for (uint32_t r = w.first; r < a.nregions; r += w.rstep) {
+	const uint32_t count = a.bcount[r];
+	const uint32_t *bl = a.blist + (uint64_t)r * a.xregion;
+	for (uint32_t b = w.bfirst; b < count; b += w.bstep) {
 		const uint32_t nb = count - b < (uint32_t)kWave ? count - b : kWave;
 		const bool act = (uint32_t)lane < nb;
 		const uint64_t i = bl[b + (act ? lane : 0)];
@@ -1295,16 +1319,17 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_bulk_kernel(RxArgs a)
 		uint64_t flo = ((uint64_t)m.y << 32) | m.x;
 		uint32_t fnb = m.z, o = 0, acc = 0;
 		while (__ballot(live)) {
-			uint4 v[2];
+			uint4 v[U];
 #pragma unroll
-			for (int u = 0; u < 2; u++) {
+			for (int u = 0; u < U; u++) {
 				const uint32_t ou = o + 256 * u + 16 * sub;
 				v[u] = make_uint4(0, 0, 0, 0);
 				if (live && ou < fnb)
-					v[u] = *reinterpret_cast<const uint4 *>(a.umem + flo + ou);
+					v[u] = NT ? ld_nt16(a.umem + flo + ou)
+						  : *reinterpret_cast<const uint4 *>(a.umem + flo + ou);
 			}
 #pragma unroll
-			for (int u = 0; u < 2; u++) {
+			for (int u = 0; u < U; u++) {
 				const uint32_t ou = o + 256 * u + 16 * sub;
 				if (ou + 16 > fnb && ou < fnb) {
 					const uint4 mk = chunk_keep(ou, 0, fnb);
@@ -1316,7 +1341,7 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_bulk_kernel(RxArgs a)
 				acc += halves(v[u].x) + halves(v[u].y) + halves(v[u].z) +
 				       halves(v[u].w);
 			}
-			o += 512;
+			o += 256 * U;
 			const bool done = live && o >= fnb;
 			const uint64_t dq = __ballot(done && sub == 0);
 			if (dq) {
@@ -1369,6 +1394,7 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_bulk_kernel(RxArgs a)
 		}
 		__builtin_amdgcn_wave_barrier();
 	}
+	}
 
 	if (a.stats) {
 		const uint64_t bytes = wave_sum64(my_bytes);
@@ -1404,15 +1430,18 @@ __global__ __launch_bounds__(kBlock) void xdp_rx_generic_kernel(RxArgs a)
 		blk_cnt[threadIdx.x] = 0;
 	__syncthreads();
 
-	const uint64_t wgid = (uint64_t)blockIdx.x * kWavesPerBlock + wid;
-	const uint32_t count = a.xcount[wgid];
-	const uint32_t *xl = a.xlist + wgid * a.xregion;
+	const uint32_t nwaves = gridDim.x * kWavesPerBlock;
 	uint32_t cnt[CNT_FRAG + 1] = {};
 	uint64_t my_bytes = 0;
-	for (uint32_t b = 0; b < count; b += kWave) {
-		const bool act = b + lane < count;
-		const uint64_t i = act ? xl[b + lane] : 0;
-		generic_batch<WIN>(a, win, dtab, lane, i, act, cnt, my_bytes);
+	const RegionWalk w(a.nregions, nwaves, blockIdx.x * kWavesPerBlock + wid);
+	for (uint32_t r = w.first; r < a.nregions; r += w.rstep) {
+		const uint32_t count = a.xcount[r];
+		const uint32_t *xl = a.xlist + (uint64_t)r * a.xregion;
+		for (uint32_t b = w.bfirst; b < count; b += w.bstep) {
+			const bool act = b + lane < count;
+			const uint64_t i = act ? xl[b + lane] : 0;
+			generic_batch<WIN>(a, win, dtab, lane, i, act, cnt, my_bytes);
+		}
 	}
 
 	if (a.stats) {
@@ -1488,8 +1517,10 @@ uint32_t rx_grid_blocks(uint32_t n, uint32_t max_blocks)
 
 /* Kernel variants selectable by cfg.tune (diagnostic A/B): bits 0-7 =
  * waves per SIMD the fast kernel's register allocation is held to (0 =
- * compiler's choice), bit 9 = every frame through the exception kernel. */
-template <int MINW>
+ * compiler's choice), bit 9 = every frame through the exception kernel,
+ * bits 10-11 = bulk-kernel variant. */
+/* Blocks of a kernel resident at once on the device (occupancy x CUs). */
+template <auto KERN>
 static uint32_t resident_blocks()
 {
 	static uint32_t cached = 0;
@@ -1499,40 +1530,65 @@ static uint32_t resident_blocks()
 		if (hipGetDevice(&dev) != hipSuccess ||
 		    hipGetDeviceProperties(&prop, dev) != hipSuccess ||
 		    hipOccupancyMaxActiveBlocksPerMultiprocessor(
-			    &per_cu, xdp_rx_kernel<MINW>, kBlock, 0) != hipSuccess ||
+			    &per_cu, KERN, kBlock, 0) != hipSuccess ||
 		    per_cu <= 0)
 			return kMaxRxBlocks;
 		cached = (uint32_t)per_cu * (uint32_t)prop.multiProcessorCount;
+		if (cached > kMaxRxBlocks)
+			cached = kMaxRxBlocks;
 	}
 	return cached;
 }
 
 /* Launch the fast kernel on a grid of resident blocks (no partial second
- * round), then the bulk and exception kernels on the same grid (their wave
- * regions are the fast kernel's).  a.xlist and a.blist must each hold
- * blocks * kWavesPerBlock * rx_xregion(a.n, blocks) entries. */
+ * round), then the bulk and exception kernels, each on its own resident
+ * grid, over the fast kernel's wave regions.  a.xlist and a.blist must each
+ * hold blocks * kWavesPerBlock * rx_xregion(a.n, blocks) entries. */
+template <auto KERN>
+static hipError_t launch_resident(const RxArgs &a, uint32_t cap,
+				  hipStream_t stream)
+{
+	uint32_t blocks = resident_blocks<KERN>();
+	if (blocks > cap)
+		blocks = cap;
+	hipLaunchKernelGGL(KERN, dim3(blocks), dim3(kBlock), 0, stream, a);
+	return hipGetLastError();
+}
+
 template <int WIN, int MINW>
 static hipError_t launch_sized(RxArgs a, uint32_t max_blocks,
-			       hipStream_t stream)
+			       hipStream_t stream, uint32_t bulk_variant)
 {
-	uint32_t cap = resident_blocks<MINW>();
+	uint32_t cap = resident_blocks<xdp_rx_kernel<MINW>>();
 	if (cap < max_blocks)
 		max_blocks = cap;
 	const uint32_t blocks = rx_grid_blocks(a.n, max_blocks);
 	a.xregion = rx_xregion(a.n, blocks);
+	a.nregions = blocks * kWavesPerBlock;
 	hipLaunchKernelGGL((xdp_rx_kernel<MINW>), dim3(blocks),
 			   dim3(kBlock), 0, stream, a);
 	hipError_t e = hipGetLastError();
 	if (e != hipSuccess)
 		return e;
-	hipLaunchKernelGGL((xdp_rx_bulk_kernel<8>), dim3(blocks), dim3(kBlock), 0,
-			   stream, a);
-	e = hipGetLastError();
+	/* at most one wave per (region, batch) */
+	const uint64_t items = (uint64_t)a.nregions * (a.xregion / kWave);
+	const uint32_t icap = (uint32_t)((items + kWavesPerBlock - 1) / kWavesPerBlock);
+	switch (bulk_variant) {
+	case 1:
+		e = launch_resident<xdp_rx_bulk_kernel<8, 2, false>>(a, icap, stream);
+		break;
+	case 2:
+		e = launch_resident<xdp_rx_bulk_kernel<8, 4, true>>(a, icap, stream);
+		break;
+	case 3:
+		e = launch_resident<xdp_rx_bulk_kernel<8, 4, false>>(a, icap, stream);
+		break;
+	default:
+		e = launch_resident<xdp_rx_bulk_kernel<8, 2, true>>(a, icap, stream);
+	}
 	if (e != hipSuccess)
 		return e;
-	hipLaunchKernelGGL((xdp_rx_generic_kernel<WIN>), dim3(blocks),
-			   dim3(kBlock), 0, stream, a);
-	return hipGetLastError();
+	return launch_resident<xdp_rx_generic_kernel<WIN>>(a, icap, stream);
 }
 
 uint32_t rx_xregion(uint32_t n, uint32_t blocks)
@@ -1546,13 +1602,16 @@ hipError_t launch_rx(const RxArgs &a, uint32_t window, uint32_t max_blocks,
 		     hipStream_t stream, uint32_t tune)
 {
 	const uint32_t waves = tune & 0xff;
+	/* bits 10-11: bulk-kernel loads per lane and step (0: 2 non-temporal,
+	 * 1: 2, 2: 4 non-temporal, 3: 4) */
+	const uint32_t bu = (tune >> 10) & 3;
 	if (window == 128)
-		return launch_sized<128, 1>(a, max_blocks, stream);
+		return launch_sized<128, 1>(a, max_blocks, stream, bu);
 	if (waves == 6)
-		return launch_sized<64, 6>(a, max_blocks, stream);
+		return launch_sized<64, 6>(a, max_blocks, stream, bu);
 	if (waves == 8)
-		return launch_sized<64, 8>(a, max_blocks, stream);
-	return launch_sized<64, 1>(a, max_blocks, stream);
+		return launch_sized<64, 8>(a, max_blocks, stream, bu);
+	return launch_sized<64, 1>(a, max_blocks, stream, bu);
 }
 
 /* ------------------------------------------------------------------ */

@@ -43,7 +43,9 @@ struct RxArgs {
 	uint32_t *blist;           /* bulk list (payload beyond the header
 				    * window), xregion per wave            */
 	uint32_t *bcount;          /* bulk frames per wave                  */
-	uint32_t xregion;          /* set by the launcher                   */
+	uint32_t xregion;          /* set by the launcher: entries per wave
+				    * region of both lists                  */
+	uint32_t nregions;         /* set by the launcher: fast-kernel waves */
 	uint32_t force_generic;    /* 1: defer every frame (diagnostic)     */
 };
 

@@ -124,7 +124,8 @@ struct xdpgpu_cfg {
 				 * LDS: 64 or 128 (0: 64) */
 	uint32_t tune;          /* kernel variant (diagnostic): bits 0-7 waves per
 				 * SIMD, bit 8 reserved, bit 9 exception path
-				 * only; 0 = default */
+				 * only, bits 10-11 bulk-kernel variant;
+				 * 0 = default */
 	uint32_t rsvd;
 };
 

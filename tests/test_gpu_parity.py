@@ -27,9 +27,9 @@ def to_dev(a: np.ndarray, pad: int = 64):
     return t
 
 
-# kernel variants (cfg.tune): default fast+exception kernels, every frame
-# through the generic kernel, software-pipelined window loads
-TUNES = [0, 512, 256]
+# kernel variants (cfg.tune): default kernels, every frame through the
+# exception kernel, 6-wave fast kernel with the 4-load plain bulk kernel
+TUNES = [0, 512, 6 | (3 << 10)]
 
 
 def run_dev(umem, descs, flags=0x5, initval=0, fmt=1, window=64, tune=0):
@@ -136,6 +136,65 @@ def test_pool_vs_oracle(dev, name, kind, size, seed, n, kw, window, tune):
         oracle_stats_match(st, ost)
         if flags == 0x5:
             np.testing.assert_array_equal(v, expect)
+
+
+def bulk_frames(seed: int, n: int):
+    """Fast-shape IPv4 UDP/TCP frames of every length class around and past
+    the 64-byte header window (0..2 VLAN tags, odd lengths, trailing pad,
+    bad and absent checksums), 16-byte aligned with random gaps; the last
+    frame ends at the UMEM end with an odd UDP length (over-read past the
+    UMEM reads as zero)."""
+    import frames as F
+    rng = np.random.default_rng(seed)
+    blobs = []
+    for k in range(n):
+        tags = [(0x8100, 5)] * int(rng.integers(0, 3))
+        plen = int(rng.integers(0, 60)) if k % 3 else int(rng.integers(0, 2960))
+        pay = rng.integers(0, 256, plen, dtype=np.uint8).tobytes()
+        if rng.random() < 0.5 or k == n - 1:
+            seg = F.udp(int(rng.integers(1, 65536)), 53, pay)
+            fr = F.v4_frame(17, seg, tags=tags)
+            if rng.random() < 0.05:
+                fr = fr[:-len(seg)] + F.set_csum(seg, 6, 0)
+        else:
+            fr = F.v4_frame(6, F.tcp(int(rng.integers(1, 65536)), 80, pay,
+                                     doff=int(rng.integers(5, 9))), tags=tags)
+        if rng.random() < 0.1 and plen:
+            b = bytearray(fr)
+            b[-1 - int(rng.integers(0, plen))] ^= 0x5A
+            fr = bytes(b)
+        if rng.random() < 0.1 and k != n - 1:
+            fr += rng.integers(0, 256, int(rng.integers(1, 9)), dtype=np.uint8).tobytes()
+        blobs.append(fr)
+    if len(blobs[-1]) % 2 == 0:        # odd UDP length for the last frame
+        seg = F.udp(7, 53, b"\x11" * 31)
+        blobs[-1] = F.v4_frame(17, seg)
+    offs, o = [], 0
+    for fr in blobs:
+        o += 16 * int(rng.integers(0, 4))
+        offs.append(o)
+        o = (o + len(fr) + 15) & ~15
+    size = offs[-1] + len(blobs[-1])
+    umem = np.zeros(size, np.uint8)
+    for off, fr in zip(offs, blobs):
+        umem[off:off + len(fr)] = np.frombuffer(fr, np.uint8)
+    descs = np.zeros(n, xdpgpu.DESC_DTYPE)
+    descs["addr"] = offs
+    descs["len"] = [len(fr) for fr in blobs]
+    return umem, descs
+
+
+@pytest.mark.parametrize("tune", TUNES)
+def test_bulk_lengths_vs_oracle(dev, tune):
+    """The bulk path (checksum ranges past the window) and its boundaries."""
+    umem, descs = bulk_frames(21, 3000)
+    for flags, iv, fmt in ((0x5, 0, 1), (0x4, 0x12345, 2)):
+        ov, ores, otup, ost = oracle.process(umem.copy(), descs, flags, iv, fmt)
+        v, res, tup, um, st = run_dev(umem, descs, flags, iv, fmt, 64, tune)
+        assert_same((v, res, tup, None), (ov, ores, otup, None), f"bulk/{flags:#x}")
+        oracle_stats_match(st, ost)
+        if flags == 0x5:
+            assert (ov == xdpgpu.REDIRECT).sum() > 2000 and (ov == xdpgpu.DROP).sum() > 100
 
 
 def test_unaligned_encoded_descriptors(dev):

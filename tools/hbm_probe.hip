@@ -239,8 +239,109 @@ static void run_direct(void *) { hipLaunchKernelGGL((k_rxdirect<NT, U>), dim3(C.
 template <bool NT, int U>
 static void run_mix(void *) { hipLaunchKernelGGL((k_rxmix<NT, U>), dim3(C.grid), dim3(256), 0, 0, C.desc, C.a, C.res, C.tup, C.verd, C.frames); }
 
+/* bulk payload probes: bytes [64, 1500) of frames at stride 1536 */
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void k_bulkq(const uint8_t *fr, size_t nframes,
+					       uint32_t *out)
+{
+	const int lane = threadIdx.x & 63, q = lane >> 4, sub = lane & 15;
+	const size_t nw = (size_t)gridDim.x * 4;
+	uint32_t x = 0;
+	for (size_t t = blockIdx.x * 4ull + (threadIdx.x >> 6); t < nframes / 64; t += nw) {
+		for (int j = 0; j < 16; j++) {
+			const uint8_t *f = fr + (t * 64 + 4 * j + q) * 1536ull + 64;
+			for (uint32_t o = 0; o < 1436; o += 256 * U) {
+				uint4 v[U];
+#pragma unroll
+				for (int u = 0; u < U; u++) {
+					const uint32_t ou = o + 256 * u + 16 * sub;
+					v[u] = make_uint4(0, 0, 0, 0);
+					if (ou < 1436)
+						v[u] = NT ? ntl((const uint4 *)(f + ou)) : *(const uint4 *)(f + ou);
+				}
+#pragma unroll
+				for (int u = 0; u < U; u++)
+					x += v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+			}
+		}
+	}
+	if (x == 0x12345678u)
+		out[0] = x;
+}
+
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void k_bulkw(const uint8_t *fr, size_t nframes,
+					       uint32_t *out)
+{
+	const int lane = threadIdx.x & 63;
+	const size_t nw = (size_t)gridDim.x * 4;
+	uint32_t x = 0;
+	for (size_t t = blockIdx.x * 4ull + (threadIdx.x >> 6); t < nframes / U; t += nw) {
+		uint4 v[2 * U];
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const uint8_t *f = fr + (t * U + u) * 1536ull + 64;
+#pragma unroll
+			for (int h = 0; h < 2; h++) {
+				const uint32_t ou = 1024 * h + 16 * lane;
+				v[2 * u + h] = make_uint4(0, 0, 0, 0);
+				if (ou < 1436)
+					v[2 * u + h] = NT ? ntl((const uint4 *)(f + ou)) : *(const uint4 *)(f + ou);
+			}
+		}
+#pragma unroll
+		for (int u = 0; u < 2 * U; u++)
+			x += v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+	}
+	if (x == 0x12345678u)
+		out[0] = x;
+}
+
+static uint8_t *bulk_buf;
+static size_t bulk_frames = 2ull << 20;
+template <int U, bool NT>
+static void run_bulkq(void *) { hipLaunchKernelGGL((k_bulkq<U, NT>), dim3(C.grid), dim3(256), 0, 0, bulk_buf, bulk_frames, C.out); }
+template <int U, bool NT>
+static void run_bulkw(void *) { hipLaunchKernelGGL((k_bulkw<U, NT>), dim3(C.grid), dim3(256), 0, 0, bulk_buf, bulk_frames, C.out); }
+template <bool NT>
+static void run_bulkflat(void *) { hipLaunchKernelGGL((k_read<NT>), dim3(C.grid), dim3(256), 0, 0, (const uint4 *)bulk_buf, bulk_frames * 1536 / 16, C.out); }
+
+static int bulk_main()
+{
+	CK(hipMalloc(&bulk_buf, bulk_frames * 1536));
+	CK(hipMemset(bulk_buf, 3, bulk_frames * 1536));
+	CK(hipMalloc(&C.out, 64));
+	const double gb = bulk_frames * 1436.0 / 1e9;
+	const int grids[] = {1024, 1536, 2048, 4096};
+	for (int gi = 0; gi < 4; gi++) {
+		C.grid = grids[gi];
+		float t;
+		t = time_it(run_bulkflat<false>, 0, 20);
+		printf("grid %5d flat       %7.1f GB/s (of 1436 B/frame) %.4f ms\n", C.grid, gb / t * 1e3, t);
+		t = time_it(run_bulkflat<true>, 0, 20);
+		printf("grid %5d flat_nt    %7.1f GB/s  %.4f ms\n", C.grid, gb / t * 1e3, t);
+		t = time_it(run_bulkq<2, false>, 0, 20);
+		printf("grid %5d q_u2       %7.1f GB/s  %.4f ms\n", C.grid, gb / t * 1e3, t);
+		t = time_it(run_bulkq<2, true>, 0, 20);
+		printf("grid %5d q_u2_nt    %7.1f GB/s  %.4f ms\n", C.grid, gb / t * 1e3, t);
+		t = time_it(run_bulkq<4, true>, 0, 20);
+		printf("grid %5d q_u4_nt    %7.1f GB/s  %.4f ms\n", C.grid, gb / t * 1e3, t);
+		t = time_it(run_bulkq<6, true>, 0, 20);
+		printf("grid %5d q_u6_nt    %7.1f GB/s  %.4f ms\n", C.grid, gb / t * 1e3, t);
+		t = time_it(run_bulkw<1, true>, 0, 20);
+		printf("grid %5d w_u1_nt    %7.1f GB/s  %.4f ms\n", C.grid, gb / t * 1e3, t);
+		t = time_it(run_bulkw<2, true>, 0, 20);
+		printf("grid %5d w_u2_nt    %7.1f GB/s  %.4f ms\n", C.grid, gb / t * 1e3, t);
+		t = time_it(run_bulkw<4, true>, 0, 20);
+		printf("grid %5d w_u4_nt    %7.1f GB/s  %.4f ms\n", C.grid, gb / t * 1e3, t);
+	}
+	return 0;
+}
+
 int main(int argc, char **argv)
 {
+	if (argc > 1 && !strcmp(argv[1], "bulk"))
+		return bulk_main();
 	const size_t frames = 16ull << 20;
 	C.frames = frames;
 	C.n16 = frames * 64 / 16;              /* 1 GiB */
