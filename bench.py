@@ -6,14 +6,19 @@ UMEM pool, xdpsock geometry), one pool shard per GPU (config 5 at N > 1).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
-A step = one launch of the RX kernel over the whole 16 M-frame shard that is
-resident in HBM.  Timing: W untimed steps, barrier + synchronize, K timed
-steps, synchronize + barrier, max over ranks.  value = frames processed by
-all ranks / that time (Mpps, whole job).  The roofline figure is the
-dominant kernel's algorithmic bytes (113 B/frame) over its
-average duration from HIP events on the launch stream.  The CPU baseline is
-the oracle (oracle/xdp_oracle.c, a restatement of the reference C) timed on
-this host, rank 0 at N = 1 only, on a bounded sample.
+A step = one RX launch (fast, bulk and exception kernels, back to back on
+one stream) over the whole 16 M-frame shard resident in HBM.  Timing: W
+untimed steps, barrier + synchronize, K timed steps, synchronize + barrier,
+max over ranks.  value = frames processed by all ranks / that time (Mpps,
+whole job).  The roofline figure is the algorithmic bytes of a launch
+(113 B/frame) over the launch's kernel time from HIP events
+recorded on the launch stream around each of the three kernels
+(xdpgpu_kernel_times); the per-kernel split is reported beside it.  traffic
+is the HBM bytes per launch from the committed rocprofv3 PMC summary
+(profiles/r01_pmc.json, tools/pmc_profile.sh).  The CPU baseline is the
+oracle (oracle/xdp_oracle.c, a restatement of the reference C) timed on this
+host, rank 0 at N = 1 only, on a bounded sample.  Secondary lines: config 2
+geometry at 1500 B, and config 3 (16 M IMIX, 44 B network_tuple).
 """
 from __future__ import annotations
 
@@ -34,6 +39,7 @@ import torch.distributed as dist  # noqa: E402
 import xdpgpu  # noqa: E402
 
 BYTES_PER_FRAME = 16 + 64 + 16 + 16 + 1   # desc + frame + result + tuple + verdict
+RX_KERNELS = ("xdp_rx_kernel", "xdp_rx_bulk_kernel", "xdp_rx_generic_kernel")
 HBM_PEAK_GBS = 8000.0                      # MI355X HBM3E, MI355X_MICROARCH.md
 METRIC = ("Mpps + GB/s device-resident parse+csum+jhash, 64B & 1500B frames, "
           "1/2/4/8 GPU")
@@ -52,26 +58,23 @@ def to_dev(a: np.ndarray, dev, pad: int = 64) -> torch.Tensor:
 
 def time_device(ctx, d_umem, usize, d_desc, n, d_v, d_res, d_tup, stream,
                 steps, warmup, world):
-    """W untimed + K timed launches; returns (wall seconds, avg kernel ms)."""
+    """W untimed + K timed launches; returns (wall seconds, per-kernel
+    average ms from the HIP events the library records on the stream)."""
     for _ in range(warmup):
         ctx.process_dev(d_umem, usize, d_desc, n, d_v, d_res, d_tup, stream)
     torch.cuda.synchronize()
+    ctx.kernel_times()                       # drop the warm-up records
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(steps)]
     t0 = time.perf_counter()
-    for s, e in ev:
-        s.record(stream)
+    for _ in range(steps):
         ctx.process_dev(d_umem, usize, d_desc, n, d_v, d_res, d_tup, stream)
-        e.record(stream)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
-    kms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
-    return t1 - t0, kms
+    return t1 - t0, ctx.kernel_times()
 
 
 def cpu_baseline(umem, descs, budget_s: float = 10.0):
@@ -100,9 +103,10 @@ def cpu_baseline(umem, descs, budget_s: float = 10.0):
                       f"(gcc -O2) on {threads} threads ({dt:.1f} s)"}
 
 
-def pmc_traffic():
-    """HBM bytes per launch of the RX kernel from the committed rocprofv3
-    PMC summary (profiles/*_pmc.json, see tools/pmc_traffic.py), or None."""
+def pmc_traffic(n: int, size: int):
+    """HBM bytes per RX launch from the committed rocprofv3 PMC summary
+    (profiles/*_pmc.json, tools/pmc_profile.sh + tools/pmc_summary.py), if it
+    was taken on this workload; else None."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
     if not files:
@@ -110,9 +114,39 @@ def pmc_traffic():
     try:
         with open(files[-1]) as f:
             d = json.load(f)
+        if d.get("frames") != n or d.get("frame_size") != size:
+            return None
         return d.get("hbm_bytes_per_launch")
     except Exception:
         return None
+
+
+def kt_round(kt: dict) -> dict:
+    return {k: (round(v, 4) if isinstance(v, float) else v) for k, v in kt.items()}
+
+
+def side_run(ctx, dev, stream, n, kind, size, seed, fmt, steps, label, bpf_fn):
+    """One secondary workload: pool, K timed launches, verdict check."""
+    u, ds, ex = xdpgpu.pool_generate(n, kind, size, seed)
+    g_umem = to_dev(u, dev)
+    g_desc = to_dev(ds, dev, 0)
+    tb = xdpgpu.TUPLE_BYTES[fmt]
+    g_v = torch.empty(n, dtype=torch.uint8, device=dev)
+    g_res = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    g_tup = torch.empty(n * tb, dtype=torch.uint8, device=dev)
+    w, kt = time_device(ctx, g_umem, u.nbytes, g_desc, n, g_v, g_res, g_tup,
+                        stream, steps, 2, 1)
+    ok = bool(np.array_equal(g_v.cpu().numpy(), ex))
+    algo = bpf_fn(ds)
+    out = {"workload": label, "frames": n,
+           "mpps": round(n * steps / w / 1e6, 1),
+           "algorithmic_bytes_per_launch": int(algo),
+           "gbps": round(algo / (kt["total_ms"] * 1e-3) / 1e9, 1),
+           "roofline_frac": round(algo / (kt["total_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "kernel_ms": kt_round(kt), "verdicts_ok": ok}
+    del g_umem, g_desc, g_v, g_res, g_tup
+    torch.cuda.empty_cache()
+    return out
 
 
 def main():
@@ -125,6 +159,7 @@ def main():
     ap.add_argument("--window", type=int, default=64)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--imix-frames", type=int, default=16 << 20)
     ap.add_argument("--e2e", action="store_true", help="also time the host path")
     args = ap.parse_args()
 
@@ -147,11 +182,13 @@ def main():
     d_v = torch.empty(n, dtype=torch.uint8, device=dev)
     d_res = torch.empty(n * 16, dtype=torch.uint8, device=dev)
     d_tup = torch.empty(n * 16, dtype=torch.uint8, device=dev)
-    ctx = xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT, 0, xdpgpu.TUPLE_V4, args.window)
+    ctx = xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT | xdpgpu.CFG_TIMING, 0,
+                        xdpgpu.TUPLE_V4, args.window)
     stream = torch.cuda.Stream(dev)
 
-    wall, kms = time_device(ctx, d_umem, umem.nbytes, d_desc, n, d_v, d_res, d_tup,
-                            stream, args.steps, args.warmup, world)
+    wall, kt = time_device(ctx, d_umem, umem.nbytes, d_desc, n, d_v, d_res, d_tup,
+                           stream, args.steps, args.warmup, world)
+    kms = kt["total_ms"]
     # correctness spot check of the timed outputs against the generator
     v = d_v.cpu().numpy()
     ok = bool(np.array_equal(v, expect))
@@ -168,27 +205,28 @@ def main():
     gbps = total_frames * BYTES_PER_FRAME / wall_max / 1e9
     achieved = BYTES_PER_FRAME * n / (kms * 1e-3) / 1e9
 
-    secondary = None
+    achieved_fast = BYTES_PER_FRAME * n / (kt["fast_ms"] * 1e-3) / 1e9
+
+    secondary = {}
     if not args.no_secondary and rank == 0 and world == 1:
-        # 1500 B frames (BASELINE metric names both sizes): payload checksum
-        # by the cooperative wave path; 2 M frames (3 GB) per launch
         del d_umem
         torch.cuda.empty_cache()
-        n2 = 2 << 20
-        u2, ds2, ex2 = xdpgpu.pool_generate(n2, xdpgpu.POOL_UDP4, 1500, 0x5EED0012)
-        g_umem = to_dev(u2, dev)
-        g_desc = to_dev(ds2, dev, 0)
-        w2, k2 = time_device(ctx, g_umem, u2.nbytes, g_desc, n2, d_v, d_res, d_tup,
-                             stream, max(5, args.steps // 5), 2, 1)
-        ok2 = bool(np.array_equal(d_v[:n2].cpu().numpy(), ex2))
-        b2 = 16 + 1500 + 16 + 16 + 1
-        secondary = {"workload": "config2-geometry 2M x 1500B IPv4/UDP",
-                     "mpps": round(n2 * max(5, args.steps // 5) / w2 / 1e6, 1),
-                     "gbps": round(n2 * b2 / (k2 * 1e-3) / 1e9, 1),
-                     "kernel_ms": round(k2, 4),
-                     "roofline_frac": round(n2 * b2 / (k2 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                     "verdicts_ok": ok2}
-        del g_umem, g_desc
+        steps2 = max(5, args.steps // 5)
+        # 1500 B frames (BASELINE metric names both sizes), config 2 geometry
+        secondary["secondary_1500B"] = side_run(
+            ctx, dev, stream, 2 << 20, xdpgpu.POOL_UDP4, 1500, 0x5EED0012,
+            xdpgpu.TUPLE_V4, steps2, "config2-geometry 2M x 1500B IPv4/UDP, V4 tuple",
+            lambda ds: len(ds) * (16 + 16 + 16 + 1) + int(ds["len"].astype(np.int64).sum()))
+        # config 3: IMIX with the 44 B network_tuple (429.3 B/frame)
+        ctx3 = xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT | xdpgpu.CFG_TIMING, 0,
+                             xdpgpu.TUPLE_NET, 64)
+        secondary["config3_imix"] = side_run(
+            ctx3, dev, stream, args.imix_frames, xdpgpu.POOL_IMIX, 64, 0x5EED0003,
+            xdpgpu.TUPLE_NET, steps2,
+            f"config3: {args.imix_frames} IMIX frames (64/570/1500 7:4:1, VLAN, IPv6), "
+            "network_tuple",
+            lambda ds: len(ds) * (16 + 16 + 44 + 1) + int(ds["len"].astype(np.int64).sum()))
+        ctx3.close()
 
     e2e = None
     if args.e2e and rank == 0 and world == 1:
@@ -223,7 +261,7 @@ def main():
         cpu = cpu_baseline(umem, descs)
 
     if rank == 0:
-        traffic = pmc_traffic()
+        traffic = pmc_traffic(n, args.size)
         line = {
             "metric": METRIC,
             "value": round(mpps, 1),
@@ -247,13 +285,15 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
-                         "kernel_ms": round(kms, 4),
-                         "bytes_per_frame": BYTES_PER_FRAME},
+                         "kernels": "+".join(RX_KERNELS),
+                         "kernel_ms": kt_round(kt),
+                         "fast_kernel_achieved": round(achieved_fast, 1),
+                         "bytes_per_frame": BYTES_PER_FRAME,
+                         "algorithmic_bytes_per_launch": BYTES_PER_FRAME * n},
             "cpu_baseline": cpu,
             "verdicts_ok": bool(ok_t.item() > 0),
         }
-        if secondary:
-            line["secondary_1500B"] = secondary
+        line.update(secondary)
         if e2e:
             line["e2e_host_path"] = e2e
         print(json.dumps(line), flush=True)

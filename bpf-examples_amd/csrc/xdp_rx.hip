@@ -922,7 +922,7 @@ __device__ __forceinline__ void generic_batch(const RxArgs &a, uint32_t *win,
 /* LE 16-bit loads of the VLAN TPIDs 0x8100 / 0x88A8 (parsing_helpers.h:75) */
 __device__ __forceinline__ bool le_is_vlan(uint32_t v)
 {
-	return v == 0x0081u || v == 0xa888u;
+	return (v == 0x0081u) | (v == 0xa888u);
 }
 
 /* mask of the first nb (0..4) bytes of a dword */
@@ -1031,15 +1031,17 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 		return *reinterpret_cast<const uint4 *>(a.desc + i);
 	};
 	/* DMA the 64-byte windows of a tile into buf: frames that are not
-	 * valid, 16-byte aligned and whole inside the UMEM load the UMEM's
-	 * first chunks instead (their lanes are deferred) */
-	auto issue = [&](uint4 dv) {
+	 * valid, 16-byte aligned and whole inside the UMEM, and every frame of
+	 * a tile past the end (live false), load the UMEM's first 64 bytes
+	 * instead (one cached line; their lanes are deferred or inactive).
+	 * Issued unconditionally so that no wait for it is placed early. */
+	auto issue = [&](uint4 dv, bool live) {
 		const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
 		const uint32_t len = dv.z;
 		const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
-		const bool ok = dma && len >= 14 && (uint64_t)len <= a.usize &&
-				eff <= a.usize - len && !(eff & 15) &&
-				eff + 64 <= ((a.usize + 15) & ~15ull);
+		const bool ok = live & dma & (len >= 14) & ((uint64_t)len <= a.usize) &
+				(eff <= a.usize - len) & !(eff & 15) &
+				(eff + 64 <= ((a.usize + 15) & ~15ull));
 		dtab[lane] = ok ? eff : 0ull;
 		__builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -1057,8 +1059,7 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 	if (t < ntiles) {
 		dcur = ld_desc(t);
 		dnext = ld_desc(t + nwaves);
-		if (dma)
-			issue(dcur);
+		issue(dcur, true);
 	}
 	for (; t < ntiles; t += nwaves) {
 		const uint64_t i = t * kWave + lane;
@@ -1082,54 +1083,49 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 		}
 		__builtin_amdgcn_s_waitcnt(0xc07f);   /* lgkmcnt(0): buf read */
 		__builtin_amdgcn_wave_barrier();
-		if (t + nwaves < ntiles) {
-			dcur = dnext;
-			if (dma)
-				issue(dcur);
-			dnext = ld_desc(t + 2 * nwaves);
-		}
+		dcur = dnext;
+		issue(dcur, t + nwaves < ntiles);
+		dnext = ld_desc(t + 2 * nwaves);
 
 		const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
 		const uint32_t len = dv.z;
 		const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
-		const bool staged = dma && active && len >= 14 && (uint64_t)len <= a.usize &&
-				    eff <= a.usize - len && !(eff & 15) &&
-				    eff + 64 <= ((a.usize + 15) & ~15ull);
+		const bool staged = dma & active & (len >= 14) & ((uint64_t)len <= a.usize) &
+				    (eff <= a.usize - len) & !(eff & 15) &
+				    (eff + 64 <= ((a.usize + 15) & ~15ull));
 
-		/* 2. fast-shape classification.  r[j] = frame dword j + nv */
-		uint32_t nv = 0;
-		if (le_is_vlan(F[3] & 0xffff)) {
-			nv = 1;
-			if (le_is_vlan(F[4] & 0xffff))
-				nv = 2;
-		}
+		/* 2. fast-shape classification, branch free (bitwise &/| on
+		 * flags, selects).  r[j] = frame dword j + nv */
+		const bool v1 = le_is_vlan(F[3] & 0xffff);
+		const bool v2 = v1 & le_is_vlan(F[4] & 0xffff);
+		const uint32_t nv = (uint32_t)v1 + (uint32_t)v2;
+		/* masks, not selects: a select chain over F is turned into a
+		 * dynamically indexed private array (scratch) by the compiler */
+		const uint32_t m2 = 0u - (uint32_t)v2;
+		const uint32_t m1 = (0u - (uint32_t)v1) & ~m2;
+		const uint32_t m0 = ~(m1 | m2);
 		uint32_t r[16];
 #pragma unroll
 		for (int j = 3; j < 16; j++)
-			r[j] = nv == 0 ? F[j] : nv == 1 ? F[j + 1] : F[j + 2];
+			r[j] = (F[j] & m0) | (F[j + 1] & m1) | (F[j + 2] & m2);
 		const uint32_t l3 = 14 + 4 * nv, l4 = l3 + 20;
 		const uint32_t tot = bswap16(r[4] & 0xffff);
 		const uint32_t proto = r[5] >> 24;
 		const bool udp = proto == 17;
-		uint32_t cl;
-		bool fast = !a.force_generic && staged &&
-			    (r[3] & 0x00ffffffu) == 0x00450008u &&
-			    (r[5] & 0xff3fu) == 0 && (udp || proto == 6) &&
-			    tot >= 20 && l3 + tot <= len;
-		if (udp) {
-			cl = bswap16(r[9] >> 16);
-			fast = fast && len >= l4 + 8 && cl >= 8 && l4 + cl <= l3 + tot;
-		} else {
-			const uint32_t thl = ((r[11] >> 20) & 0xf) * 4;
-			cl = tot - 20;
-			fast = fast && len >= l4 + 20 && thl >= 20 && l4 + thl <= len &&
-			       cl >= thl;
-		}
+		const uint32_t thl = ((r[11] >> 20) & 0xf) * 4;
+		const uint32_t cl = udp ? bswap16(r[9] >> 16) : tot - 20;
+		const bool ok_udp = (len >= l4 + 8) & (cl >= 8) & (l4 + cl <= l3 + tot);
+		const bool ok_tcp = (len >= l4 + 20) & (thl >= 20) & (l4 + thl <= len) &
+				    (cl >= thl);
+		bool fast = (!a.force_generic) & staged &
+			    ((r[3] & 0x00ffffffu) == 0x00450008u) &
+			    ((r[5] & 0xff3fu) == 0) & (udp | (proto == 6)) &
+			    (tot >= 20) & (l3 + tot <= len) & (udp ? ok_udp : ok_tcp);
 		/* a checksum range (with udp_csum's odd over-read byte) that ends
 		 * past the window: the bulk kernel adds the payload sum */
 		const bool shape = fast;
-		fast = shape && l4 + cl + (cl & 1) <= 64u;
-		const bool bulk = shape && !fast && a.res;
+		fast = shape & (l4 + cl + (cl & 1) <= 64u);
+		const bool bulk = shape & !fast & (a.res != nullptr);
 
 		/* 3. defer the frames of other shapes to the exception list and
 		 * the long ones to the bulk list of this wave */
@@ -1516,8 +1512,8 @@ uint32_t rx_grid_blocks(uint32_t n, uint32_t max_blocks)
 }
 
 /* Kernel variants selectable by cfg.tune (diagnostic A/B): bits 0-7 =
- * waves per SIMD the fast kernel's register allocation is held to (0 =
- * compiler's choice), bit 9 = every frame through the exception kernel,
+ * waves per SIMD the fast kernel's register allocation is held to (0:
+ * compiler's choice, 6, 8), bit 9 = every frame through the exception kernel,
  * bits 10-11 = bulk-kernel variant. */
 /* Blocks of a kernel resident at once on the device (occupancy x CUs). */
 template <auto KERN>
@@ -1557,7 +1553,8 @@ static hipError_t launch_resident(const RxArgs &a, uint32_t cap,
 
 template <int WIN, int MINW>
 static hipError_t launch_sized(RxArgs a, uint32_t max_blocks,
-			       hipStream_t stream, uint32_t bulk_variant)
+			       hipStream_t stream, uint32_t bulk_variant,
+			       hipEvent_t *ev)
 {
 	uint32_t cap = resident_blocks<xdp_rx_kernel<MINW>>();
 	if (cap < max_blocks)
@@ -1565,11 +1562,15 @@ static hipError_t launch_sized(RxArgs a, uint32_t max_blocks,
 	const uint32_t blocks = rx_grid_blocks(a.n, max_blocks);
 	a.xregion = rx_xregion(a.n, blocks);
 	a.nregions = blocks * kWavesPerBlock;
+	if (ev)
+		(void)hipEventRecord(ev[0], stream);
 	hipLaunchKernelGGL((xdp_rx_kernel<MINW>), dim3(blocks),
 			   dim3(kBlock), 0, stream, a);
 	hipError_t e = hipGetLastError();
 	if (e != hipSuccess)
 		return e;
+	if (ev)
+		(void)hipEventRecord(ev[1], stream);
 	/* at most one wave per (region, batch) */
 	const uint64_t items = (uint64_t)a.nregions * (a.xregion / kWave);
 	const uint32_t icap = (uint32_t)((items + kWavesPerBlock - 1) / kWavesPerBlock);
@@ -1588,7 +1589,12 @@ static hipError_t launch_sized(RxArgs a, uint32_t max_blocks,
 	}
 	if (e != hipSuccess)
 		return e;
-	return launch_resident<xdp_rx_generic_kernel<WIN>>(a, icap, stream);
+	if (ev)
+		(void)hipEventRecord(ev[2], stream);
+	e = launch_resident<xdp_rx_generic_kernel<WIN>>(a, icap, stream);
+	if (ev && e == hipSuccess)
+		(void)hipEventRecord(ev[3], stream);
+	return e;
 }
 
 uint32_t rx_xregion(uint32_t n, uint32_t blocks)
@@ -1599,19 +1605,19 @@ uint32_t rx_xregion(uint32_t n, uint32_t blocks)
 }
 
 hipError_t launch_rx(const RxArgs &a, uint32_t window, uint32_t max_blocks,
-		     hipStream_t stream, uint32_t tune)
+		     hipStream_t stream, uint32_t tune, hipEvent_t *ev)
 {
 	const uint32_t waves = tune & 0xff;
 	/* bits 10-11: bulk-kernel loads per lane and step (0: 2 non-temporal,
 	 * 1: 2, 2: 4 non-temporal, 3: 4) */
 	const uint32_t bu = (tune >> 10) & 3;
 	if (window == 128)
-		return launch_sized<128, 1>(a, max_blocks, stream, bu);
+		return launch_sized<128, 1>(a, max_blocks, stream, bu, ev);
 	if (waves == 6)
-		return launch_sized<64, 6>(a, max_blocks, stream, bu);
+		return launch_sized<64, 6>(a, max_blocks, stream, bu, ev);
 	if (waves == 8)
-		return launch_sized<64, 8>(a, max_blocks, stream, bu);
-	return launch_sized<64, 1>(a, max_blocks, stream, bu);
+		return launch_sized<64, 8>(a, max_blocks, stream, bu, ev);
+	return launch_sized<64, 1>(a, max_blocks, stream, bu, ev);
 }
 
 /* ------------------------------------------------------------------ */

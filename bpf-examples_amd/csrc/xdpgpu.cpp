@@ -57,6 +57,9 @@ struct xdpgpu_ctx {
 	bool pinned = false;
 	uint8_t *d_umem = nullptr;       /* device mirror                  */
 	uint8_t *d_umem_mapped = nullptr; /* device view of pinned host UMEM */
+	/* XDPGPU_CFG_TIMING: 4 events per recorded launch */
+	hipEvent_t *tev = nullptr;
+	uint32_t tn = 0;
 	char err[256];
 };
 
@@ -135,6 +138,12 @@ void xdpgpu_fini(xdpgpu_ctx *ctx)
 	(void)hipDeviceSynchronize();
 	for (uint32_t i = 0; i < kSlots; i++)
 		free_slot(ctx->slot[i]);
+	if (ctx->tev) {
+		for (uint32_t i = 0; i < 4 * XDPGPU_TIMING_MAX; i++)
+			if (ctx->tev[i])
+				(void)hipEventDestroy(ctx->tev[i]);
+		delete[] ctx->tev;
+	}
 	if (ctx->d_umem)
 		(void)hipFree(ctx->d_umem);
 	if (ctx->pinned)
@@ -184,6 +193,16 @@ int xdpgpu_init(const xdpgpu_cfg *cfg, xdpgpu_ctx **out)
 			    hipMalloc(&s.d_stats, stat_bytes) != hipSuccess ||
 			    hipMemset(s.d_stats, 0, stat_bytes) != hipSuccess)
 				rc = set_err(ctx, -ENOMEM, "slot %u allocation failed", i);
+		}
+		if (!rc && (cfg->flags & XDPGPU_CFG_TIMING)) {
+			ctx->tev = new (std::nothrow) hipEvent_t[4 * XDPGPU_TIMING_MAX]();
+			if (!ctx->tev) {
+				rc = set_err(ctx, -ENOMEM, "timing events");
+				break;
+			}
+			for (uint32_t i = 0; i < 4 * XDPGPU_TIMING_MAX && !rc; i++)
+				if (hipEventCreate(&ctx->tev[i]) != hipSuccess)
+					rc = set_err(ctx, -ENOMEM, "timing event %u", i);
 		}
 	} while (0);
 	if (rc) {
@@ -299,8 +318,36 @@ static int enqueue_rx(xdpgpu_ctx *ctx, Slot &s, uint8_t *d_umem, uint64_t usize,
 	a.blist = s.d_xlist + s.xcap;
 	a.bcount = s.d_xcount + kMaxRxBlocks * 4;
 	a.force_generic = (ctx->cfg.tune >> 9) & 1;
+	hipEvent_t *ev = nullptr;
+	if (ctx->tev && ctx->tn < XDPGPU_TIMING_MAX)
+		ev = ctx->tev + 4 * ctx->tn++;
 	HIP_TRY(ctx, launch_rx(a, ctx->cfg.window, ctx->max_blocks, stream,
-			       ctx->cfg.tune));
+			       ctx->cfg.tune, ev));
+	return 0;
+}
+
+int xdpgpu_kernel_times(xdpgpu_ctx *ctx, xdpgpu_ktimes *out)
+{
+	if (!ctx || !out)
+		return -EINVAL;
+	memset(out, 0, sizeof(*out));
+	if (!ctx->tev)
+		return set_err(ctx, -EINVAL, "context made without XDPGPU_CFG_TIMING");
+	HIP_TRY(ctx, hipSetDevice(ctx->cfg.device));
+	for (uint32_t k = 0; k < ctx->tn; k++) {
+		hipEvent_t *e = ctx->tev + 4 * k;
+		float t[3], all;
+		HIP_TRY(ctx, hipEventSynchronize(e[3]));
+		for (int j = 0; j < 3; j++)
+			HIP_TRY(ctx, hipEventElapsedTime(&t[j], e[j], e[j + 1]));
+		HIP_TRY(ctx, hipEventElapsedTime(&all, e[0], e[3]));
+		out->fast_ms += t[0];
+		out->bulk_ms += t[1];
+		out->exception_ms += t[2];
+		out->total_ms += all;
+	}
+	out->launches = ctx->tn;
+	ctx->tn = 0;
 	return 0;
 }
 

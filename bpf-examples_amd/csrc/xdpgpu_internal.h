@@ -49,8 +49,10 @@ struct RxArgs {
 	uint32_t force_generic;    /* 1: defer every frame (diagnostic)     */
 };
 
+/* ev (nullable): four events recorded before the fast kernel and after
+ * each of the fast, bulk and exception kernels */
 hipError_t launch_rx(const RxArgs &a, uint32_t window, uint32_t max_blocks,
-		     hipStream_t stream, uint32_t tune);
+		     hipStream_t stream, uint32_t tune, hipEvent_t *ev);
 uint32_t rx_grid_blocks(uint32_t n, uint32_t max_blocks);
 uint32_t rx_xregion(uint32_t n, uint32_t blocks);
 hipError_t launch_ceiling(const RxArgs &a, uint32_t blocks, hipStream_t stream);

@@ -38,6 +38,7 @@ VERDICT_NAMES = ("ABORTED", "DROP", "PASS", "TX", "REDIRECT")
 
 CFG_VERIFY_CSUM = 0x1
 CFG_ICMP6_ECHO = 0x2
+CFG_TIMING = 0x8
 CFG_STATS = 0x4
 CFG_DEFAULT = CFG_VERIFY_CSUM | CFG_STATS
 
@@ -90,6 +91,12 @@ class Stats(C.Structure):
                 "l4_absent": self.l4_absent, "frag": self.frag}
 
 
+class KTimes(C.Structure):
+    _fields_ = [("launches", C.c_uint64), ("fast_ms", C.c_double),
+                ("bulk_ms", C.c_double), ("exception_ms", C.c_double),
+                ("total_ms", C.c_double)]
+
+
 class PoolSpec(C.Structure):
     _fields_ = [("kind", C.c_uint32), ("frame_size", C.c_uint32),
                 ("stride", C.c_uint32), ("headroom", C.c_uint32),
@@ -115,7 +122,8 @@ EXPORTS = (
     "xdpgpu_init", "xdpgpu_fini", "xdpgpu_register_umem", "xdpgpu_process",
     "xdpgpu_submit", "xdpgpu_wait", "xdpgpu_process_dev", "xdpgpu_stats",
     "xdpgpu_stats_reset", "xdpgpu_jhash_dev", "xdpgpu_ip_fast_csum_dev",
-    "xdpgpu_sync", "xdpgpu_ceiling_dev", "xdpgpu_device_count", "xdpgpu_last_error",
+    "xdpgpu_sync", "xdpgpu_ceiling_dev", "xdpgpu_kernel_times",
+    "xdpgpu_device_count", "xdpgpu_last_error",
     "xdpgpu_abi_version", "xdpgpu_pool_size", "xdpgpu_pool_generate",
     "xdpgpu_pool_spec_default",
 )
@@ -145,6 +153,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.xdpgpu_ip_fast_csum_dev.argtypes = [vp, vp, u32, u32, vp, vp]
     lib.xdpgpu_sync.argtypes = [vp, vp]
     lib.xdpgpu_ceiling_dev.argtypes = [vp, vp, u64, vp, u32, vp, vp, vp, vp]
+    lib.xdpgpu_kernel_times.argtypes = [vp, C.POINTER(KTimes)]
     lib.xdpgpu_device_count.argtypes = []
     lib.xdpgpu_last_error.argtypes = [vp]
     lib.xdpgpu_last_error.restype = C.c_char_p
@@ -299,6 +308,17 @@ class XdpGpu:
 
     def stats_reset(self) -> None:
         self._check(self.lib.xdpgpu_stats_reset(self.h), "xdpgpu_stats_reset")
+
+    def kernel_times(self) -> dict:
+        """Per-kernel HIP-event times of the launches since the last call
+        (context made with CFG_TIMING); averages in ms per launch."""
+        t = KTimes()
+        self._check(self.lib.xdpgpu_kernel_times(self.h, C.byref(t)),
+                    "xdpgpu_kernel_times")
+        n = max(t.launches, 1)
+        return {"launches": t.launches, "fast_ms": t.fast_ms / n,
+                "bulk_ms": t.bulk_ms / n, "exception_ms": t.exception_ms / n,
+                "total_ms": t.total_ms / n}
 
 
 def pool_spec(kind: int = POOL_UDP4, frame_size: int = 64, seed: int = 0x5EED0002,

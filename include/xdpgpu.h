@@ -112,6 +112,7 @@ struct xdpgpu_network_tuple {
 #define XDPGPU_CFG_VERIFY_CSUM 0x1 /* bad checksum -> XDP_DROP (xdp_synproxy_kern.c:610-623) */
 #define XDPGPU_CFG_ICMP6_ECHO  0x2 /* process_packet echo responder (af_xdp_user.c:968-1040)  */
 #define XDPGPU_CFG_STATS       0x4 /* keep per-verdict counters (xdpgpu_stats)                */
+#define XDPGPU_CFG_TIMING      0x8 /* record HIP events around each RX kernel (diagnostic)     */
 #define XDPGPU_CFG_DEFAULT     (XDPGPU_CFG_VERIFY_CSUM | XDPGPU_CFG_STATS)
 
 struct xdpgpu_cfg {
@@ -208,6 +209,21 @@ int xdpgpu_ceiling_dev(struct xdpgpu_ctx *ctx, const void *d_umem,
 		       uint64_t umem_size, const struct xdpgpu_desc *d_descs,
 		       uint32_t n, uint8_t *d_verdict, void *d_res,
 		       void *d_tuples, void *stream);
+
+/* Diagnostic (XDPGPU_CFG_TIMING): RX launches recorded since the last call
+ * and the summed durations of their three kernels (fast, bulk, exception)
+ * from HIP events on the launch stream.  Waits for the recorded work;
+ * resets the record.  At most XDPGPU_TIMING_MAX launches are kept between
+ * calls (later ones are not recorded). */
+#define XDPGPU_TIMING_MAX 1024
+struct xdpgpu_ktimes {
+	uint64_t launches;
+	double fast_ms;
+	double bulk_ms;
+	double exception_ms;
+	double total_ms;     /* first event to last event, summed per launch */
+};
+int xdpgpu_kernel_times(struct xdpgpu_ctx *ctx, struct xdpgpu_ktimes *out);
 
 /* Wait for all work of the context (or of stream if non-NULL). */
 int xdpgpu_sync(struct xdpgpu_ctx *ctx, void *stream);

@@ -1,5 +1,6 @@
 #!/bin/bash
-# One gpurun session: smoke -> pytest -m gpu -> bench -> rocprofv3 stats.
+# One gpurun session: smoke -> pytest -m gpu -> bench -> rocprofv3 stats
+# -> PMC passes -> host-path (end-to-end) bench.
 # Each GPU step has its own time limit; a crash/abort/timeout (anything but
 # exit 0 or a plain Python failure 1) ends the session immediately.
 set -u
@@ -27,5 +28,7 @@ for s in $STEPS; do
 	prof)   cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 		step prof 600 rocprofv3 --kernel-trace --stats --output-format csv \
 			-d "$OUT/prof" -o run -- python3 bench.py --no-cpu --no-secondary --steps 20 ;;
+	pmc)    step pmc 900 env DEST=$OUT/pmc_summary.json bash tools/pmc_profile.sh ;;
+	e2e)    step e2e 600 python bench.py --no-cpu --no-secondary --steps 10 --e2e ;;
 	esac
 done

@@ -5,9 +5,10 @@ set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=${OUT:-gpurun_out/pmc}
 VARIANT=${VARIANT:-64:0}
+DEST=${DEST:-}
 mkdir -p $OUT
 export TMPDIR=/tmp
-CMD="python3 tools/tune_rx.py --variants ceil,$VARIANT --rounds 1 --reps 3"
+CMD="python3 tools/tune_rx.py --variants $VARIANT --rounds 1 --reps 3"
 i=0
 for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
 	   "SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE" \
@@ -19,4 +20,4 @@ for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD S
 	echo "== pass $i rc=$rc"
 	if [ $rc -ne 0 ]; then tail -20 $OUT/p$i.log; exit $rc; fi
 done
-python3 tools/pmc_summary.py $OUT
+python3 tools/pmc_summary.py $OUT $DEST

@@ -12,7 +12,10 @@ import sys
 from collections import defaultdict
 
 
-def main(out):
+RX = ("xdp_rx_kernel", "xdp_rx_bulk_kernel", "xdp_rx_generic_kernel")
+
+
+def main(out, dest=None, frames=16 << 20, size=64):
     acc = defaultdict(lambda: defaultdict(list))
     for f in glob.glob(os.path.join(out, "p*", "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
@@ -38,7 +41,23 @@ def main(out):
     print(json.dumps(summary, indent=1))
     with open(os.path.join(out, "summary.json"), "w") as fh:
         json.dump(summary, fh, indent=1)
+    # bench.py form: HBM bytes per RX launch = sum over the three kernels
+    rx = {k: v for k, v in summary.items()
+          if any(k.split("<")[0].split("(")[0].endswith(r) for r in RX)}
+    tot = sum(v.get("hbm_bytes_per_launch", 0.0) for v in rx.values())
+    doc = {"workload": f"config2 pool: {frames} x {size} B IPv4/UDP "
+                       "(tools/tune_rx.py, V4 tuples)",
+           "frames": frames, "frame_size": size,
+           "method": "rocprofv3 --pmc, one counter group per pass; "
+                     "bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 "
+                     "(gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md HBM)",
+           "hbm_bytes_per_launch": tot if rx else None,
+           "per_kernel": summary}
+    if dest:
+        with open(dest, "w") as fh:
+            json.dump(doc, fh, indent=1)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc")
+    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc",
+         sys.argv[2] if len(sys.argv) > 2 else None)
