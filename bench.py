@@ -36,6 +36,7 @@ sys.path.insert(0, os.path.join(ROOT, "bpf-examples_amd"))
 import torch  # noqa: E402  (before libxdpgpu: one HIP runtime)
 import torch.distributed as dist  # noqa: E402
 
+import shard  # noqa: E402
 import xdpgpu  # noqa: E402
 
 BYTES_PER_FRAME = 16 + 64 + 16 + 16 + 1   # desc + frame + result + tuple + verdict
@@ -175,7 +176,7 @@ def main():
     t = time.time()
     n = args.frames
     umem, descs, expect = xdpgpu.pool_generate(n, xdpgpu.POOL_UDP4, args.size,
-                                               0x5EED0002 + rank)
+                                               shard.shard_seed(0x5EED0002, rank))
     log(f"[rank {rank}] pool {n} x {args.size} B generated in {time.time() - t:.1f} s")
     d_umem = to_dev(umem, dev)
     d_desc = to_dev(descs, dev, 0)
@@ -192,15 +193,8 @@ def main():
     # correctness spot check of the timed outputs against the generator
     v = d_v.cpu().numpy()
     ok = bool(np.array_equal(v, expect))
-    wall_t = torch.tensor([wall], dtype=torch.float64, device=dev)
-    frames_t = torch.tensor([float(n) * args.steps], dtype=torch.float64, device=dev)
-    ok_t = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(frames_t, op=dist.ReduceOp.SUM)
-        dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
-    wall_max = float(wall_t.item())
-    total_frames = float(frames_t.item())
+    # max time / summed frames over ranks (no data-path collective)
+    wall_max, total_frames, all_ok = shard.reduce_timing(wall, n * args.steps, ok, dev)
     mpps = total_frames / wall_max / 1e6
     gbps = total_frames * BYTES_PER_FRAME / wall_max / 1e9
     achieved = BYTES_PER_FRAME * n / (kms * 1e-3) / 1e9
@@ -291,7 +285,7 @@ def main():
                          "bytes_per_frame": BYTES_PER_FRAME,
                          "algorithmic_bytes_per_launch": BYTES_PER_FRAME * n},
             "cpu_baseline": cpu,
-            "verdicts_ok": bool(ok_t.item() > 0),
+            "verdicts_ok": all_ok,
         }
         line.update(secondary)
         if e2e:

@@ -1,0 +1,71 @@
+# SPDX-License-Identifier: GPL-2.0
+"""The N > 1 path on CPU: two gloo ranks, each owning a contiguous shard of
+one pool (shard.py), process it (oracle as the stand-in for the device
+path: these tests check the split and the reductions, not the kernels) and
+reduce counters and timing as bench.py does.  The reduced counters must
+equal one pass over the whole pool."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import oracle
+import shard
+import xdpgpu
+
+torch = pytest.importorskip("torch")
+
+N_TOTAL = 20011            # odd: ranks get unequal shares
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _rank_main(rank, world, port, out_dir):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    umem, descs, _ = xdpgpu.pool_generate(N_TOTAL, xdpgpu.POOL_IMIX, 64, 0x5EED0003)
+    lo, hi = shard.shard_range(N_TOTAL, world, rank)
+    _, _, _, st = oracle.process(umem.copy(), np.ascontiguousarray(descs[lo:hi]), 0x5, 0, 1)
+    st = dict(st)
+    st["verdict"] = dict(zip(shard.VERDICT_NAMES, st["verdict"]))
+    tot = shard.reduce_stats(st)
+    secs, frames, ok = shard.reduce_timing(0.5 + rank, hi - lo, rank != 7)
+    if rank == 0:
+        np.save(os.path.join(out_dir, "tot.npy"), np.array(shard.stats_vector(tot)))
+        np.save(os.path.join(out_dir, "timing.npy"), np.array([secs, frames, ok]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shard_range_covers_pool():
+    for world in (1, 2, 3, 8):
+        spans = [shard.shard_range(N_TOTAL, world, r) for r in range(world)]
+        assert spans[0][0] == 0 and spans[-1][1] == N_TOTAL
+        assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+        sizes = [h - l for l, h in spans]
+        assert max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        shard.shard_range(10, 2, 2)
+
+
+def test_two_rank_gloo_reduction(tmp_path):
+    import torch.multiprocessing as mp
+    world = 2
+    mp.spawn(_rank_main, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    got = shard.stats_from_vector(np.load(tmp_path / "tot.npy"))
+    umem, descs, _ = xdpgpu.pool_generate(N_TOTAL, xdpgpu.POOL_IMIX, 64, 0x5EED0003)
+    _, _, _, want = oracle.process(umem.copy(), descs, 0x5, 0, 1)
+    for k in shard.STAT_KEYS:
+        assert got[k] == want[k], k
+    assert [got["verdict"][v] for v in shard.VERDICT_NAMES] == want["verdict"]
+    secs, frames, ok = np.load(tmp_path / "timing.npy")
+    assert secs == 1.5 and frames == N_TOTAL and ok == 1.0
