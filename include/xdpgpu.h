@@ -153,7 +153,7 @@ int xdpgpu_init(const struct xdpgpu_cfg *cfg, struct xdpgpu_ctx **out);
 void xdpgpu_fini(struct xdpgpu_ctx *ctx);
 
 /* Register the host UMEM (replaces xsk_umem__create's buffer argument,
- * af_xdp_user.c:433 / xdpsock.c:1004).  The memory stays owned by the caller;
+ * af_xdp_user.c:433 / xdpsock.c:1013).  The memory stays owned by the caller;
  * it is pinned (hipHostRegister) and mirrored on the device. */
 int xdpgpu_register_umem(struct xdpgpu_ctx *ctx, void *base, uint64_t size,
 			 uint32_t chunk_size, uint32_t headroom, uint32_t flags);
