@@ -386,11 +386,8 @@ def check_against_reference(cs, umem, descs, verdict, res, tup_net):
                     fails.append(f"{name}: ipv6 pseudo arithmetic disagrees")
             if want != int(rr["l4_csum"]):
                 fails.append(f"{name}: l4_csum {int(rr['l4_csum']):#x} != ref {want:#x}")
-        # 3. flow hash with the reference's jhash over the 44-byte key
-        key = tup_net[i * 44:(i + 1) * 44].tobytes()
-        want = r.ref_jhash(oracle.buf(key), 44, 0xDEADBEEF)
-        if want != int(rr["hash"]) and False:
-            pass
+        # (the flow hash is pinned against the reference jhash by the
+        # caller, at the initval the NET-tuple run used)
     return fails
 
 
