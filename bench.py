@@ -13,7 +13,10 @@ max over ranks.  value = frames processed by all ranks / that time (Mpps,
 whole job).  The roofline figure is the algorithmic bytes of a launch
 (113 B/frame) over the launch's kernel time from HIP events
 recorded on the launch stream around each of the three kernels
-(xdpgpu_kernel_times); the per-kernel split is reported beside it.  traffic
+(xdpgpu_kernel_times), in a second pass of K launches on a context with
+XDPGPU_CFG_TIMING so the events do not perturb the timed steps; the
+per-kernel split is reported beside it (the event packets add a few us per
+kernel, so the split is conservative).  traffic
 is the HBM bytes per launch from the committed rocprofv3 PMC summary
 (profiles/r01_pmc.json, tools/pmc_profile.sh).  The CPU baseline is the
 oracle (oracle/xdp_oracle.c, a restatement of the reference C) timed on this
@@ -59,12 +62,11 @@ def to_dev(a: np.ndarray, dev, pad: int = 64) -> torch.Tensor:
 
 def time_device(ctx, d_umem, usize, d_desc, n, d_v, d_res, d_tup, stream,
                 steps, warmup, world):
-    """W untimed + K timed launches; returns (wall seconds, per-kernel
-    average ms from the HIP events the library records on the stream)."""
+    """W untimed + K timed launches between barrier + synchronize; returns
+    wall seconds."""
     for _ in range(warmup):
         ctx.process_dev(d_umem, usize, d_desc, n, d_v, d_res, d_tup, stream)
     torch.cuda.synchronize()
-    ctx.kernel_times()                       # drop the warm-up records
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -75,7 +77,21 @@ def time_device(ctx, d_umem, usize, d_desc, n, d_v, d_res, d_tup, stream,
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
-    return t1 - t0, ctx.kernel_times()
+    return t1 - t0
+
+
+def kernel_breakdown(tctx, d_umem, usize, d_desc, n, d_v, d_res, d_tup, stream,
+                     steps):
+    """Per-kernel average ms from the HIP events the library records on the
+    launch stream around each kernel (a context with CFG_TIMING; a pass of
+    its own, so the events do not perturb the timed steps)."""
+    tctx.process_dev(d_umem, usize, d_desc, n, d_v, d_res, d_tup, stream)
+    torch.cuda.synchronize()
+    tctx.kernel_times()
+    for _ in range(steps):
+        tctx.process_dev(d_umem, usize, d_desc, n, d_v, d_res, d_tup, stream)
+    torch.cuda.synchronize()
+    return tctx.kernel_times()
 
 
 def cpu_baseline(umem, descs, budget_s: float = 10.0):
@@ -126,8 +142,9 @@ def kt_round(kt: dict) -> dict:
     return {k: (round(v, 4) if isinstance(v, float) else v) for k, v in kt.items()}
 
 
-def side_run(ctx, dev, stream, n, kind, size, seed, fmt, steps, label, bpf_fn):
-    """One secondary workload: pool, K timed launches, verdict check."""
+def side_run(ctx, tctx, dev, stream, n, kind, size, seed, fmt, steps, label, bpf_fn):
+    """One secondary workload: pool, K timed launches, kernel split,
+    verdict check."""
     u, ds, ex = xdpgpu.pool_generate(n, kind, size, seed)
     g_umem = to_dev(u, dev)
     g_desc = to_dev(ds, dev, 0)
@@ -135,15 +152,18 @@ def side_run(ctx, dev, stream, n, kind, size, seed, fmt, steps, label, bpf_fn):
     g_v = torch.empty(n, dtype=torch.uint8, device=dev)
     g_res = torch.empty(n * 16, dtype=torch.uint8, device=dev)
     g_tup = torch.empty(n * tb, dtype=torch.uint8, device=dev)
-    w, kt = time_device(ctx, g_umem, u.nbytes, g_desc, n, g_v, g_res, g_tup,
-                        stream, steps, 2, 1)
+    w = time_device(ctx, g_umem, u.nbytes, g_desc, n, g_v, g_res, g_tup,
+                    stream, steps, 2, 1)
+    kt = kernel_breakdown(tctx, g_umem, u.nbytes, g_desc, n, g_v, g_res, g_tup,
+                          stream, steps)
     ok = bool(np.array_equal(g_v.cpu().numpy(), ex))
     algo = bpf_fn(ds)
     out = {"workload": label, "frames": n,
            "mpps": round(n * steps / w / 1e6, 1),
            "algorithmic_bytes_per_launch": int(algo),
-           "gbps": round(algo / (kt["total_ms"] * 1e-3) / 1e9, 1),
-           "roofline_frac": round(algo / (kt["total_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "ms_per_launch": round(w / steps * 1e3, 4),
+           "gbps": round(algo / w * steps / 1e9, 1),
+           "roofline_frac": round(algo / w * steps / 1e9 / HBM_PEAK_GBS, 4),
            "kernel_ms": kt_round(kt), "verdicts_ok": ok}
     del g_umem, g_desc, g_v, g_res, g_tup
     torch.cuda.empty_cache()
@@ -183,12 +203,15 @@ def main():
     d_v = torch.empty(n, dtype=torch.uint8, device=dev)
     d_res = torch.empty(n * 16, dtype=torch.uint8, device=dev)
     d_tup = torch.empty(n * 16, dtype=torch.uint8, device=dev)
-    ctx = xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT | xdpgpu.CFG_TIMING, 0,
-                        xdpgpu.TUPLE_V4, args.window)
+    ctx = xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT, 0, xdpgpu.TUPLE_V4, args.window)
+    tctx = xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT | xdpgpu.CFG_TIMING, 0,
+                         xdpgpu.TUPLE_V4, args.window)
     stream = torch.cuda.Stream(dev)
 
-    wall, kt = time_device(ctx, d_umem, umem.nbytes, d_desc, n, d_v, d_res, d_tup,
-                           stream, args.steps, args.warmup, world)
+    wall = time_device(ctx, d_umem, umem.nbytes, d_desc, n, d_v, d_res, d_tup,
+                       stream, args.steps, args.warmup, world)
+    kt = kernel_breakdown(tctx, d_umem, umem.nbytes, d_desc, n, d_v, d_res, d_tup,
+                          stream, args.steps)
     kms = kt["total_ms"]
     # correctness spot check of the timed outputs against the generator
     v = d_v.cpu().numpy()
@@ -208,19 +231,21 @@ def main():
         steps2 = max(5, args.steps // 5)
         # 1500 B frames (BASELINE metric names both sizes), config 2 geometry
         secondary["secondary_1500B"] = side_run(
-            ctx, dev, stream, 2 << 20, xdpgpu.POOL_UDP4, 1500, 0x5EED0012,
+            ctx, tctx, dev, stream, 2 << 20, xdpgpu.POOL_UDP4, 1500, 0x5EED0012,
             xdpgpu.TUPLE_V4, steps2, "config2-geometry 2M x 1500B IPv4/UDP, V4 tuple",
             lambda ds: len(ds) * (16 + 16 + 16 + 1) + int(ds["len"].astype(np.int64).sum()))
         # config 3: IMIX with the 44 B network_tuple (429.3 B/frame)
-        ctx3 = xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT | xdpgpu.CFG_TIMING, 0,
-                             xdpgpu.TUPLE_NET, 64)
+        ctx3 = xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT, 0, xdpgpu.TUPLE_NET, 64)
+        tctx3 = xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT | xdpgpu.CFG_TIMING, 0,
+                              xdpgpu.TUPLE_NET, 64)
         secondary["config3_imix"] = side_run(
-            ctx3, dev, stream, args.imix_frames, xdpgpu.POOL_IMIX, 64, 0x5EED0003,
+            ctx3, tctx3, dev, stream, args.imix_frames, xdpgpu.POOL_IMIX, 64, 0x5EED0003,
             xdpgpu.TUPLE_NET, steps2,
             f"config3: {args.imix_frames} IMIX frames (64/570/1500 7:4:1, VLAN, IPv6), "
             "network_tuple",
             lambda ds: len(ds) * (16 + 16 + 44 + 1) + int(ds["len"].astype(np.int64).sum()))
         ctx3.close()
+        tctx3.close()
 
     e2e = None
     if args.e2e and rank == 0 and world == 1:
@@ -292,6 +317,7 @@ def main():
             line["e2e_host_path"] = e2e
         print(json.dumps(line), flush=True)
     ctx.close()
+    tctx.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -919,6 +919,30 @@ __device__ __forceinline__ void generic_batch(const RxArgs &a, uint32_t *win,
 	my_bytes += active ? len : 0;
 }
 
+/* Counters: a wave's uniform counts into the block's LDS slot, then the
+ * block's slot into its own global slot (one read-modify-write per block;
+ * xdpgpu_stats sums the slots).  Every thread of the block calls it. */
+__device__ __forceinline__ void block_stats_flush(const RxArgs &a,
+						  unsigned long long *blk_cnt,
+						  const uint32_t (&cnt)[CNT_FRAG + 1],
+						  uint64_t my_bytes, int lane)
+{
+	if (!a.stats)
+		return;
+	const uint64_t bytes = wave_sum64(my_bytes);
+	if (lane == 0) {
+		atomicAdd(&blk_cnt[CNT_BYTES], (unsigned long long)bytes);
+#pragma unroll
+		for (int k = 0; k <= CNT_FRAG; k++)
+			if (k != CNT_BYTES && cnt[k])
+				atomicAdd(&blk_cnt[k], (unsigned long long)cnt[k]);
+	}
+	__syncthreads();
+	if (threadIdx.x < CNT_SLOT && blk_cnt[threadIdx.x])
+		a.stats[(uint64_t)blockIdx.x * CNT_SLOT + threadIdx.x] +=
+			blk_cnt[threadIdx.x];
+}
+
 /* LE 16-bit loads of the VLAN TPIDs 0x8100 / 0x88A8 (parsing_helpers.h:75) */
 __device__ __forceinline__ bool le_is_vlan(uint32_t v)
 {
@@ -950,6 +974,131 @@ __device__ __forceinline__ uint4 ld_nt16(const void *p)
 }
 
 /*
+ * Bulk kernel: completes the fast-shape frames whose L4 checksum range runs
+ * past the 64-byte window, by summing frame bytes [64, end of range) (with
+ * udp_csum's over-read byte; zero past the UMEM) into the window sum the
+ * fast kernel left in the result record.
+ *
+ * Per batch of 64 listed frames the wave works as four quarter-waves: a
+ * quarter streams one frame at a time, 16 lanes x 16 B x U per step, and on finishing a frame takes the next unassigned one of the batch
+ * (dynamic, so long and short frames balance).  Per-lane partial sums go to
+ * LDS; lane f then adds frame f's 16 partials and completes its record.
+ * Frames are 16-byte aligned (a fast-shape condition), so absolute and
+ * frame-relative 16-bit words coincide.
+ */
+/* One batch of up to 64 bulk-list frames (bl[0..nb)), wave-wide: the
+ * quarter-wave payload streaming described above, then lane f completes
+ * frame f's record, verdict and counters.  meta: 64 uint4, part4: 256
+ * uint4 of this wave's LDS. */
+template <int U, bool NT>
+__device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
+					   uint4 *part4, int lane,
+					   const uint32_t *bl, uint32_t nb,
+					   uint32_t (&cnt)[CNT_FRAG + 1],
+					   uint64_t &my_bytes)
+{
+	uint32_t *part = reinterpret_cast<uint32_t *>(part4);
+	const uint32_t sub = lane & 15;
+	const bool act = (uint32_t)lane < nb;
+	const uint64_t i = bl[act ? lane : 0];
+	const uint4 dv = *reinterpret_cast<const uint4 *>(a.desc + i);
+	uint4 rv = *reinterpret_cast<const uint4 *>(a.res + i);
+	const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
+	const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
+	const uint32_t cl = rv.w >> 16;
+	const uint32_t l4 = ((rv.z >> 16) & 0xff) + 20;
+	uint64_t lim = eff + l4 + cl + (cl & 1);
+	lim = lim < a.usize ? lim : a.usize;
+	const uint64_t lo = eff + 64;
+	meta[lane] = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32),
+				(uint32_t)(lim > lo ? lim - lo : 0), 0);
+	__builtin_amdgcn_wave_barrier();
+
+	/* quarter-wave streaming with dynamic frame assignment */
+	uint32_t k = lane >> 4;            /* this quarter's frame */
+	uint32_t nxt = 4;                  /* next unassigned (uniform) */
+	bool live = k < nb;
+	uint4 m = meta[live ? k : 0];
+	uint64_t flo = ((uint64_t)m.y << 32) | m.x;
+	uint32_t fnb = m.z, o = 0, acc = 0;
+	while (__ballot(live)) {
+		uint4 v[U];
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const uint32_t ou = o + 256 * u + 16 * sub;
+			v[u] = make_uint4(0, 0, 0, 0);
+			if (live && ou < fnb)
+				v[u] = NT ? ld_nt16(a.umem + flo + ou)
+					  : *reinterpret_cast<const uint4 *>(a.umem + flo + ou);
+		}
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const uint32_t ou = o + 256 * u + 16 * sub;
+			if (ou + 16 > fnb && ou < fnb) {
+				const uint4 mk = chunk_keep(ou, 0, fnb);
+				v[u].x &= mk.x;
+				v[u].y &= mk.y;
+				v[u].z &= mk.z;
+				v[u].w &= mk.w;
+			}
+			acc += halves(v[u].x) + halves(v[u].y) + halves(v[u].z) +
+			       halves(v[u].w);
+		}
+		o += 256 * U;
+		const bool done = live && o >= fnb;
+		const uint64_t dq = __ballot(done && sub == 0);
+		if (dq) {
+			if (done) {
+				part[16 * k + sub] = acc;
+				acc = 0;
+				k = nxt + (uint32_t)__popcll(dq & ((1ull << (lane & ~15)) - 1));
+				live = k < nb;
+				m = meta[live ? k : 0];
+				flo = ((uint64_t)m.y << 32) | m.x;
+				fnb = m.z;
+				o = 0;
+			}
+			nxt += (uint32_t)__popcll(dq);
+		}
+	}
+	__builtin_amdgcn_wave_barrier();
+
+	/* lane f completes frame f: exact, a range is < 64 KiB + 64 B so
+	 * the raw sum of 16-bit halves fits 32 bits */
+	uint32_t t = 0;
+#pragma unroll
+	for (int j = 0; j < 4; j++) {
+		const uint4 x = part4[4 * lane + ((j + lane) & 3)];
+		t += x.x + x.y + x.z + x.w;
+	}
+	const uint32_t c4 = rv.w & 0xffff;
+	const uint32_t sum4 = fold16((uint64_t)(rv.y >> 16) + t);
+	const bool udp = ((rv.z >> 8) & 0xff) == 17;
+	const bool l3_ok = rv.z & XDPGPU_F_L3_OK;
+	const bool absent = udp && c4 == 0;
+	const bool l4_ok = absent || (~fold16((uint64_t)sum4 + c4) & 0xffff) == 0;
+	const bool drop = (a.flags & XDPGPU_CFG_VERIFY_CSUM) && (!l3_ok || !l4_ok);
+	if (act) {
+		rv.y = (rv.y & 0xffff) | ((~sum4 & 0xffff) << 16);
+		rv.z |= (l4_ok ? XDPGPU_F_L4_OK : 0u) |
+			(absent ? XDPGPU_F_L4_ABSENT : 0u);
+		rv.w = l4 | (cl << 16);
+		st_nt16(a.res + i, rv);
+		a.verdict[i] = (uint8_t)(drop ? XDPGPU_DROP : XDPGPU_REDIRECT);
+		my_bytes += dv.z;
+	}
+	if (a.stats) {
+		cnt[CNT_FRAMES] += __popcll(__ballot(act));
+		cnt[CNT_VERDICT0 + XDPGPU_DROP] += __popcll(__ballot(act && drop));
+		cnt[CNT_VERDICT0 + XDPGPU_REDIRECT] += __popcll(__ballot(act && !drop));
+		cnt[CNT_L3_BAD] += __popcll(__ballot(act && !l3_ok));
+		cnt[CNT_L4_BAD] += __popcll(__ballot(act && !l4_ok));
+		cnt[CNT_L4_ABSENT] += __popcll(__ballot(act && absent));
+	}
+	__builtin_amdgcn_wave_barrier();
+}
+
+/*
  * Fast kernel, 64-byte header windows staged by LDS-DMA.
  *
  * Per wave and tile of 64 frames: the 256 16-byte chunks of the windows go
@@ -967,7 +1116,7 @@ __device__ __forceinline__ uint4 ld_nt16(const void *p)
  * payload sum here and go to the bulk list; every other frame is deferred
  * to the exception kernel.
  */
-template <int MINW>
+template <int MINW, bool FB>
 __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 {
 	constexpr int XQ = 2 * kWave;      /* deferral queues per wave */
@@ -975,6 +1124,7 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 	__shared__ uint64_t dtab_all[kWavesPerBlock * kWave];
 	__shared__ uint32_t xq_all[kWavesPerBlock * XQ];
 	__shared__ uint32_t bq_all[kWavesPerBlock * XQ];
+	__shared__ uint4 meta_all[FB ? kWavesPerBlock * kWave : 1];
 	__shared__ unsigned long long blk_cnt[CNT_SLOT];
 
 	const int lane = threadIdx.x & (kWave - 1);
@@ -998,10 +1148,12 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 	/* queued / flushed deferrals (uniform): exception and bulk lists */
 	uint32_t xq_n = 0, xout = 0, bq_n = 0, bout = 0;
 
-	/* append the frames of the lanes with want set to a wave's list: LDS
-	 * queue in lane order, flushed to the list 64 entries at a time */
+	/* append the frames of the lanes with want set to a list: LDS queue
+	 * in lane order, flushed 64 entries at a time either to this wave's
+	 * region (ctr null) or to a device-wide compact list whose length ctr
+	 * counts (one atomic per 64 entries) */
 	auto defer = [&](bool want, uint64_t i, uint32_t *q, uint32_t &qn,
-			 uint32_t *gl, uint32_t &gout) {
+			 uint32_t *gl, uint32_t &gout, uint32_t *ctr) {
 		const uint64_t dm = __ballot(want);
 		if (!dm)
 			return;
@@ -1012,7 +1164,14 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 		qn += (uint32_t)__popcll(dm);
 		if (qn >= (uint32_t)kWave) {
 			__builtin_amdgcn_wave_barrier();
-			gl[gout + lane] = q[lane];
+			uint32_t at = gout;
+			if (ctr) {
+				uint32_t base = 0;
+				if (lane == 0)
+					base = atomicAdd(ctr, (uint32_t)kWave);
+				at = __builtin_amdgcn_readfirstlane(base);
+			}
+			gl[at + lane] = q[lane];
 			gout += kWave;
 			const uint32_t rest = q[kWave + lane];
 			__builtin_amdgcn_wave_barrier();
@@ -1129,8 +1288,8 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 
 		/* 3. defer the frames of other shapes to the exception list and
 		 * the long ones to the bulk list of this wave */
-		defer(active && !fast && !bulk, i, xq, xq_n, xl, xout);
-		defer(bulk, i, bq, bq_n, bl, bout);
+		defer(active && !fast && !bulk, i, xq, xq_n, xl, xout, nullptr);
+		defer(bulk, i, bq, bq_n, bl, bout, nullptr);
 
 		/* 4. fast frames: flow key, hash, tuple, checksums, verdict */
 		const uint32_t sa = (r[6] >> 16) | (r[7] << 16);
@@ -1215,25 +1374,26 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 		xl[xout + lane] = xq[lane];
 	if ((uint32_t)lane < bq_n)
 		bl[bout + lane] = bq[lane];
+	const uint32_t nbulk = bout + bq_n;
 	if (lane == 0) {
 		a.xcount[wgid] = xout + xq_n;
-		a.bcount[wgid] = bout + bq_n;
+		a.bcount[wgid] = nbulk;
 	}
 
-	if (a.stats) {
-		const uint64_t bytes = wave_sum64(my_bytes);
-		if (lane == 0) {
-			atomicAdd(&blk_cnt[CNT_BYTES], (unsigned long long)bytes);
-#pragma unroll
-			for (int k = 0; k <= CNT_FRAG; k++)
-				if (k != CNT_BYTES)
-					atomicAdd(&blk_cnt[k], (unsigned long long)cnt[k]);
+	/* fused bulk pass: this wave's own bulk list, read back after its
+	 * stores are done (agent-scope fence: L1 invalidated) */
+	if constexpr (FB) {
+		if (nbulk) {
+			__threadfence();
+			uint4 *meta = meta_all + wid * kWave;
+			for (uint32_t b = 0; b < nbulk; b += kWave)
+				bulk_batch<2, true>(a, meta, buf, lane, bl + b,
+						    nbulk - b < (uint32_t)kWave ? nbulk - b : kWave,
+						    cnt, my_bytes);
 		}
-		__syncthreads();
-		if (threadIdx.x < CNT_SLOT)
-			a.stats[(uint64_t)blockIdx.x * CNT_SLOT + threadIdx.x] +=
-				blk_cnt[threadIdx.x];
 	}
+
+	block_stats_flush(a, blk_cnt, cnt, my_bytes, lane);
 }
 
 
@@ -1253,19 +1413,7 @@ struct RegionWalk {
 	}
 };
 
-/*
- * Bulk kernel: completes the fast-shape frames whose L4 checksum range runs
- * past the 64-byte window, by summing frame bytes [64, end of range) (with
- * udp_csum's over-read byte; zero past the UMEM) into the window sum the
- * fast kernel left in the result record.
- *
- * Per batch of 64 listed frames the wave works as four quarter-waves: a
- * quarter streams one frame at a time, 16 lanes x 16 B x U per step, and on finishing a frame takes the next unassigned one of the batch
- * (dynamic, so long and short frames balance).  Per-lane partial sums go to
- * LDS; lane f then adds frame f's 16 partials and completes its record.
- * Frames are 16-byte aligned (a fast-shape condition), so absolute and
- * frame-relative 16-bit words coincide.
- */
+/* Bulk kernel: the bulk pass as a kernel of its own (cfg.tune bit 8). */
 template <int MINW, int U, bool NT>
 __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_bulk_kernel(RxArgs a)
 {
@@ -1277,135 +1425,23 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_bulk_kernel(RxArgs a)
 	const int wid = threadIdx.x / kWave;
 	uint4 *meta = meta_all + wid * kWave;
 	uint4 *part4 = part_all + wid * kWave * 4;
-	uint32_t *part = reinterpret_cast<uint32_t *>(part4);
 	if (threadIdx.x < CNT_SLOT)
 		blk_cnt[threadIdx.x] = 0;
 	__syncthreads();
 
 	const uint32_t nwaves = gridDim.x * kWavesPerBlock;
-	const uint32_t sub = lane & 15;
 	uint32_t cnt[CNT_FRAG + 1] = {};
 	uint64_t my_bytes = 0;
 	const RegionWalk w(a.nregions, nwaves, blockIdx.x * kWavesPerBlock + wid);
 	for (uint32_t r = w.first; r < a.nregions; r += w.rstep) {
-	const uint32_t count = a.bcount[r];
-	const uint32_t *bl = a.blist + (uint64_t)r * a.xregion;
-	for (uint32_t b = w.bfirst; b < count; b += w.bstep) {
-		const uint32_t nb = count - b < (uint32_t)kWave ? count - b : kWave;
-		const bool act = (uint32_t)lane < nb;
-		const uint64_t i = bl[b + (act ? lane : 0)];
-		const uint4 dv = *reinterpret_cast<const uint4 *>(a.desc + i);
-		uint4 rv = *reinterpret_cast<const uint4 *>(a.res + i);
-		const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
-		const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
-		const uint32_t cl = rv.w >> 16;
-		const uint32_t l4 = ((rv.z >> 16) & 0xff) + 20;
-		uint64_t lim = eff + l4 + cl + (cl & 1);
-		lim = lim < a.usize ? lim : a.usize;
-		const uint64_t lo = eff + 64;
-		meta[lane] = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32),
-					(uint32_t)(lim > lo ? lim - lo : 0), 0);
-		__builtin_amdgcn_wave_barrier();
-
-		/* quarter-wave streaming with dynamic frame assignment */
-		uint32_t k = lane >> 4;            /* this quarter's frame */
-		uint32_t nxt = 4;                  /* next unassigned (uniform) */
-		bool live = k < nb;
-		uint4 m = meta[live ? k : 0];
-		uint64_t flo = ((uint64_t)m.y << 32) | m.x;
-		uint32_t fnb = m.z, o = 0, acc = 0;
-		while (__ballot(live)) {
-			uint4 v[U];
-#pragma unroll
-			for (int u = 0; u < U; u++) {
-				const uint32_t ou = o + 256 * u + 16 * sub;
-				v[u] = make_uint4(0, 0, 0, 0);
-				if (live && ou < fnb)
-					v[u] = NT ? ld_nt16(a.umem + flo + ou)
-						  : *reinterpret_cast<const uint4 *>(a.umem + flo + ou);
-			}
-#pragma unroll
-			for (int u = 0; u < U; u++) {
-				const uint32_t ou = o + 256 * u + 16 * sub;
-				if (ou + 16 > fnb && ou < fnb) {
-					const uint4 mk = chunk_keep(ou, 0, fnb);
-					v[u].x &= mk.x;
-					v[u].y &= mk.y;
-					v[u].z &= mk.z;
-					v[u].w &= mk.w;
-				}
-				acc += halves(v[u].x) + halves(v[u].y) + halves(v[u].z) +
-				       halves(v[u].w);
-			}
-			o += 256 * U;
-			const bool done = live && o >= fnb;
-			const uint64_t dq = __ballot(done && sub == 0);
-			if (dq) {
-				if (done) {
-					part[16 * k + sub] = acc;
-					acc = 0;
-					k = nxt + (uint32_t)__popcll(dq & ((1ull << (lane & ~15)) - 1));
-					live = k < nb;
-					m = meta[live ? k : 0];
-					flo = ((uint64_t)m.y << 32) | m.x;
-					fnb = m.z;
-					o = 0;
-				}
-				nxt += (uint32_t)__popcll(dq);
-			}
-		}
-		__builtin_amdgcn_wave_barrier();
-
-		/* lane f completes frame f: exact, a range is < 64 KiB + 64 B so
-		 * the raw sum of 16-bit halves fits 32 bits */
-		uint32_t t = 0;
-#pragma unroll
-		for (int j = 0; j < 4; j++) {
-			const uint4 x = part4[4 * lane + ((j + lane) & 3)];
-			t += x.x + x.y + x.z + x.w;
-		}
-		const uint32_t c4 = rv.w & 0xffff;
-		const uint32_t sum4 = fold16((uint64_t)(rv.y >> 16) + t);
-		const bool udp = ((rv.z >> 8) & 0xff) == 17;
-		const bool l3_ok = rv.z & XDPGPU_F_L3_OK;
-		const bool absent = udp && c4 == 0;
-		const bool l4_ok = absent || (~fold16((uint64_t)sum4 + c4) & 0xffff) == 0;
-		const bool drop = (a.flags & XDPGPU_CFG_VERIFY_CSUM) && (!l3_ok || !l4_ok);
-		if (act) {
-			rv.y = (rv.y & 0xffff) | ((~sum4 & 0xffff) << 16);
-			rv.z |= (l4_ok ? XDPGPU_F_L4_OK : 0u) |
-				(absent ? XDPGPU_F_L4_ABSENT : 0u);
-			rv.w = l4 | (cl << 16);
-			st_nt16(a.res + i, rv);
-			a.verdict[i] = (uint8_t)(drop ? XDPGPU_DROP : XDPGPU_REDIRECT);
-			my_bytes += dv.z;
-		}
-		if (a.stats) {
-			cnt[CNT_FRAMES] += __popcll(__ballot(act));
-			cnt[CNT_VERDICT0 + XDPGPU_DROP] += __popcll(__ballot(act && drop));
-			cnt[CNT_VERDICT0 + XDPGPU_REDIRECT] += __popcll(__ballot(act && !drop));
-			cnt[CNT_L3_BAD] += __popcll(__ballot(act && !l3_ok));
-			cnt[CNT_L4_BAD] += __popcll(__ballot(act && !l4_ok));
-			cnt[CNT_L4_ABSENT] += __popcll(__ballot(act && absent));
-		}
-		__builtin_amdgcn_wave_barrier();
+		const uint32_t count = a.bcount[r];
+		const uint32_t *bl = a.blist + (uint64_t)r * a.xregion;
+		for (uint32_t b = w.bfirst; b < count; b += w.bstep)
+			bulk_batch<U, NT>(a, meta, part4, lane, bl + b,
+					  count - b < (uint32_t)kWave ? count - b : kWave,
+					  cnt, my_bytes);
 	}
-	}
-
-	if (a.stats) {
-		const uint64_t bytes = wave_sum64(my_bytes);
-		if (lane == 0) {
-			atomicAdd(&blk_cnt[CNT_BYTES], (unsigned long long)bytes);
-#pragma unroll
-			for (int k = 0; k <= CNT_FRAG; k++)
-				if (k != CNT_BYTES)
-					atomicAdd(&blk_cnt[k], (unsigned long long)cnt[k]);
-		}
-		__syncthreads();
-		if (threadIdx.x < CNT_SLOT)
-			a.stats[(uint64_t)blockIdx.x * CNT_SLOT + threadIdx.x] +=
-				blk_cnt[threadIdx.x];
-	}
+	block_stats_flush(a, blk_cnt, cnt, my_bytes, lane);
 }
 
 /* Exception kernel: the generic pipeline on the frames the fast kernel
@@ -1440,20 +1476,7 @@ __global__ __launch_bounds__(kBlock) void xdp_rx_generic_kernel(RxArgs a)
 		}
 	}
 
-	if (a.stats) {
-		const uint64_t bytes = wave_sum64(my_bytes);
-		if (lane == 0) {
-			atomicAdd(&blk_cnt[CNT_BYTES], (unsigned long long)bytes);
-#pragma unroll
-			for (int k = 0; k <= CNT_FRAG; k++)
-				if (k != CNT_BYTES)
-					atomicAdd(&blk_cnt[k], (unsigned long long)cnt[k]);
-		}
-		__syncthreads();
-		if (threadIdx.x < CNT_SLOT)
-			a.stats[(uint64_t)blockIdx.x * CNT_SLOT + threadIdx.x] +=
-				blk_cnt[threadIdx.x];
-	}
+	block_stats_flush(a, blk_cnt, cnt, my_bytes, lane);
 }
 
 /* Memory ceiling for the RX traffic pattern (diagnostic): the same
@@ -1513,8 +1536,9 @@ uint32_t rx_grid_blocks(uint32_t n, uint32_t max_blocks)
 
 /* Kernel variants selectable by cfg.tune (diagnostic A/B): bits 0-7 =
  * waves per SIMD the fast kernel's register allocation is held to (0:
- * compiler's choice, 6, 8), bit 9 = every frame through the exception kernel,
- * bits 10-11 = bulk-kernel variant. */
+ * compiler's choice, 6, 8), bit 8 = bulk pass fused into the fast kernel,
+ * bit 9 = every frame through the exception kernel, bits 10-11 = bulk-kernel
+ * variant. */
 /* Blocks of a kernel resident at once on the device (occupancy x CUs). */
 template <auto KERN>
 static uint32_t resident_blocks()
@@ -1551,12 +1575,12 @@ static hipError_t launch_resident(const RxArgs &a, uint32_t cap,
 	return hipGetLastError();
 }
 
-template <int WIN, int MINW>
+template <int WIN, int MINW, bool FB>
 static hipError_t launch_sized(RxArgs a, uint32_t max_blocks,
 			       hipStream_t stream, uint32_t bulk_variant,
 			       hipEvent_t *ev)
 {
-	uint32_t cap = resident_blocks<xdp_rx_kernel<MINW>>();
+	uint32_t cap = resident_blocks<xdp_rx_kernel<MINW, FB>>();
 	if (cap < max_blocks)
 		max_blocks = cap;
 	const uint32_t blocks = rx_grid_blocks(a.n, max_blocks);
@@ -1564,7 +1588,7 @@ static hipError_t launch_sized(RxArgs a, uint32_t max_blocks,
 	a.nregions = blocks * kWavesPerBlock;
 	if (ev)
 		(void)hipEventRecord(ev[0], stream);
-	hipLaunchKernelGGL((xdp_rx_kernel<MINW>), dim3(blocks),
+	hipLaunchKernelGGL((xdp_rx_kernel<MINW, FB>), dim3(blocks),
 			   dim3(kBlock), 0, stream, a);
 	hipError_t e = hipGetLastError();
 	if (e != hipSuccess)
@@ -1574,21 +1598,23 @@ static hipError_t launch_sized(RxArgs a, uint32_t max_blocks,
 	/* at most one wave per (region, batch) */
 	const uint64_t items = (uint64_t)a.nregions * (a.xregion / kWave);
 	const uint32_t icap = (uint32_t)((items + kWavesPerBlock - 1) / kWavesPerBlock);
-	switch (bulk_variant) {
-	case 1:
-		e = launch_resident<xdp_rx_bulk_kernel<8, 2, false>>(a, icap, stream);
-		break;
-	case 2:
-		e = launch_resident<xdp_rx_bulk_kernel<8, 4, true>>(a, icap, stream);
-		break;
-	case 3:
-		e = launch_resident<xdp_rx_bulk_kernel<8, 4, false>>(a, icap, stream);
-		break;
-	default:
-		e = launch_resident<xdp_rx_bulk_kernel<8, 2, true>>(a, icap, stream);
+	if constexpr (!FB) {
+		switch (bulk_variant) {
+		case 1:
+			e = launch_resident<xdp_rx_bulk_kernel<8, 2, false>>(a, icap, stream);
+			break;
+		case 2:
+			e = launch_resident<xdp_rx_bulk_kernel<8, 4, true>>(a, icap, stream);
+			break;
+		case 3:
+			e = launch_resident<xdp_rx_bulk_kernel<8, 4, false>>(a, icap, stream);
+			break;
+		default:
+			e = launch_resident<xdp_rx_bulk_kernel<8, 2, true>>(a, icap, stream);
+		}
+		if (e != hipSuccess)
+			return e;
 	}
-	if (e != hipSuccess)
-		return e;
 	if (ev)
 		(void)hipEventRecord(ev[2], stream);
 	e = launch_resident<xdp_rx_generic_kernel<WIN>>(a, icap, stream);
@@ -1611,13 +1637,17 @@ hipError_t launch_rx(const RxArgs &a, uint32_t window, uint32_t max_blocks,
 	/* bits 10-11: bulk-kernel loads per lane and step (0: 2 non-temporal,
 	 * 1: 2, 2: 4 non-temporal, 3: 4) */
 	const uint32_t bu = (tune >> 10) & 3;
+	/* bit 8: bulk pass fused into the fast kernel's tail (each wave sums
+	 * its own bulk list) instead of the bulk kernel */
+	if ((tune >> 8) & 1)
+		return launch_sized<64, 1, true>(a, max_blocks, stream, bu, ev);
 	if (window == 128)
-		return launch_sized<128, 1>(a, max_blocks, stream, bu, ev);
+		return launch_sized<128, 1, false>(a, max_blocks, stream, bu, ev);
 	if (waves == 6)
-		return launch_sized<64, 6>(a, max_blocks, stream, bu, ev);
+		return launch_sized<64, 6, false>(a, max_blocks, stream, bu, ev);
 	if (waves == 8)
-		return launch_sized<64, 8>(a, max_blocks, stream, bu, ev);
-	return launch_sized<64, 1>(a, max_blocks, stream, bu, ev);
+		return launch_sized<64, 8, false>(a, max_blocks, stream, bu, ev);
+	return launch_sized<64, 1, false>(a, max_blocks, stream, bu, ev);
 }
 
 /* ------------------------------------------------------------------ */

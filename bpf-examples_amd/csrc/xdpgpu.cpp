@@ -275,8 +275,10 @@ static int ensure_slot_buffers(xdpgpu_ctx *ctx, Slot &s, uint32_t n)
 static int ensure_xlist(xdpgpu_ctx *ctx, Slot &s, uint32_t n)
 {
 	const uint64_t need = (uint64_t)n + 64ull * 4 * kMaxRxBlocks + 64;
-	if (!s.d_xcount &&
-	    hipMalloc(&s.d_xcount, (size_t)kMaxRxBlocks * 4 * 2 * sizeof(uint32_t)) != hipSuccess)
+	/* per-wave exception and bulk counts */
+	const size_t cbytes = (size_t)kMaxRxBlocks * 4 * 2 * sizeof(uint32_t);
+	if (!s.d_xcount && (hipMalloc(&s.d_xcount, cbytes) != hipSuccess ||
+			    hipMemset(s.d_xcount, 0, cbytes) != hipSuccess))
 		return set_err(ctx, -ENOMEM, "exception counts");
 	if (s.xcap >= need)
 		return 0;

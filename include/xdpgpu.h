@@ -124,9 +124,9 @@ struct xdpgpu_cfg {
 	uint32_t window;        /* header bytes the exception path stages in
 				 * LDS: 64 or 128 (0: 64) */
 	uint32_t tune;          /* kernel variant (diagnostic): bits 0-7 waves per
-				 * SIMD, bit 8 reserved, bit 9 exception path
-				 * only, bits 10-11 bulk-kernel variant;
-				 * 0 = default */
+				 * SIMD, bit 8 bulk pass fused into the fast
+				 * kernel, bit 9 exception path only, bits
+				 * 10-11 bulk-kernel variant; 0 = default */
 	uint32_t rsvd;
 };
 

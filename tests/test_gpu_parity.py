@@ -27,9 +27,10 @@ def to_dev(a: np.ndarray, pad: int = 64):
     return t
 
 
-# kernel variants (cfg.tune): default kernels, every frame through the
-# exception kernel, 6-wave fast kernel with the 4-load plain bulk kernel
-TUNES = [0, 512, 6 | (3 << 10)]
+# kernel variants (cfg.tune): default, every frame through the exception
+# kernel, bulk pass fused into the fast kernel, 6-wave fast kernel with the
+# 4-load plain bulk kernel
+TUNES = [0, 512, 256, 6 | (3 << 10)]
 
 
 def run_dev(umem, descs, flags=0x5, initval=0, fmt=1, window=64, tune=0):
