@@ -692,6 +692,7 @@ template <int WIN>
 __device__ __forceinline__ void generic_batch(const RxArgs &a, uint32_t *win,
 					      uint64_t *dtab, int lane,
 					      uint64_t i, bool active,
+					      uint4 *yl, uint32_t *yc,
 					      uint32_t (&cnt)[CNT_FRAG + 1],
 					      uint64_t &my_bytes)
 {
@@ -745,9 +746,19 @@ __device__ __forceinline__ void generic_batch(const RxArgs &a, uint32_t *win,
 		}
 	}
 
-	const uint32_t ext_sum = ext_sums<WIN>(
-		a, L.st() == ST_GO && L.has_csum() && L.rhi() > (uint32_t)WIN,
-		eff, L.l4(), L.rhi(), L.chk(), L.c4(), lane);
+	/* a checksum range past the window: the payload sum is deferred to
+	 * the bulk kernel (yl entry), except for echo candidates, whose TX
+	 * verdict needs it here */
+	const bool echo_cand = (a.flags & XDPGPU_CFG_ICMP6_ECHO) &&
+			       L.nvlan() == 0 && L.ipv6() && len >= 62 &&
+			       F.b8(20) == 58 && F.b8(54) == 128;
+	const bool need_ext = L.st() == ST_GO && L.has_csum() &&
+			      L.rhi() > (uint32_t)WIN;
+	const bool ydef = need_ext && a.ydefer && a.res && !echo_cand &&
+			  L.rhi() < 65536u;
+	const uint32_t ext_sum = ext_sums<WIN>(a, need_ext && !ydef, eff, L.l4(),
+					       L.rhi(), L.chk(), L.c4(), lane);
+	uint32_t partial = 0;   /* ydef: the L4 sum without the payload part */
 
 	/* checksums, flow key, verdict */
 	uint32_t verdict = L.st() == ST_PASS ? XDPGPU_PASS : XDPGPU_ABORTED;
@@ -780,6 +791,7 @@ __device__ __forceinline__ void generic_batch(const RxArgs &a, uint32_t *win,
 				     F.win_sum(L.l3() + 8, L.l3() + 40);
 			}
 			/* ICMPv4: no pseudo header, ~do_csum(msg) */
+			partial = fold16(body + ph);
 			l4c = ~fold16(body + ph) & 0xffff;
 			l4_ok = (~fold16(body + c4 + ph) & 0xffff) == 0;
 			if (L.ipv4() && nh == 17 && c4 == 0) {
@@ -799,9 +811,9 @@ __device__ __forceinline__ void generic_batch(const RxArgs &a, uint32_t *win,
 				flags |= XDPGPU_F_FRAG;
 			if (L.has_l4())
 				flags |= XDPGPU_F_L4;
-			if (L.has_csum() && l4_ok)
+			if (L.has_csum() && l4_ok && !ydef)
 				flags |= XDPGPU_F_L4_OK;
-			if (absent)
+			if (absent && !ydef)
 				flags |= XDPGPU_F_L4_ABSENT;
 			/* flow key: pping.h:120-139, v4 mapped as in
 			 * pping_kern.c:212-217 */
@@ -824,7 +836,7 @@ __device__ __forceinline__ void generic_batch(const RxArgs &a, uint32_t *win,
 		rec.x = jhash_key44(key, a.initval);
 		l3_bad = L.ipv4() && !l3_ok;
 		l4_bad = L.has_csum() && !l4_ok;
-		rec.y = l3c | (l4c << 16);
+		rec.y = l3c | ((ydef ? 0u : l4c) << 16);
 		rec.z = flags | ((ip ? nh : 0u) << 8) | (L.l3() << 16) |
 			(L.nvlan() << 24);
 		rec.w = ip ? (L.l4() | ((L.has_csum() ? cl : 0u) << 16)) : 0u;
@@ -877,9 +889,31 @@ __device__ __forceinline__ void generic_batch(const RxArgs &a, uint32_t *win,
 	}
 	const bool rec_live = verdict != XDPGPU_ABORTED && verdict != XDPGPU_PASS;
 
-	/* outputs */
+	/* deferred payload sums: entries appended to this region's list */
+	const uint64_t ym = __ballot(active && ydef);
+	if (ym) {
+		uint32_t base = 0;
+		if (lane == 0)
+			base = atomicAdd(yc, (uint32_t)__popcll(ym));
+		base = __builtin_amdgcn_readfirstlane(base);
+		if (active && ydef) {
+			const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+				(uint32_t)(ym >> 32),
+				__builtin_amdgcn_mbcnt_lo((uint32_t)ym, 0));
+			const uint32_t start = L.l4() > (uint32_t)WIN ? L.l4() : (uint32_t)WIN;
+			const bool chk_in = L.chk() >= (uint32_t)WIN;
+			const uint32_t fl = ((L.ipv4() && L.nh() == 17) ? 1u : 0u) |
+					    (chk_in ? 2u : 0u);
+			yl[base + rank] = make_uint4((uint32_t)i, partial | (L.c4() << 16),
+						     start | ((chk_in ? L.chk() : 0u) << 16),
+						     L.rhi() | (fl << 16));
+		}
+	}
+
+	/* outputs (a deferred frame's verdict is the bulk kernel's) */
 	if (active) {
-		a.verdict[i] = (uint8_t)verdict;
+		if (!ydef)
+			a.verdict[i] = (uint8_t)verdict;
 		if (a.res)
 			*reinterpret_cast<uint4 *>(a.res + i) = rec;
 		if (a.tup) {
@@ -904,19 +938,21 @@ __device__ __forceinline__ void generic_batch(const RxArgs &a, uint32_t *win,
 		}
 	}
 
-	/* counters: ballot + popcount */
+	/* counters: ballot + popcount (deferred frames: the bulk kernel) */
+	const bool own = active && !ydef;
+	const bool live = rec_live && !ydef;
 	if (a.stats) {
-		cnt[CNT_FRAMES] += __popcll(__ballot(active));
+		cnt[CNT_FRAMES] += __popcll(__ballot(own));
 #pragma unroll
 		for (int v = 0; v < 5; v++)
 			cnt[CNT_VERDICT0 + v] +=
-				__popcll(__ballot(active && verdict == (uint32_t)v));
-		cnt[CNT_L3_BAD] += __popcll(__ballot(rec_live && l3_bad));
-		cnt[CNT_L4_BAD] += __popcll(__ballot(rec_live && l4_bad));
-		cnt[CNT_L4_ABSENT] += __popcll(__ballot(rec_live && absent));
-		cnt[CNT_FRAG] += __popcll(__ballot(rec_live && L.frag()));
+				__popcll(__ballot(own && verdict == (uint32_t)v));
+		cnt[CNT_L3_BAD] += __popcll(__ballot(live && l3_bad));
+		cnt[CNT_L4_BAD] += __popcll(__ballot(live && l4_bad));
+		cnt[CNT_L4_ABSENT] += __popcll(__ballot(live && absent));
+		cnt[CNT_FRAG] += __popcll(__ballot(live && L.frag()));
 	}
-	my_bytes += active ? len : 0;
+	my_bytes += own ? len : 0;
 }
 
 /* Counters: a wave's uniform counts into the block's LDS slot, then the
@@ -986,32 +1022,46 @@ __device__ __forceinline__ uint4 ld_nt16(const void *p)
  * Frames are 16-byte aligned (a fast-shape condition), so absolute and
  * frame-relative 16-bit words coincide.
  */
-/* One batch of up to 64 bulk-list frames (bl[0..nb)), wave-wide: the
- * quarter-wave payload streaming described above, then lane f completes
- * frame f's record, verdict and counters.  meta: 64 uint4, part4: 256
- * uint4 of this wave's LDS. */
-template <int U, bool NT>
+/* One batch of up to 64 listed frames, wave-wide: the quarter-wave payload
+ * streaming described above, then lane f completes frame f's record,
+ * verdict and counters.  GEN false: fast-kernel bulk list (u32 indices,
+ * 16-byte aligned frames, range [64, end), window sum and check word in the
+ * result record).  GEN true: exception-kernel entries (xdpgpu ylist: index,
+ * partial sum | check word, range start | check offset, range end | flags;
+ * any alignment).  meta: 64 uint4, part4: 256 uint4 of this wave's LDS. */
+template <int U, bool NT, bool GEN>
 __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 					   uint4 *part4, int lane,
-					   const uint32_t *bl, uint32_t nb,
+					   const void *list, uint32_t nb,
 					   uint32_t (&cnt)[CNT_FRAG + 1],
 					   uint64_t &my_bytes)
 {
 	uint32_t *part = reinterpret_cast<uint32_t *>(part4);
 	const uint32_t sub = lane & 15;
 	const bool act = (uint32_t)lane < nb;
-	const uint64_t i = bl[act ? lane : 0];
+	uint4 ye = make_uint4(0, 0, 0, 0);
+	uint64_t i;
+	if constexpr (GEN) {
+		ye = reinterpret_cast<const uint4 *>(list)[act ? lane : 0];
+		i = ye.x;
+	} else {
+		i = reinterpret_cast<const uint32_t *>(list)[act ? lane : 0];
+	}
 	const uint4 dv = *reinterpret_cast<const uint4 *>(a.desc + i);
 	uint4 rv = *reinterpret_cast<const uint4 *>(a.res + i);
 	const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
 	const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
 	const uint32_t cl = rv.w >> 16;
-	const uint32_t l4 = ((rv.z >> 16) & 0xff) + 20;
-	uint64_t lim = eff + l4 + cl + (cl & 1);
+	const uint32_t l4 = GEN ? (rv.w & 0xffff) : ((rv.z >> 16) & 0xff) + 20;
+	const uint32_t rhi = GEN ? (ye.w & 0xffff) : l4 + cl + (cl & 1);
+	uint64_t lim = eff + rhi;
 	lim = lim < a.usize ? lim : a.usize;
-	const uint64_t lo = eff + 64;
-	meta[lane] = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32),
-				(uint32_t)(lim > lo ? lim - lo : 0), 0);
+	/* absolute range [lo, lim), streamed from its 16-byte aligned start */
+	const uint64_t lo = eff + (GEN ? (ye.z & 0xffff) : 64u);
+	const uint64_t lo_al = lo & ~15ull;
+	meta[lane] = make_uint4((uint32_t)lo_al, (uint32_t)(lo_al >> 32),
+				(uint32_t)(lim > lo ? lim - lo_al : 0),
+				(uint32_t)(lo - lo_al));
 	__builtin_amdgcn_wave_barrier();
 
 	/* quarter-wave streaming with dynamic frame assignment */
@@ -1020,7 +1070,7 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 	bool live = k < nb;
 	uint4 m = meta[live ? k : 0];
 	uint64_t flo = ((uint64_t)m.y << 32) | m.x;
-	uint32_t fnb = m.z, o = 0, acc = 0;
+	uint32_t fnb = m.z, fsk = m.w, o = 0, acc = 0;
 	while (__ballot(live)) {
 		uint4 v[U];
 #pragma unroll
@@ -1034,8 +1084,8 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 #pragma unroll
 		for (int u = 0; u < U; u++) {
 			const uint32_t ou = o + 256 * u + 16 * sub;
-			if (ou + 16 > fnb && ou < fnb) {
-				const uint4 mk = chunk_keep(ou, 0, fnb);
+			if ((ou + 16 > fnb || ou < fsk) && ou < fnb) {
+				const uint4 mk = chunk_keep(ou, fsk, fnb);
 				v[u].x &= mk.x;
 				v[u].y &= mk.y;
 				v[u].z &= mk.z;
@@ -1056,6 +1106,7 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 				m = meta[live ? k : 0];
 				flo = ((uint64_t)m.y << 32) | m.x;
 				fnb = m.z;
+				fsk = m.w;
 				o = 0;
 			}
 			nxt += (uint32_t)__popcll(dq);
@@ -1071,13 +1122,30 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 		const uint4 x = part4[4 * lane + ((j + lane) & 3)];
 		t += x.x + x.y + x.z + x.w;
 	}
-	const uint32_t c4 = rv.w & 0xffff;
-	const uint32_t sum4 = fold16((uint64_t)(rv.y >> 16) + t);
-	const bool udp = ((rv.z >> 8) & 0xff) == 17;
-	const bool l3_ok = rv.z & XDPGPU_F_L3_OK;
-	const bool absent = udp && c4 == 0;
+	uint32_t c4, sum4;
+	bool absent, l3_bad;
+	if constexpr (GEN) {
+		/* the exception kernel's ext_sums arithmetic: check word in
+		 * the range removed exactly, absolute vs frame-relative
+		 * parity */
+		c4 = ye.y >> 16;
+		if (ye.w & (2u << 16))
+			t -= (eff & 1) ? bswap16(c4) : c4;
+		uint32_t f = fold16(t);
+		if (eff & 1)
+			f = bswap16(f);
+		sum4 = fold16((uint64_t)(ye.y & 0xffff) + f);
+		absent = (ye.w & (1u << 16)) && c4 == 0;
+		l3_bad = (rv.z & XDPGPU_F_IP) && !(rv.z & XDPGPU_F_IPV6) &&
+			 !(rv.z & XDPGPU_F_L3_OK);
+	} else {
+		c4 = rv.w & 0xffff;
+		sum4 = fold16((uint64_t)(rv.y >> 16) + t);
+		absent = ((rv.z >> 8) & 0xff) == 17 && c4 == 0;
+		l3_bad = !(rv.z & XDPGPU_F_L3_OK);
+	}
 	const bool l4_ok = absent || (~fold16((uint64_t)sum4 + c4) & 0xffff) == 0;
-	const bool drop = (a.flags & XDPGPU_CFG_VERIFY_CSUM) && (!l3_ok || !l4_ok);
+	const bool drop = (a.flags & XDPGPU_CFG_VERIFY_CSUM) && (l3_bad || !l4_ok);
 	if (act) {
 		rv.y = (rv.y & 0xffff) | ((~sum4 & 0xffff) << 16);
 		rv.z |= (l4_ok ? XDPGPU_F_L4_OK : 0u) |
@@ -1091,9 +1159,11 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 		cnt[CNT_FRAMES] += __popcll(__ballot(act));
 		cnt[CNT_VERDICT0 + XDPGPU_DROP] += __popcll(__ballot(act && drop));
 		cnt[CNT_VERDICT0 + XDPGPU_REDIRECT] += __popcll(__ballot(act && !drop));
-		cnt[CNT_L3_BAD] += __popcll(__ballot(act && !l3_ok));
+		cnt[CNT_L3_BAD] += __popcll(__ballot(act && l3_bad));
 		cnt[CNT_L4_BAD] += __popcll(__ballot(act && !l4_ok));
 		cnt[CNT_L4_ABSENT] += __popcll(__ballot(act && absent));
+		if constexpr (GEN)
+			cnt[CNT_FRAG] += __popcll(__ballot(act && (rv.z & XDPGPU_F_FRAG)));
 	}
 	__builtin_amdgcn_wave_barrier();
 }
@@ -1116,7 +1186,7 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
  * payload sum here and go to the bulk list; every other frame is deferred
  * to the exception kernel.
  */
-template <int MINW, bool FB>
+template <int MINW>
 __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 {
 	constexpr int XQ = 2 * kWave;      /* deferral queues per wave */
@@ -1124,7 +1194,6 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 	__shared__ uint64_t dtab_all[kWavesPerBlock * kWave];
 	__shared__ uint32_t xq_all[kWavesPerBlock * XQ];
 	__shared__ uint32_t bq_all[kWavesPerBlock * XQ];
-	__shared__ uint4 meta_all[FB ? kWavesPerBlock * kWave : 1];
 	__shared__ unsigned long long blk_cnt[CNT_SLOT];
 
 	const int lane = threadIdx.x & (kWave - 1);
@@ -1374,23 +1443,10 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 		xl[xout + lane] = xq[lane];
 	if ((uint32_t)lane < bq_n)
 		bl[bout + lane] = bq[lane];
-	const uint32_t nbulk = bout + bq_n;
 	if (lane == 0) {
 		a.xcount[wgid] = xout + xq_n;
-		a.bcount[wgid] = nbulk;
-	}
-
-	/* fused bulk pass: this wave's own bulk list, read back after its
-	 * stores are done (agent-scope fence: L1 invalidated) */
-	if constexpr (FB) {
-		if (nbulk) {
-			__threadfence();
-			uint4 *meta = meta_all + wid * kWave;
-			for (uint32_t b = 0; b < nbulk; b += kWave)
-				bulk_batch<2, true>(a, meta, buf, lane, bl + b,
-						    nbulk - b < (uint32_t)kWave ? nbulk - b : kWave,
-						    cnt, my_bytes);
-		}
+		a.bcount[wgid] = bout + bq_n;
+		a.ycount[wgid] = 0;   /* filled by the exception kernel */
 	}
 
 	block_stats_flush(a, blk_cnt, cnt, my_bytes, lane);
@@ -1437,9 +1493,15 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_bulk_kernel(RxArgs a)
 		const uint32_t count = a.bcount[r];
 		const uint32_t *bl = a.blist + (uint64_t)r * a.xregion;
 		for (uint32_t b = w.bfirst; b < count; b += w.bstep)
-			bulk_batch<U, NT>(a, meta, part4, lane, bl + b,
-					  count - b < (uint32_t)kWave ? count - b : kWave,
-					  cnt, my_bytes);
+			bulk_batch<U, NT, false>(a, meta, part4, lane, bl + b,
+						 count - b < (uint32_t)kWave ? count - b : kWave,
+						 cnt, my_bytes);
+		const uint32_t ycount = a.ycount[r];
+		const uint4 *yl = a.ylist + (uint64_t)r * a.xregion;
+		for (uint32_t b = w.bfirst; b < ycount; b += w.bstep)
+			bulk_batch<U, NT, true>(a, meta, part4, lane, yl + b,
+						ycount - b < (uint32_t)kWave ? ycount - b : kWave,
+						cnt, my_bytes);
 	}
 	block_stats_flush(a, blk_cnt, cnt, my_bytes, lane);
 }
@@ -1472,7 +1534,9 @@ __global__ __launch_bounds__(kBlock) void xdp_rx_generic_kernel(RxArgs a)
 		for (uint32_t b = w.bfirst; b < count; b += w.bstep) {
 			const bool act = b + lane < count;
 			const uint64_t i = act ? xl[b + lane] : 0;
-			generic_batch<WIN>(a, win, dtab, lane, i, act, cnt, my_bytes);
+			generic_batch<WIN>(a, win, dtab, lane, i, act,
+					   a.ylist + (uint64_t)r * a.xregion,
+					   a.ycount + r, cnt, my_bytes);
 		}
 	}
 
@@ -1536,9 +1600,8 @@ uint32_t rx_grid_blocks(uint32_t n, uint32_t max_blocks)
 
 /* Kernel variants selectable by cfg.tune (diagnostic A/B): bits 0-7 =
  * waves per SIMD the fast kernel's register allocation is held to (0:
- * compiler's choice, 6, 8), bit 8 = bulk pass fused into the fast kernel,
- * bit 9 = every frame through the exception kernel, bits 10-11 = bulk-kernel
- * variant. */
+ * compiler's choice, 6, 8), bit 9 = every frame through the exception
+ * kernel (bulk pass off for it), bits 10-11 = bulk-kernel variant. */
 /* Blocks of a kernel resident at once on the device (occupancy x CUs). */
 template <auto KERN>
 static uint32_t resident_blocks()
@@ -1575,12 +1638,12 @@ static hipError_t launch_resident(const RxArgs &a, uint32_t cap,
 	return hipGetLastError();
 }
 
-template <int WIN, int MINW, bool FB>
+template <int WIN, int MINW>
 static hipError_t launch_sized(RxArgs a, uint32_t max_blocks,
 			       hipStream_t stream, uint32_t bulk_variant,
 			       hipEvent_t *ev)
 {
-	uint32_t cap = resident_blocks<xdp_rx_kernel<MINW, FB>>();
+	uint32_t cap = resident_blocks<xdp_rx_kernel<MINW>>();
 	if (cap < max_blocks)
 		max_blocks = cap;
 	const uint32_t blocks = rx_grid_blocks(a.n, max_blocks);
@@ -1588,7 +1651,7 @@ static hipError_t launch_sized(RxArgs a, uint32_t max_blocks,
 	a.nregions = blocks * kWavesPerBlock;
 	if (ev)
 		(void)hipEventRecord(ev[0], stream);
-	hipLaunchKernelGGL((xdp_rx_kernel<MINW, FB>), dim3(blocks),
+	hipLaunchKernelGGL((xdp_rx_kernel<MINW>), dim3(blocks),
 			   dim3(kBlock), 0, stream, a);
 	hipError_t e = hipGetLastError();
 	if (e != hipSuccess)
@@ -1598,26 +1661,24 @@ static hipError_t launch_sized(RxArgs a, uint32_t max_blocks,
 	/* at most one wave per (region, batch) */
 	const uint64_t items = (uint64_t)a.nregions * (a.xregion / kWave);
 	const uint32_t icap = (uint32_t)((items + kWavesPerBlock - 1) / kWavesPerBlock);
-	if constexpr (!FB) {
-		switch (bulk_variant) {
-		case 1:
-			e = launch_resident<xdp_rx_bulk_kernel<8, 2, false>>(a, icap, stream);
-			break;
-		case 2:
-			e = launch_resident<xdp_rx_bulk_kernel<8, 4, true>>(a, icap, stream);
-			break;
-		case 3:
-			e = launch_resident<xdp_rx_bulk_kernel<8, 4, false>>(a, icap, stream);
-			break;
-		default:
-			e = launch_resident<xdp_rx_bulk_kernel<8, 2, true>>(a, icap, stream);
-		}
-		if (e != hipSuccess)
-			return e;
-	}
+	e = launch_resident<xdp_rx_generic_kernel<WIN>>(a, icap, stream);
+	if (e != hipSuccess)
+		return e;
 	if (ev)
 		(void)hipEventRecord(ev[2], stream);
-	e = launch_resident<xdp_rx_generic_kernel<WIN>>(a, icap, stream);
+	switch (bulk_variant) {
+	case 1:
+		e = launch_resident<xdp_rx_bulk_kernel<8, 2, false>>(a, icap, stream);
+		break;
+	case 2:
+		e = launch_resident<xdp_rx_bulk_kernel<8, 4, true>>(a, icap, stream);
+		break;
+	case 3:
+		e = launch_resident<xdp_rx_bulk_kernel<8, 4, false>>(a, icap, stream);
+		break;
+	default:
+		e = launch_resident<xdp_rx_bulk_kernel<8, 2, true>>(a, icap, stream);
+	}
 	if (ev && e == hipSuccess)
 		(void)hipEventRecord(ev[3], stream);
 	return e;
@@ -1637,17 +1698,13 @@ hipError_t launch_rx(const RxArgs &a, uint32_t window, uint32_t max_blocks,
 	/* bits 10-11: bulk-kernel loads per lane and step (0: 2 non-temporal,
 	 * 1: 2, 2: 4 non-temporal, 3: 4) */
 	const uint32_t bu = (tune >> 10) & 3;
-	/* bit 8: bulk pass fused into the fast kernel's tail (each wave sums
-	 * its own bulk list) instead of the bulk kernel */
-	if ((tune >> 8) & 1)
-		return launch_sized<64, 1, true>(a, max_blocks, stream, bu, ev);
 	if (window == 128)
-		return launch_sized<128, 1, false>(a, max_blocks, stream, bu, ev);
+		return launch_sized<128, 1>(a, max_blocks, stream, bu, ev);
 	if (waves == 6)
-		return launch_sized<64, 6, false>(a, max_blocks, stream, bu, ev);
+		return launch_sized<64, 6>(a, max_blocks, stream, bu, ev);
 	if (waves == 8)
-		return launch_sized<64, 8, false>(a, max_blocks, stream, bu, ev);
-	return launch_sized<64, 1, false>(a, max_blocks, stream, bu, ev);
+		return launch_sized<64, 8>(a, max_blocks, stream, bu, ev);
+	return launch_sized<64, 1>(a, max_blocks, stream, bu, ev);
 }
 
 /* ------------------------------------------------------------------ */

@@ -38,6 +38,7 @@ struct Slot {
 	xdpgpu_result *d_res = nullptr;
 	uint8_t *d_tup = nullptr;
 	uint32_t *d_xlist = nullptr;  /* exception list (fast -> generic kernel) */
+	uint4 *d_ylist = nullptr;     /* exception payload sums (generic -> bulk) */
 	uint64_t xcap = 0;
 	uint32_t *d_xcount = nullptr;
 	bool busy = false;
@@ -123,6 +124,8 @@ static void free_slot(Slot &s)
 		(void)hipFree(s.d_xlist);
 	if (s.d_xcount)
 		(void)hipFree(s.d_xcount);
+	if (s.d_ylist)
+		(void)hipFree(s.d_ylist);
 	if (s.done)
 		(void)hipEventDestroy(s.done);
 	if (s.stream)
@@ -275,21 +278,24 @@ static int ensure_slot_buffers(xdpgpu_ctx *ctx, Slot &s, uint32_t n)
 static int ensure_xlist(xdpgpu_ctx *ctx, Slot &s, uint32_t n)
 {
 	const uint64_t need = (uint64_t)n + 64ull * 4 * kMaxRxBlocks + 64;
-	/* per-wave exception and bulk counts */
-	const size_t cbytes = (size_t)kMaxRxBlocks * 4 * 2 * sizeof(uint32_t);
+	/* per-wave exception, bulk and deferred-payload counts */
+	const size_t cbytes = (size_t)kMaxRxBlocks * 4 * 3 * sizeof(uint32_t);
 	if (!s.d_xcount && (hipMalloc(&s.d_xcount, cbytes) != hipSuccess ||
 			    hipMemset(s.d_xcount, 0, cbytes) != hipSuccess))
 		return set_err(ctx, -ENOMEM, "exception counts");
 	if (s.xcap >= need)
 		return 0;
-	if (s.d_xlist) {
+	if (s.d_xlist || s.d_ylist) {
 		(void)hipDeviceSynchronize();
 		(void)hipFree(s.d_xlist);
+		(void)hipFree(s.d_ylist);
 		s.d_xlist = nullptr;
+		s.d_ylist = nullptr;
 		s.xcap = 0;
 	}
-	if (hipMalloc(&s.d_xlist, 2 * need * sizeof(uint32_t)) != hipSuccess)
-		return set_err(ctx, -ENOMEM, "exception list of %llu entries",
+	if (hipMalloc(&s.d_xlist, 2 * need * sizeof(uint32_t)) != hipSuccess ||
+	    hipMalloc(&s.d_ylist, need * sizeof(uint4)) != hipSuccess)
+		return set_err(ctx, -ENOMEM, "deferral lists of %llu entries",
 			       (unsigned long long)need);
 	s.xcap = need;
 	return 0;
@@ -319,6 +325,9 @@ static int enqueue_rx(xdpgpu_ctx *ctx, Slot &s, uint8_t *d_umem, uint64_t usize,
 	a.xcount = s.d_xcount;
 	a.blist = s.d_xlist + s.xcap;
 	a.bcount = s.d_xcount + kMaxRxBlocks * 4;
+	a.ylist = s.d_ylist;
+	a.ycount = s.d_xcount + kMaxRxBlocks * 4 * 2;
+	a.ydefer = !((ctx->cfg.tune >> 8) & 1);
 	a.force_generic = (ctx->cfg.tune >> 9) & 1;
 	hipEvent_t *ev = nullptr;
 	if (ctx->tev && ctx->tn < XDPGPU_TIMING_MAX)
@@ -343,9 +352,9 @@ int xdpgpu_kernel_times(xdpgpu_ctx *ctx, xdpgpu_ktimes *out)
 		for (int j = 0; j < 3; j++)
 			HIP_TRY(ctx, hipEventElapsedTime(&t[j], e[j], e[j + 1]));
 		HIP_TRY(ctx, hipEventElapsedTime(&all, e[0], e[3]));
-		out->fast_ms += t[0];
-		out->bulk_ms += t[1];
-		out->exception_ms += t[2];
+		out->fast_ms += t[0];       /* launch order: fast, exception, bulk */
+		out->exception_ms += t[1];
+		out->bulk_ms += t[2];
 		out->total_ms += all;
 	}
 	out->launches = ctx->tn;

@@ -43,6 +43,11 @@ struct RxArgs {
 	uint32_t *blist;           /* bulk list (payload beyond the header
 				    * window), xregion per wave            */
 	uint32_t *bcount;          /* bulk frames per wave                  */
+	uint4 *ylist;              /* exception frames whose payload sum the
+				    * bulk kernel adds: 16 B entries,
+				    * xregion per fast-kernel wave region   */
+	uint32_t *ycount;          /* entries per region (atomic)           */
+	uint32_t ydefer;           /* exception kernel may defer payload sums */
 	uint32_t xregion;          /* set by the launcher: entries per wave
 				    * region of both lists                  */
 	uint32_t nregions;         /* set by the launcher: fast-kernel waves */
@@ -50,7 +55,7 @@ struct RxArgs {
 };
 
 /* ev (nullable): four events recorded before the fast kernel and after
- * each of the fast, bulk and exception kernels */
+ * each of the fast, exception and bulk kernels (launch order) */
 hipError_t launch_rx(const RxArgs &a, uint32_t window, uint32_t max_blocks,
 		     hipStream_t stream, uint32_t tune, hipEvent_t *ev);
 uint32_t rx_grid_blocks(uint32_t n, uint32_t max_blocks);

@@ -124,9 +124,10 @@ struct xdpgpu_cfg {
 	uint32_t window;        /* header bytes the exception path stages in
 				 * LDS: 64 or 128 (0: 64) */
 	uint32_t tune;          /* kernel variant (diagnostic): bits 0-7 waves per
-				 * SIMD, bit 8 bulk pass fused into the fast
-				 * kernel, bit 9 exception path only, bits
-				 * 10-11 bulk-kernel variant; 0 = default */
+				 * SIMD, bit 8 exception kernel keeps its
+				 * payload sums, bit 9 exception path only,
+				 * bits 10-11 bulk-kernel variant;
+				 * 0 = default */
 	uint32_t rsvd;
 };
 
@@ -211,7 +212,7 @@ int xdpgpu_ceiling_dev(struct xdpgpu_ctx *ctx, const void *d_umem,
 		       void *d_tuples, void *stream);
 
 /* Diagnostic (XDPGPU_CFG_TIMING): RX launches recorded since the last call
- * and the summed durations of their three kernels (fast, bulk, exception)
+ * and the summed durations of their three kernels (fast, exception, bulk)
  * from HIP events on the launch stream.  Waits for the recorded work;
  * resets the record.  At most XDPGPU_TIMING_MAX launches are kept between
  * calls (later ones are not recorded). */
