@@ -1,0 +1,710 @@
+// SPDX-License-Identifier: GPL-2.0
+/*
+ * nat64.hip - the nat64-bpf translator (nat64-bpf/nat64_kern.c) as a batch
+ * transform over UMEM frames on gfx950, BASELINE config 4.
+ *
+ * One lane per frame, 64 frames per wave-tile.  Frame bytes [-32, 96) (the
+ * 32 bytes in front hold an IPv4 -> IPv6 frame's grown header) are staged
+ * into a per-lane LDS row with transposed 16-byte loads (consecutive lanes
+ * read consecutive chunks of one frame), falling back to byte loads for
+ * frames that are not 16-byte aligned or sit at the UMEM edges.  The lane
+ * then follows nat64_handler (nat64_kern.c:875-890) on its row: parse,
+ * prefix and state checks, the new IP header, the ICMP rewrite and the
+ * incremental checksum updates, writing the translated header bytes back
+ * into the row.  Finally the rewritten span goes to HBM as dword stores
+ * (byte stores only where the frame is not 4-byte aligned or the span's
+ * edge is not).  Headers past the staged window (long IPv6 extension
+ * chains) are read from HBM.
+ *
+ * The static v6_state_map / v4_reversemap are open-addressing tables in
+ * HBM (32 B slots, linear probing), built by the host (xdpgpu.cpp).
+ *
+ * Checksum arithmetic: bpf_csum_diff and bpf_l4_csum_replace restated mod
+ * 0xffff (see oracle/nat64_oracle.c for the derivation): each update is
+ * c' = ~F((~c + delta) mod 0xffff), F(0) = 0xffff.
+ */
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "xdpgpu_internal.h"
+
+namespace xdpgpu {
+
+namespace {
+
+constexpr int kWaveN = 64;
+constexpr int kWavesN = 4;
+constexpr int kBlockN = kWaveN * kWavesN;
+constexpr int kRowDw = 33;        /* 128 B row + 4 B pad (bank spread) */
+constexpr int kFront = 32;        /* row byte 0 = frame byte -32 */
+constexpr int kWinEnd = 96;       /* staged frame bytes [-32, 96) */
+
+__device__ __forceinline__ uint32_t slot_hash(uint32_t a, uint32_t b, uint32_t c,
+					      uint32_t d)
+{
+	uint32_t h = a * 0x9E3779B1u ^ b * 0x85EBCA77u ^ c * 0xC2B2AE3Du ^
+		     d * 0x27D4EB2Fu;
+	h ^= h >> 15;
+	h *= 0x2C1B3C6Du;
+	h ^= h >> 13;
+	return h;
+}
+
+/* x mod 0xffff for x < 2^32 */
+__device__ __forceinline__ uint32_t mod_ffff(uint32_t x)
+{
+	x = (x & 0xffff) + (x >> 16);
+	x = (x & 0xffff) + (x >> 16);
+	return x == 0xffff ? 0 : x;
+}
+
+/* one bpf_l4_csum_replace on checksum c (LE u16 as stored) */
+__device__ __forceinline__ uint32_t csum_upd(uint32_t c, uint32_t delta)
+{
+	const uint32_t v = mod_ffff(mod_ffff(~c & 0xffff) + delta);
+	const uint32_t f = v ? v : 0xffff;
+	return ~f & 0xffff;
+}
+
+struct Row {
+	uint8_t *rb;          /* LDS row: rb[kFront + o] = frame byte o */
+	const uint8_t *g;     /* frame in HBM, for bytes past the window */
+
+	__device__ __forceinline__ uint32_t b(int o) const
+	{
+		return o < kWinEnd ? rb[kFront + o] : g[o];
+	}
+	__device__ __forceinline__ uint32_t be16(int o) const
+	{
+		return (b(o) << 8) | b(o + 1);
+	}
+	__device__ __forceinline__ uint32_t be32(int o) const
+	{
+		return (be16(o) << 16) | be16(o + 2);
+	}
+	__device__ __forceinline__ uint32_t le16(int o) const
+	{
+		return b(o) | (b(o + 1) << 8);
+	}
+	__device__ __forceinline__ void put(int o, uint32_t v) const
+	{
+		rb[kFront + o] = (uint8_t)v;
+	}
+	/* sum mod 0xffff of the LE 16-bit words of [o, o+n), n even */
+	__device__ __forceinline__ uint32_t words(int o, int n) const
+	{
+		uint32_t s = 0;
+		for (int k = 0; k < n; k += 2)
+			s += le16(o + k);
+		return mod_ffff(s);
+	}
+};
+
+/* bpf_csum_diff(from, .., to, ..) mod 0xffff from the two word sums */
+__device__ __forceinline__ uint32_t diff_mod(uint32_t from, uint32_t to)
+{
+	return mod_ffff(to + 0xffff - from);
+}
+
+/* bpf_l4_csum_replace at frame offset co of the row */
+__device__ __forceinline__ void row_csum(const Row &R, int co, uint32_t delta,
+					 bool mangled0)
+{
+	uint32_t c = R.le16(co);
+	if (mangled0 && c == 0)
+		return;
+	c = csum_upd(c, delta);
+	if (mangled0 && c == 0)
+		c = 0xffff;
+	R.put(co, c & 0xff);
+	R.put(co + 1, c >> 8);
+}
+
+/* sum of the (LE words of the) pseudo header of update_icmp_checksum
+ * (nat64_kern.c:120-158) from an IPv6 header at v6 bytes */
+__device__ __forceinline__ uint32_t icmp_ph_sum(const uint8_t *v6)
+{
+	uint32_t s = 0;
+	for (int k = 8; k < 40; k += 2)
+		s += v6[k] | (v6[k + 1] << 8);
+	s += v6[4] | (v6[5] << 8);        /* .len = payload_len (a __be16) */
+	s += 58u << 8;                    /* .nh, last byte */
+	return mod_ffff(s);
+}
+
+/* update_icmp_checksum: icmp header at frame offset h of the row (already
+ * rewritten), old[8] the original */
+__device__ __forceinline__ void icmp_csum(const Row &R, int h, const uint8_t *old,
+					  const uint8_t *v6, bool add)
+{
+	const uint32_t ph = icmp_ph_sum(v6);
+	const int co = h + 2;
+	row_csum(R, co, add ? ph : diff_mod(ph, 0), false);
+	const uint32_t hb = old[0] | (old[1] << 8), ha = R.le16(h);
+	row_csum(R, co, diff_mod(hb, ha), false);
+	const uint32_t ub = mod_ffff((old[4] | (old[5] << 8)) + (old[6] | (old[7] << 8)));
+	const uint32_t ua = mod_ffff(R.le16(h + 4) + R.le16(h + 6));
+	bool same = true;
+	for (int k = 4; k < 8; k++)
+		same = same && old[k] == R.b(h + k);
+	if (!same)
+		row_csum(R, co, diff_mod(ub, ua), false);
+}
+
+__device__ __forceinline__ void put_be32r(const Row &R, int o, uint32_t v)
+{
+	R.put(o, v >> 24);
+	R.put(o + 1, v >> 16);
+	R.put(o + 2, v >> 8);
+	R.put(o + 3, v);
+}
+
+/* rewrite_icmpv6 (nat64_kern.c:644-739) at frame offset h */
+__device__ bool rewrite_icmpv6(const Row &R, int h, const uint8_t *v6)
+{
+	uint8_t old[8];
+	for (int k = 0; k < 8; k++)
+		old[k] = (uint8_t)R.b(h + k);
+	uint32_t t = old[0], c = old[1], nt = t, nc = c;
+	switch (t) {
+	case 128: nt = 8; break;
+	case 129: nt = 0; break;
+	case 1:
+		nt = 3;
+		if (c == 0 || c == 2 || c == 3) nc = 1;
+		else if (c == 1) nc = 10;
+		else if (c == 4) nc = 3;
+		else return false;
+		break;
+	case 2: {
+		nt = 3;
+		nc = 4;
+		const uint32_t mtu = ((uint32_t)old[4] << 24 | (uint32_t)old[5] << 16 |
+				      (uint32_t)old[6] << 8 | old[7]) - 20;
+		if (mtu > 0xffff)
+			return false;
+		R.put(h + 6, mtu >> 8);
+		R.put(h + 7, mtu);
+		break;
+	}
+	case 3: nt = 11; break;
+	case 4:
+		if (c == 0) {
+			nt = 12;
+			nc = 0;
+			const uint32_t ptr = (uint32_t)old[4] << 24 | (uint32_t)old[5] << 16 |
+					     (uint32_t)old[6] << 8 | old[7];
+			uint32_t r;
+			if (ptr == 0 || ptr == 1) r = ptr;
+			else if (ptr == 4 || ptr == 5) r = 2;
+			else if (ptr == 6) r = 9;
+			else if (ptr == 7) r = 8;
+			else if (ptr >= 8 && ptr <= 23) r = 12;
+			else if (ptr >= 24 && ptr <= 39) r = 16;
+			else return false;
+			R.put(h + 4, r);
+		} else if (c == 1) {
+			nt = 3;
+			nc = 2;
+		} else {
+			return false;
+		}
+		break;
+	default:
+		return false;
+	}
+	R.put(h, nt);
+	R.put(h + 1, nc);
+	icmp_csum(R, h, old, v6, false);
+	return true;
+}
+
+/* rewrite_icmp (nat64_kern.c:325-441) at frame offset h */
+__device__ bool rewrite_icmp(const Row &R, int h, const uint8_t *v6)
+{
+	uint8_t old[8];
+	for (int k = 0; k < 8; k++)
+		old[k] = (uint8_t)R.b(h + k);
+	uint32_t t = old[0], c = old[1], nt = t, nc = c;
+	switch (t) {
+	case 8: nt = 128; break;
+	case 0: nt = 129; break;
+	case 3:
+		nt = 1;
+		switch (c) {
+		case 0: case 1: case 5: case 6: case 7: case 8: case 11: case 12:
+			nc = 0;
+			break;
+		case 2:
+			nt = 4;
+			nc = 1;
+			put_be32r(R, h + 4, 6);
+			break;
+		case 3: nc = 4; break;
+		case 4: {
+			nt = 2;
+			nc = 0;
+			uint32_t mtu = (((uint32_t)old[6] << 8) | old[7]) + 20;
+			if (mtu < 1280)
+				mtu = 1280;
+			put_be32r(R, h + 4, mtu);
+			break;
+		}
+		case 9: case 10: case 13: case 15: nc = 1; break;
+		default: return false;
+		}
+		break;
+	case 12: {
+		if (c == 1)
+			return false;
+		nt = 4;
+		nc = 0;
+		const uint32_t r = old[4];
+		uint32_t p;
+		if (r == 0) p = 0;
+		else if (r == 1) p = 1;
+		else if (r == 2 || r == 3) p = 4;
+		else if (r == 8) p = 7;
+		else if (r == 9) p = 6;
+		else if (r >= 12 && r <= 15) p = 8;
+		else if (r >= 16 && r <= 19) p = 24;
+		else return false;
+		put_be32r(R, h + 4, p);
+		break;
+	}
+	default:
+		return false;
+	}
+	R.put(h, nt);
+	R.put(h + 1, nc);
+	icmp_csum(R, h, old, v6, true);
+	return true;
+}
+
+/* RFC 6052 byte positions of the embedded IPv4 address per prefix length
+ * (v4addr_to_v6 / v6addr_to_v4, nat64_kern.c:180-323); pref_end is the
+ * number of prefix bytes kept (bytes [pref_end, 16) of the prefix are 0,
+ * except /64 keeps 8 and the u octet 8 is 0) */
+__device__ __forceinline__ bool v4pos(uint32_t plen, int (&pos)[4], int &pref_end)
+{
+	switch (plen) {
+	case 96: pos[0] = 12; pos[1] = 13; pos[2] = 14; pos[3] = 15; pref_end = 12; return true;
+	case 64: pos[0] = 9; pos[1] = 10; pos[2] = 11; pos[3] = 12; pref_end = 8; return true;
+	case 56: pos[0] = 7; pos[1] = 9; pos[2] = 10; pos[3] = 11; pref_end = 7; return true;
+	case 48: pos[0] = 6; pos[1] = 7; pos[2] = 9; pos[3] = 10; pref_end = 6; return true;
+	case 40: pos[0] = 5; pos[1] = 6; pos[2] = 7; pos[3] = 9; pref_end = 5; return true;
+	case 32: pos[0] = 4; pos[1] = 5; pos[2] = 6; pos[3] = 7; pref_end = 4; return true;
+	default: return false;
+	}
+}
+
+struct Tables {
+	const uint4 *v6map;    /* slots: {v6 w0..w3} then {v4, used, 0, 0} */
+	uint32_t v6mask;
+	const uint4 *v4map;    /* slots: {v4, used, 0, 0} then {v6 w0..w3} */
+	uint32_t v4mask;
+};
+
+/* v6_state_map lookup: v4 (host order) or 0 */
+__device__ uint32_t lookup_v6(const Tables &T, const uint32_t (&w)[4], bool &found)
+{
+	uint32_t s = slot_hash(w[0], w[1], w[2], w[3]) & T.v6mask;
+	for (uint32_t probe = 0; probe <= T.v6mask; probe++) {
+		const uint4 k = T.v6map[2 * s];
+		const uint4 v = T.v6map[2 * s + 1];
+		if (!v.y)
+			break;
+		if (k.x == w[0] && k.y == w[1] && k.z == w[2] && k.w == w[3]) {
+			found = true;
+			return v.x;
+		}
+		s = (s + 1) & T.v6mask;
+	}
+	found = false;
+	return 0;
+}
+
+__device__ bool lookup_v4(const Tables &T, uint32_t v4, uint32_t (&w)[4])
+{
+	uint32_t s = slot_hash(v4, 0, 0, 0) & T.v4mask;
+	for (uint32_t probe = 0; probe <= T.v4mask; probe++) {
+		const uint4 k = T.v4map[2 * s];
+		if (!k.y)
+			break;
+		if (k.x == v4) {
+			const uint4 v = T.v4map[2 * s + 1];
+			w[0] = v.x;
+			w[1] = v.y;
+			w[2] = v.z;
+			w[3] = v.w;
+			return true;
+		}
+		s = (s + 1) & T.v4mask;
+	}
+	return false;
+}
+
+struct Plan {
+	int lo, hi;       /* frame-relative span rewritten in the row */
+	int co;           /* extra 2-byte store (TCP checksum) or -1 */
+};
+
+/* nat64_handle_v6 (nat64_kern.c:741-873) */
+__device__ uint32_t handle_v6(const Row &R, uint32_t len, int l3,
+			      const Nat64Args &a, const Tables &T, Plan &P,
+			      int64_t &shift)
+{
+	if ((uint32_t)l3 + 40 > len || (R.b(l3) >> 4) != 6)
+		return XDPGPU_TC_ACT_OK;          /* parse_ip6hdr */
+	const uint32_t nexthdr = R.b(l3 + 6);
+	/* skip_ip6hdrext (parsing_helpers.h:139-172) */
+	int pos = l3 + 40;
+	int ip_type = -1;
+	uint32_t nh = nexthdr;
+	for (int k = 0; k < 6; k++) {
+		if ((uint32_t)pos + 2 > len)
+			break;
+		if (nh == 0 || nh == 60 || nh == 43 || nh == 135) {
+			const uint32_t n2 = R.b(pos);
+			pos += (R.b(pos + 1) + 1) * 8;
+			nh = n2;
+		} else if (nh == 51) {
+			const uint32_t n2 = R.b(pos);
+			pos += (R.b(pos + 1) + 2) * 4;
+			nh = n2;
+		} else if (nh == 44) {
+			nh = R.b(pos);
+			pos += 8;
+		} else {
+			ip_type = (int)nh;
+			break;
+		}
+	}
+	if (ip_type < 0)
+		return XDPGPU_TC_ACT_OK;
+	/* v6addr_to_v4 + prefix compare */
+	int p4[4], pend;
+	if (!v4pos(a.cfg.v6_plen, p4, pend))
+		return XDPGPU_TC_ACT_OK;
+	uint8_t d4[4];
+	for (int k = 0; k < 4; k++)
+		d4[k] = (uint8_t)R.b(l3 + 24 + p4[k]);
+	for (int k = 0; k < 16; k++) {
+		const uint32_t v = k < pend ? R.b(l3 + 24 + k) : 0u;
+		if (v != a.cfg.v6_prefix[k])
+			return XDPGPU_TC_ACT_OK;
+	}
+	if ((uint32_t)ip_type != nexthdr)
+		return XDPGPU_TC_ACT_SHOT;
+	const uint32_t dst = (uint32_t)d4[0] << 24 | (uint32_t)d4[1] << 16 |
+			     (uint32_t)d4[2] << 8 | d4[3];
+	if (!dst || (dst & 0xFF000000u) == 0x7F000000u || (dst & 0xF0000000u) == 0xE0000000u)
+		return XDPGPU_TC_ACT_SHOT;
+	/* allowed_v6_src: the single LPM entry */
+	if (!a.cfg.allow_plen)
+		return XDPGPU_TC_ACT_SHOT;
+	for (uint32_t bit = 0; bit < a.cfg.allow_plen; bit++) {
+		const uint32_t sh = 7 - (bit & 7);
+		if (((R.b(l3 + 8 + (bit >> 3)) >> sh) & 1) !=
+		    ((uint32_t)(a.cfg.allow_prefix[bit >> 3] >> sh) & 1))
+			return XDPGPU_TC_ACT_SHOT;
+	}
+	uint32_t w[4];
+	for (int k = 0; k < 4; k++)
+		w[k] = R.b(l3 + 8 + 4 * k) | R.b(l3 + 9 + 4 * k) << 8 |
+		       R.b(l3 + 10 + 4 * k) << 16 | R.b(l3 + 11 + 4 * k) << 24;
+	bool found;
+	const uint32_t src = lookup_v6(T, w, found);
+	if (!found)
+		return XDPGPU_NAT64_NO_STATE;
+
+	/* the original IPv6 header, kept for the checksum updates */
+	uint8_t v6[40];
+	for (int k = 0; k < 40; k++)
+		v6[k] = (uint8_t)R.b(l3 + k);
+	uint8_t h4[20];
+	h4[0] = 0x45;
+	h4[1] = (uint8_t)(((v6[0] & 0x0f) << 4) | (v6[1] >> 4));
+	const uint32_t tot = ((uint32_t)v6[4] << 8 | v6[5]) + 20;
+	h4[2] = (uint8_t)(tot >> 8);
+	h4[3] = (uint8_t)tot;
+	h4[4] = h4[5] = 0;
+	h4[6] = 0x40;
+	h4[7] = 0;
+	h4[8] = v6[7];
+	h4[9] = (uint8_t)nexthdr;
+	h4[10] = h4[11] = 0;
+	h4[12] = (uint8_t)(src >> 24);
+	h4[13] = (uint8_t)(src >> 16);
+	h4[14] = (uint8_t)(src >> 8);
+	h4[15] = (uint8_t)src;
+	for (int k = 0; k < 4; k++)
+		h4[16 + k] = d4[k];
+	const int l4 = l3 + 40;
+	P.co = -1;
+	int l4_end = l4;            /* rewritten L4 bytes [l4, l4_end) */
+	if (nexthdr == 58) {
+		if ((uint32_t)l4 + 8 > len || l4 + 8 > kWinEnd)
+			return XDPGPU_TC_ACT_SHOT;
+		if (!rewrite_icmpv6(R, l4, v6))
+			return XDPGPU_TC_ACT_SHOT;
+		h4[9] = 1;
+		l4_end = l4 + 8;
+	} else if (nexthdr == 6 || nexthdr == 17) {
+		const int co = l4 + (nexthdr == 6 ? 16 : 6);
+		if ((uint32_t)co + 2 <= len && co + 2 <= kWinEnd) {
+			uint32_t from = 0, to = 0;
+			for (int k = 8; k < 40; k += 2)
+				from += v6[k] | (v6[k + 1] << 8);
+			for (int k = 12; k < 20; k += 2)
+				to += h4[k] | (h4[k + 1] << 8);
+			row_csum(R, co, diff_mod(mod_ffff(from), mod_ffff(to)), nexthdr == 17);
+			if (nexthdr == 17)
+				l4_end = l4 + 8;
+			else
+				P.co = co;
+		}
+	}
+	/* csum_fold_helper(bpf_csum_diff(0, 0, hdr, 20, 0)) */
+	uint32_t s = 0;
+	for (int k = 0; k < 20; k += 2)
+		s += h4[k] | (h4[k + 1] << 8);
+	s = (s & 0xffff) + (s >> 16);
+	s = (s & 0xffff) + (s >> 16);
+	s = ~s & 0xffff;
+	h4[10] = (uint8_t)s;
+	h4[11] = (uint8_t)(s >> 8);
+	/* the L2 header moves 20 bytes forward (back to front: l3 may exceed
+	 * 20), h_proto = 0x0800, then the IPv4 header */
+	for (int k = l3 - 1; k >= 0; k--)
+		R.put(20 + k, R.b(k));
+	R.put(32, 0x08);
+	R.put(33, 0x00);
+	for (int k = 0; k < 20; k++)
+		R.put(20 + l3 + k, h4[k]);
+	P.lo = 20;
+	P.hi = l4_end > l3 + 40 ? l4_end : l3 + 40;
+	shift = 20;
+	return XDPGPU_TC_ACT_REDIRECT;
+}
+
+/* nat64_handle_v4 (nat64_kern.c:443-541) */
+__device__ uint32_t handle_v4(const Row &R, uint32_t len, int l3, uint64_t eff,
+			      const Nat64Args &a, const Tables &T, Plan &P,
+			      int64_t &shift)
+{
+	if ((uint32_t)l3 + 20 > len || (R.b(l3) >> 4) != 4)
+		return XDPGPU_TC_ACT_OK;          /* parse_iphdr */
+	const uint32_t ihl = (R.b(l3) & 0xf) * 4;
+	if (ihl < 20 || (uint32_t)l3 + ihl > len)
+		return XDPGPU_TC_ACT_OK;
+	const uint32_t dst = R.be32(l3 + 16);
+	if ((dst & a.cfg.v4_mask) != a.cfg.v4_prefix)
+		return XDPGPU_TC_ACT_OK;
+	if (ihl != 20 || (R.be16(l3 + 6) & ~0x4000u))
+		return XDPGPU_TC_ACT_SHOT;
+	uint32_t w[4];
+	if (!lookup_v4(T, dst, w))
+		return XDPGPU_TC_ACT_SHOT;
+	int p4[4], pend;
+	if (!v4pos(a.cfg.v6_plen, p4, pend))
+		return XDPGPU_TC_ACT_SHOT;
+	uint8_t v6[40];
+	for (int k = 0; k < 40; k++)
+		v6[k] = 0;
+	/* v4addr_to_v6: prefix bytes, then the address bytes */
+	const int keep = a.cfg.v6_plen == 64 ? 8 : pend;
+	for (int k = 0; k < keep; k++)
+		v6[8 + k] = a.cfg.v6_prefix[k];
+	for (int k = 0; k < 4; k++)
+		v6[8 + p4[k]] = (uint8_t)R.b(l3 + 12 + k);
+	for (int k = 0; k < 4; k++) {
+		v6[24 + 4 * k] = (uint8_t)w[k];
+		v6[25 + 4 * k] = (uint8_t)(w[k] >> 8);
+		v6[26 + 4 * k] = (uint8_t)(w[k] >> 16);
+		v6[27 + 4 * k] = (uint8_t)(w[k] >> 24);
+	}
+	const uint32_t tos = R.b(l3 + 1), proto = R.b(l3 + 9);
+	v6[0] = (uint8_t)(6 << 4 | ((tos & 0x70) >> 4));
+	v6[1] = (uint8_t)(tos << 4);
+	const uint32_t pl = (R.be16(l3 + 2) - 20) & 0xffff;
+	v6[4] = (uint8_t)(pl >> 8);
+	v6[5] = (uint8_t)pl;
+	v6[6] = (uint8_t)proto;
+	v6[7] = (uint8_t)R.b(l3 + 8);
+	if (eff < 20)
+		return XDPGPU_TC_ACT_SHOT;        /* no headroom to grow */
+	const int l4 = l3 + 20;
+	P.co = -1;
+	int l4_end = l4;
+	if (proto == 1) {
+		if ((uint32_t)l4 + 8 > len || l4 + 8 > kWinEnd)
+			return XDPGPU_TC_ACT_SHOT;
+		if (!rewrite_icmp(R, l4, v6))
+			return XDPGPU_TC_ACT_SHOT;
+		v6[6] = 58;
+		l4_end = l4 + 8;
+	} else if (proto == 6 || proto == 17) {
+		const int co = l4 + (proto == 6 ? 16 : 6);
+		if ((uint32_t)co + 2 <= len && co + 2 <= kWinEnd) {
+			uint32_t from = 0, to = 0;
+			for (int k = 12; k < 20; k += 2)
+				from += R.b(l3 + k) | (R.b(l3 + k + 1) << 8);
+			for (int k = 8; k < 40; k += 2)
+				to += v6[k] | (v6[k + 1] << 8);
+			row_csum(R, co, diff_mod(mod_ffff(from), mod_ffff(to)), proto == 17);
+			if (proto == 17)
+				l4_end = l4 + 8;
+			else
+				P.co = co;
+		}
+	}
+	/* the L2 header moves 20 bytes back, h_proto = 0x86DD, then the
+	 * IPv6 header */
+	for (int k = 0; k < l3; k++)
+		R.put(k - 20, R.b(k));
+	R.put(-8, 0x86);
+	R.put(-7, 0xDD);
+	for (int k = 0; k < 40; k++)
+		R.put(l3 - 20 + k, v6[k]);
+	P.lo = -20;
+	P.hi = l4_end > l4 ? l4_end : l4;
+	shift = -20;
+	return XDPGPU_TC_ACT_REDIRECT;
+}
+
+} // namespace
+
+__global__ __launch_bounds__(kBlockN) void xdp_nat64_kernel(Nat64Args a)
+{
+	__shared__ uint32_t rows_all[kWavesN * kWaveN * kRowDw];
+	__shared__ uint64_t dtab_all[kWavesN * kWaveN];
+	const int lane = threadIdx.x & (kWaveN - 1);
+	const int wid = threadIdx.x / kWaveN;
+	uint32_t *rows = rows_all + wid * kWaveN * kRowDw;
+	uint64_t *dtab = dtab_all + wid * kWaveN;
+	uint8_t *rb = reinterpret_cast<uint8_t *>(rows + lane * kRowDw);
+	const Tables T = {a.v6map, a.v6mask, a.v4map, a.v4mask};
+	const uint64_t us16 = (a.usize + 15) & ~15ull;
+
+	const uint64_t ntiles = ((uint64_t)a.n + kWaveN - 1) / kWaveN;
+	const uint64_t nwaves = (uint64_t)gridDim.x * kWavesN;
+	for (uint64_t t = (uint64_t)blockIdx.x * kWavesN + wid; t < ntiles; t += nwaves) {
+		const uint64_t i = t * kWaveN + lane;
+		const bool active = i < a.n;
+		const uint4 dv = active ? *reinterpret_cast<const uint4 *>(a.desc + i)
+					: make_uint4(0, 0, 0, 0);
+		const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
+		const uint32_t len = dv.z;
+		const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
+		const bool valid = active && (uint64_t)len <= a.usize && eff <= a.usize - len;
+
+		/* stage frame bytes [-32, 96): transposed 16-byte loads for
+		 * aligned frames with the whole span inside the UMEM */
+		const bool fastld = valid && !(eff & 15) && eff >= (uint64_t)kFront &&
+				    eff - kFront + 128 <= us16;
+		dtab[lane] = fastld ? eff - kFront : ~0ull;
+		__builtin_amdgcn_wave_barrier();
+#pragma unroll
+		for (int k = 0; k < 8; k++) {
+			const int q = k * kWaveN + lane;
+			const int f = q >> 3, c = q & 7;
+			const uint64_t base = dtab[f];
+			uint4 v = make_uint4(0, 0, 0, 0);
+			if (base != ~0ull)
+				v = *reinterpret_cast<const uint4 *>(a.umem + base + 16 * c);
+			uint32_t *dst = rows + f * kRowDw + 4 * c;
+			dst[0] = v.x;
+			dst[1] = v.y;
+			dst[2] = v.z;
+			dst[3] = v.w;
+		}
+		__builtin_amdgcn_wave_barrier();
+		if (valid && !fastld) {
+			for (int j = 0; j < 128; j++) {
+				const int64_t o = (int64_t)eff - kFront + j;
+				rb[j] = (o >= 0 && (uint64_t)o < a.usize) ? a.umem[o] : 0;
+			}
+		}
+
+		/* nat64_handler (nat64_kern.c:875-890) */
+		const Row R = {rb, a.umem + eff};
+		uint32_t act = valid ? XDPGPU_TC_ACT_OK : XDPGPU_TC_ACT_SHOT;
+		Plan P = {0, 0, -1};
+		int64_t shift = 0;
+		if (valid && len >= 14) {
+			/* parse_ethhdr (parsing_helpers.h:86-137) */
+			int l3 = 14;
+			uint32_t proto = R.be16(12);
+			for (int k = 0; k < 2; k++) {
+				if (proto != 0x8100 && proto != 0x88A8)
+					break;
+				if ((uint32_t)l3 + 4 > len)
+					break;
+				proto = R.be16(l3 + 2);
+				l3 += 4;
+			}
+			if (a.cfg.direction == XDPGPU_NAT64_EGRESS && proto == 0x0800)
+				act = handle_v4(R, len, l3, eff, a, T, P, shift);
+			else if (a.cfg.direction == XDPGPU_NAT64_INGRESS && proto == 0x86DD)
+				act = handle_v6(R, len, l3, a, T, P, shift);
+		}
+
+		/* write back the rewritten span [P.lo, P.hi) of the row (the
+		 * translated frame ends where the original did) and the TCP
+		 * checksum */
+		if (act == XDPGPU_TC_ACT_REDIRECT) {
+			const int hi = P.hi < (int)len ? P.hi : (int)len;
+			uint8_t *g = a.umem + eff;
+			int o = P.lo;
+			if (!(eff & 3)) {
+				for (; o + 4 <= hi; o += 4)
+					*reinterpret_cast<uint32_t *>(g + o) =
+						*reinterpret_cast<const uint32_t *>(rb + kFront + o);
+			}
+			for (; o < hi; o++)
+				g[o] = rb[kFront + o];
+			if (P.co >= 0) {
+				g[P.co] = rb[kFront + P.co];
+				g[P.co + 1] = rb[kFront + P.co + 1];
+			}
+		}
+		if (active) {
+			a.action[i] = (uint8_t)act;
+			uint4 od = dv;
+			if (act == XDPGPU_TC_ACT_REDIRECT) {
+				const uint64_t na = eff + shift;
+				od.x = (uint32_t)na;
+				od.y = (uint32_t)(na >> 32);
+				od.z = (uint32_t)((int64_t)len - shift);
+			}
+			*reinterpret_cast<uint4 *>(a.out + i) = od;
+		}
+		__builtin_amdgcn_wave_barrier();
+	}
+}
+
+hipError_t launch_nat64(const Nat64Args &a, uint32_t max_blocks, hipStream_t stream)
+{
+	uint64_t tiles = ((uint64_t)a.n + kWaveN - 1) / kWaveN;
+	uint64_t blocks = (tiles + kWavesN - 1) / kWavesN;
+	if (blocks > max_blocks)
+		blocks = max_blocks;
+	if (!blocks)
+		return hipSuccess;
+	hipLaunchKernelGGL(xdp_nat64_kernel, dim3((uint32_t)blocks), dim3(kBlockN), 0,
+			   stream, a);
+	return hipGetLastError();
+}
+
+uint32_t nat64_slot_hash(uint32_t a, uint32_t b, uint32_t c, uint32_t d)
+{
+	uint32_t h = a * 0x9E3779B1u ^ b * 0x85EBCA77u ^ c * 0xC2B2AE3Du ^
+		     d * 0x27D4EB2Fu;
+	h ^= h >> 15;
+	h *= 0x2C1B3C6Du;
+	h ^= h >> 13;
+	return h;
+}
+
+} // namespace xdpgpu

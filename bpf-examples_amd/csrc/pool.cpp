@@ -447,6 +447,185 @@ uint32_t gen_base_frame(const xdpgpu_pool_spec *sp, uint8_t *p)
 	return xs ? L2 : S;
 }
 
+/* ---- NAT64 pools (BASELINE config 4) ---- */
+const uint8_t kPref64[16] = { 0, 0x64, 0xff, 0x9b, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0 };
+const uint8_t kAllow[16] = { 0x20, 0x01, 0x0d, 0xb8, 0, 1, 0, 2, 0, 0, 0, 0, 0, 0, 0, 0 };
+constexpr uint32_t kV4Pool = 0x0A630000u; /* 10.99.0.0/16 */
+constexpr uint32_t kNat64Map = 65533;     /* nat64.c:396 for a /16 */
+
+void nat64_src(uint8_t *a6, uint32_t k)
+{
+	memcpy(a6, kAllow, 16);
+	a6[12] = (uint8_t)(k >> 24);
+	a6[13] = (uint8_t)(k >> 16);
+	a6[14] = (uint8_t)(k >> 8);
+	a6[15] = (uint8_t)k;
+}
+
+/* a public IPv4 address (not 0/8, 10/8, 127/8, >= 224/4) */
+void public_v4(uint64_t h, uint8_t *a4)
+{
+	a4[0] = (uint8_t)(11 + (h % 200));
+	if (a4[0] == 127)
+		a4[0] = 128;
+	a4[1] = (uint8_t)(h >> 8);
+	a4[2] = (uint8_t)(h >> 16);
+	a4[3] = (uint8_t)(1 + ((h >> 24) % 254));
+}
+
+enum : uint8_t { A_OK = XDPGPU_TC_ACT_OK, A_SHOT = XDPGPU_TC_ACT_SHOT,
+		 A_REDIR = XDPGPU_TC_ACT_REDIRECT, A_NOSTATE = XDPGPU_NAT64_NO_STATE };
+
+/* config 4 (ingress): IPv6/UDP, 10 % TCP, ppm_echo6 ICMPv6 echo, toward
+ * 64:ff9b::a.b.c.d from 2001:db8:1:2::k; corruption classes reuse the ppm
+ * knobs: bad_l3 = dst outside pref64 (OK), bad_l4 = source not allowed
+ * (SHOT), ndp = allowed source without mapping (NO_STATE), arp = ARP (OK),
+ * malformed = ext header / reserved v4 dst / truncation / bad version /
+ * untranslatable ICMPv6 / UDP checksum 0. */
+uint32_t gen_nat64_frame(const xdpgpu_pool_spec *sp, uint64_t idx, uint8_t *p,
+			 uint32_t S, uint8_t *expect)
+{
+	Rng r(mix64(sp->seed ^ (idx * 0xD1B54A32D192ED03ull)));
+	const uint32_t L2 = S - 4;
+	const uint32_t fbits = sp->flow_bits ? sp->flow_bits : 16;
+	memset(p, 0, S);
+	uint32_t u = r.below(1000000);
+	uint32_t k = 1 + r.below((1u << fbits) < kNat64Map ? (1u << fbits) : kNat64Map);
+	uint64_t h = r.next();
+	*expect = A_REDIR;
+
+	uint32_t acc = sp->ppm_arp;
+	if (u < acc) {
+		uint32_t o = put_eth(p, kDefDmac, kDefSmac, 0x0806, 0, 0, 0);
+		put_be16(p + o, 1);
+		put_be16(p + o + 2, 0x0800);
+		p[o + 4] = 6;
+		p[o + 5] = 4;
+		put_be16(p + o + 6, 1);
+		*expect = A_OK;
+		return S;
+	}
+	if (sp->kind == XDPGPU_POOL_NAT64_V4) {
+		/* egress: public source toward 10.99.0.0 + k */
+		uint8_t sa[4], da[4] = { 10, 99, (uint8_t)(k >> 8), (uint8_t)k };
+		public_v4(h, sa);
+		uint32_t o = put_eth(p, kDefDmac, kDefSmac, 0x0800, 0, 0, 0);
+		uint32_t room = L2 - o - 20;
+		uint32_t pv = r.below(100), proto = pv < 80 ? 17 : pv < 90 ? 6 : 1;
+		uint8_t *l4 = p + o + 20;
+		if (proto == 1) {
+			uint32_t t = r.below(8);
+			l4[0] = t < 5 ? 8 : t == 5 ? 0 : t == 6 ? 3 : 12;
+			l4[1] = l4[0] == 3 ? (uint8_t)r.below(16) : 0;
+			rand_bytes(r, l4 + 4, room - 4);
+			if (l4[0] == 12)
+				l4[4] = (uint8_t)r.below(20);
+			icmp4_fix_csum(l4, room);
+			if ((l4[0] == 3 && (l4[1] == 14 || l4[1] > 15)) ||
+			    (l4[0] == 12 && ((l4[4] > 3 && l4[4] != 8 && l4[4] != 9 && l4[4] < 12) ||
+					     l4[4] > 19)))
+				*expect = A_SHOT;
+		} else {
+			put_be16(l4, 1024 + (uint32_t)(h >> 32) % 60000);
+			put_be16(l4 + 2, 443);
+			if (proto == 17) {
+				put_be16(l4 + 4, room);
+			} else {
+				l4[12] = 5 << 4;
+				l4[13] = 0x18;
+			}
+			rand_bytes(r, l4 + (proto == 17 ? 8 : 20), room - (proto == 17 ? 8 : 20));
+		}
+		uint32_t saddr, daddr;
+		memcpy(&saddr, sa, 4);
+		memcpy(&daddr, da, 4);
+		put_ipv4(p + o, 20 + room, proto, saddr, daddr, 64);
+		if (proto != 1)
+			l4v4_fix_csum(p + o, l4, room, proto, proto == 6 ? 16 : 6);
+		acc += sp->ppm_bad_l3;
+		if (u < acc) {          /* destination outside the v4 pool */
+			p[o + 17] = 98;
+			ipv4_fix_csum(p + o);
+			*expect = A_OK;
+		} else if (u < acc + sp->ppm_ndp) { /* no reverse mapping */
+			p[o + 18] = 0xff;
+			p[o + 19] = 0xfe;
+			ipv4_fix_csum(p + o);
+			*expect = A_SHOT;
+		} else if (u < acc + sp->ppm_ndp + sp->ppm_malformed) {
+			put_be16(p + o + 6, 0x2000 | (uint32_t)r.below(8)); /* MF */
+			ipv4_fix_csum(p + o);
+			*expect = A_SHOT;
+		}
+		return S;
+	}
+
+	/* ingress: IPv6 */
+	uint8_t s6[16], d6[16], a4[4];
+	nat64_src(s6, k);
+	public_v4(h, a4);
+	memcpy(d6, kPref64, 12);
+	memcpy(d6 + 12, a4, 4);
+	uint32_t o = put_eth(p, kDefDmac, kDefSmac, 0x86DD, 0, 0, 0);
+	uint32_t room = L2 - o - 40;
+	uint32_t pv = r.below(1000000);
+	uint32_t proto = pv < sp->ppm_echo6 ? 58 : pv < sp->ppm_echo6 + 100000 ? 6 : 17;
+	uint8_t *l4 = p + o + 40;
+	if (proto == 58) {
+		l4[0] = 128;
+		rand_bytes(r, l4 + 4, room - 4);
+	} else {
+		put_be16(l4, 1024 + (uint32_t)(h >> 32) % 60000);
+		put_be16(l4 + 2, 53);
+		if (proto == 17) {
+			put_be16(l4 + 4, room);
+		} else {
+			l4[12] = 5 << 4;
+			l4[13] = 0x18;
+		}
+		rand_bytes(r, l4 + (proto == 17 ? 8 : 20), room - (proto == 17 ? 8 : 20));
+	}
+	const uint32_t chk = proto == 6 ? 16 : proto == 17 ? 6 : 2;
+	acc += sp->ppm_bad_l3;
+	if (u < acc) {
+		d6[1] = 0x65;                           /* outside pref64 */
+		*expect = A_OK;
+	} else if (u < acc + sp->ppm_bad_l4) {
+		s6[6] = 0x99;                           /* source not allowed */
+		*expect = A_SHOT;
+	} else if (u < acc + sp->ppm_bad_l4 + sp->ppm_ndp) {
+		nat64_src(s6, kNat64Map + 1 + r.below(1000)); /* no mapping */
+		*expect = A_NOSTATE;
+	}
+	put_ipv6(p + o, room, proto, s6, d6);
+	l4v6_fix_csum(p + o, l4, room, proto, chk);
+	acc += sp->ppm_bad_l4 + sp->ppm_ndp;
+	if (u >= acc && u < acc + sp->ppm_malformed) {
+		uint32_t m = r.below(6);
+		if (m == 0) {
+			p[o + 6] = 0;                   /* hop-by-hop ext header */
+			l4[0] = (uint8_t)proto;
+			l4[1] = 0;
+			*expect = A_SHOT;
+		} else if (m == 1) {
+			p[o + 36] = 127;                /* dst 127.x.x.x */
+			*expect = A_SHOT;
+		} else if (m == 2) {
+			*expect = A_OK;                 /* truncated IPv6 header */
+			return o + 20 + r.below(20);
+		} else if (m == 3) {
+			p[o] = 0x50;                    /* version 5 */
+			*expect = A_OK;
+		} else if (m == 4 && proto == 58) {
+			l4[0] = 135;                    /* NDP: not translatable */
+			*expect = A_SHOT;
+		} else if (proto == 17) {
+			l4[6] = l4[7] = 0;              /* UDP checksum 0: kept */
+		}
+	}
+	return S;
+}
+
 uint32_t frame_size_of(const xdpgpu_pool_spec *sp, uint64_t idx)
 {
 	if (sp->kind != XDPGPU_POOL_IMIX)
@@ -491,7 +670,42 @@ void xdpgpu_pool_spec_default(xdpgpu_pool_spec *spec, uint32_t kind,
 	}
 	if (kind == XDPGPU_POOL_IMIX)
 		spec->frame_size = 64; /* size of special (ARP/NDP) frames */
+	if (kind == XDPGPU_POOL_NAT64 || kind == XDPGPU_POOL_NAT64_V4) {
+		/* config 4: 128 B frames, 10 % ICMPv6 echo; 0.5 % of each
+		 * corruption class */
+		spec->frame_size = frame_size ? frame_size : 128;
+		spec->flow_bits = 16;
+		spec->ppm_echo6 = 100000;
+		spec->ppm_bad_l3 = 5000;
+		spec->ppm_bad_l4 = 5000;
+		spec->ppm_ndp = 5000;
+		spec->ppm_arp = 1000;
+		spec->ppm_malformed = 5000;
+		if (kind == XDPGPU_POOL_NAT64_V4)
+			spec->headroom = 32;   /* the IPv6 header grows the frame */
+	}
 	spec->vlan_id = 1;
+}
+
+int xdpgpu_nat64_pool_config(uint32_t direction, xdpgpu_nat64_cfg *cfg,
+			     xdpgpu_nat64_map *map, uint32_t nmap)
+{
+	if (!cfg || (nmap && !map) || nmap > kNat64Map)
+		return -EINVAL;
+	memset(cfg, 0, sizeof(*cfg));
+	memcpy(cfg->v6_prefix, kPref64, 16);
+	cfg->v6_plen = 96;
+	cfg->v4_prefix = kV4Pool;
+	cfg->v4_mask = 0xFFFF0000u;
+	memcpy(cfg->allow_prefix, kAllow, 16);
+	cfg->allow_plen = 64;
+	cfg->direction = direction;
+	for (uint32_t k = 1; k <= nmap; k++) {
+		nat64_src(map[k - 1].v6, k);
+		map[k - 1].v4 = kV4Pool + k;
+		map[k - 1].rsvd = 0;
+	}
+	return 0;
 }
 
 uint64_t xdpgpu_pool_size(const xdpgpu_pool_spec *spec, uint32_t n)
@@ -512,9 +726,11 @@ int xdpgpu_pool_generate(const xdpgpu_pool_spec *spec, uint8_t *umem,
 {
 	if (!spec || !umem || !descs)
 		return -EINVAL;
+	const bool nat64 = spec->kind == XDPGPU_POOL_NAT64 ||
+			   spec->kind == XDPGPU_POOL_NAT64_V4;
 	const bool random = spec->kind == XDPGPU_POOL_UDP4 ||
-			    spec->kind == XDPGPU_POOL_IMIX;
-	if (spec->kind > XDPGPU_POOL_AFXDP_USER)
+			    spec->kind == XDPGPU_POOL_IMIX || nat64;
+	if (spec->kind > XDPGPU_POOL_NAT64_V4)
 		return -EINVAL;
 	uint32_t S = spec->frame_size;
 	if (spec->kind != XDPGPU_POOL_IMIX && (S < 64 || S > 9728))
@@ -561,8 +777,9 @@ int xdpgpu_pool_generate(const xdpgpu_pool_spec *spec, uint8_t *umem,
 		for (uint32_t i = lo; i < hi; i++) {
 			uint8_t e;
 			uint32_t sz = frame_size_of(spec, i);
-			descs[i].len = gen_random_frame(spec, i, umem + descs[i].addr,
-							sz, &e);
+			descs[i].len = nat64 ?
+				gen_nat64_frame(spec, i, umem + descs[i].addr, sz, &e) :
+				gen_random_frame(spec, i, umem + descs[i].addr, sz, &e);
 			if (expect)
 				expect[i] = e;
 		}

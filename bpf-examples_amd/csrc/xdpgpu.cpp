@@ -16,6 +16,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <vector>
+
 #include <algorithm>
 #include <new>
 
@@ -60,6 +62,11 @@ struct xdpgpu_ctx {
 	uint8_t *d_umem_mapped = nullptr; /* device view of pinned host UMEM */
 	/* XDPGPU_CFG_TIMING: 4 events per recorded launch */
 	hipEvent_t *tev = nullptr;
+	/* nat64 translator (xdpgpu_nat64_setup) */
+	bool nat64 = false;
+	xdpgpu_nat64_cfg ncfg;
+	uint4 *d_v6map = nullptr, *d_v4map = nullptr;
+	uint32_t v6mask = 0, v4mask = 0;
 	uint32_t tn = 0;
 	char err[256];
 };
@@ -149,6 +156,10 @@ void xdpgpu_fini(xdpgpu_ctx *ctx)
 	}
 	if (ctx->d_umem)
 		(void)hipFree(ctx->d_umem);
+	if (ctx->d_v6map)
+		(void)hipFree(ctx->d_v6map);
+	if (ctx->d_v4map)
+		(void)hipFree(ctx->d_v4map);
 	if (ctx->pinned)
 		(void)hipHostUnregister(ctx->h_umem);
 	delete ctx;
@@ -374,6 +385,96 @@ int xdpgpu_process_dev(xdpgpu_ctx *ctx, void *d_umem, uint64_t umem_size,
 	hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
 	return enqueue_rx(ctx, ctx->slot[0], (uint8_t *)d_umem, umem_size,
 			  d_descs, n, d_verdict, d_res, (uint8_t *)d_tuples, st);
+}
+
+/* ---- nat64 ---- */
+
+/* Open-addressing table of 2 x uint4 per slot, power-of-two capacity of at
+ * least twice the entries, linear probing (nat64.hip lookup_v6/lookup_v4).
+ * kv: per entry the probe key words and the two slot halves. */
+static uint32_t nat64_cap(uint32_t n)
+{
+	uint32_t cap = 64;
+	while (cap < 2 * n)
+		cap <<= 1;
+	return cap;
+}
+
+int xdpgpu_nat64_setup(xdpgpu_ctx *ctx, const xdpgpu_nat64_cfg *cfg,
+		       const xdpgpu_nat64_map *map, uint32_t nmap)
+{
+	if (!ctx || !cfg || (nmap && !map))
+		return -EINVAL;
+	const uint32_t pl = cfg->v6_plen;
+	if (pl != 32 && pl != 40 && pl != 48 && pl != 56 && pl != 64 && pl != 96)
+		return set_err(ctx, -EINVAL, "v6 prefix length %u (nat64.c:118)", pl);
+	if (cfg->direction > XDPGPU_NAT64_EGRESS || cfg->allow_plen > 128 ||
+	    (cfg->v4_prefix & ~cfg->v4_mask) || nmap > (1u << 30))
+		return -EINVAL;
+	const uint32_t cap = nat64_cap(nmap);
+	std::vector<uint4> v6t((size_t)cap * 2, make_uint4(0, 0, 0, 0));
+	std::vector<uint4> v4t((size_t)cap * 2, make_uint4(0, 0, 0, 0));
+	for (uint32_t e = 0; e < nmap; e++) {
+		uint32_t w[4];
+		memcpy(w, map[e].v6, 16);
+		uint32_t sl = nat64_slot_hash(w[0], w[1], w[2], w[3]) & (cap - 1);
+		while (v6t[2 * sl + 1].y &&
+		       !(v6t[2 * sl].x == w[0] && v6t[2 * sl].y == w[1] &&
+			 v6t[2 * sl].z == w[2] && v6t[2 * sl].w == w[3]))
+			sl = (sl + 1) & (cap - 1);
+		v6t[2 * sl] = make_uint4(w[0], w[1], w[2], w[3]);
+		v6t[2 * sl + 1] = make_uint4(map[e].v4, 1, 0, 0);
+		sl = nat64_slot_hash(map[e].v4, 0, 0, 0) & (cap - 1);
+		while (v4t[2 * sl].y && v4t[2 * sl].x != map[e].v4)
+			sl = (sl + 1) & (cap - 1);
+		v4t[2 * sl] = make_uint4(map[e].v4, 1, 0, 0);
+		v4t[2 * sl + 1] = make_uint4(w[0], w[1], w[2], w[3]);
+	}
+	HIP_TRY(ctx, hipSetDevice(ctx->cfg.device));
+	if (ctx->d_v6map)
+		(void)hipFree(ctx->d_v6map);
+	if (ctx->d_v4map)
+		(void)hipFree(ctx->d_v4map);
+	ctx->d_v6map = ctx->d_v4map = nullptr;
+	ctx->nat64 = false;
+	const size_t bytes = (size_t)cap * 2 * sizeof(uint4);
+	if (hipMalloc(&ctx->d_v6map, bytes) != hipSuccess ||
+	    hipMalloc(&ctx->d_v4map, bytes) != hipSuccess)
+		return set_err(ctx, -ENOMEM, "nat64 tables of %u slots", cap);
+	HIP_TRY(ctx, hipMemcpy(ctx->d_v6map, v6t.data(), bytes, hipMemcpyHostToDevice));
+	HIP_TRY(ctx, hipMemcpy(ctx->d_v4map, v4t.data(), bytes, hipMemcpyHostToDevice));
+	ctx->v6mask = ctx->v4mask = cap - 1;
+	ctx->ncfg = *cfg;
+	ctx->nat64 = true;
+	return 0;
+}
+
+int xdpgpu_nat64_dev(xdpgpu_ctx *ctx, void *d_umem, uint64_t umem_size,
+		     const xdpgpu_desc *d_descs, uint32_t n, uint8_t *d_action,
+		     xdpgpu_desc *d_out, void *stream)
+{
+	if (!ctx || !d_umem || !d_descs || !d_action || !d_out)
+		return -EINVAL;
+	if (!ctx->nat64)
+		return set_err(ctx, -EINVAL, "xdpgpu_nat64_setup not called");
+	if (n == 0)
+		return 0;
+	Nat64Args a;
+	memset(&a, 0, sizeof(a));
+	a.umem = (uint8_t *)d_umem;
+	a.usize = umem_size;
+	a.desc = d_descs;
+	a.n = n;
+	a.action = d_action;
+	a.out = d_out;
+	a.cfg = ctx->ncfg;
+	a.v6map = ctx->d_v6map;
+	a.v6mask = ctx->v6mask;
+	a.v4map = ctx->d_v4map;
+	a.v4mask = ctx->v4mask;
+	hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
+	HIP_TRY(ctx, launch_nat64(a, ctx->max_blocks, st));
+	return 0;
 }
 
 int xdpgpu_ceiling_dev(xdpgpu_ctx *ctx, const void *d_umem, uint64_t umem_size,

@@ -62,6 +62,24 @@ uint32_t rx_grid_blocks(uint32_t n, uint32_t max_blocks);
 uint32_t rx_xregion(uint32_t n, uint32_t blocks);
 hipError_t launch_ceiling(const RxArgs &a, uint32_t blocks, hipStream_t stream);
 
+struct Nat64Args {
+	uint8_t *umem;
+	uint64_t usize;
+	const xdpgpu_desc *desc;
+	uint32_t n;
+	uint8_t *action;
+	xdpgpu_desc *out;
+	xdpgpu_nat64_cfg cfg;
+	const uint4 *v6map;        /* 2 x uint4 per slot, v6mask + 1 slots */
+	uint32_t v6mask;
+	const uint4 *v4map;
+	uint32_t v4mask;
+};
+
+hipError_t launch_nat64(const Nat64Args &a, uint32_t max_blocks,
+			hipStream_t stream);
+uint32_t nat64_slot_hash(uint32_t a, uint32_t b, uint32_t c, uint32_t d);
+
 hipError_t launch_jhash(const uint8_t *keys, uint32_t key_len,
 			uint32_t stride, uint32_t n, uint32_t initval,
 			uint32_t *out, hipStream_t stream);

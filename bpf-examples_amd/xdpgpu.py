@@ -49,6 +49,13 @@ F_L3_OK, F_L4_OK, F_VLAN, F_IPV6 = 0x01, 0x02, 0x04, 0x08
 F_FRAG, F_L4_ABSENT, F_IP, F_L4 = 0x10, 0x20, 0x40, 0x80
 
 POOL_UDP4, POOL_IMIX, POOL_XDPSOCK, POOL_AFXDP_USER = 0, 1, 2, 3
+POOL_NAT64, POOL_NAT64_V4 = 4, 5
+
+# nat64 (include/xdpgpu.h): direction and per-frame actions
+NAT64_INGRESS, NAT64_EGRESS = 0, 1
+TC_ACT_OK, TC_ACT_SHOT, TC_ACT_REDIRECT = 0, 2, 7
+NAT64_NO_STATE = 0x80
+NAT64_MAP_DTYPE = np.dtype([("v6", "u1", (16,)), ("v4", "<u4"), ("rsvd", "<u4")])
 UMEM_UNALIGNED_CHUNK_FLAG = 1
 
 DESC_DTYPE = np.dtype([("addr", "<u8"), ("len", "<u4"), ("options", "<u4")])
@@ -111,6 +118,14 @@ class PoolSpec(C.Structure):
                 ("threads", C.c_uint32), ("rsvd", C.c_uint32 * 3)]
 
 
+class Nat64Cfg(C.Structure):
+    """struct xdpgpu_nat64_cfg"""
+    _fields_ = [("v6_prefix", C.c_uint8 * 16), ("v6_plen", C.c_uint32),
+                ("v4_prefix", C.c_uint32), ("v4_mask", C.c_uint32),
+                ("allow_plen", C.c_uint32), ("allow_prefix", C.c_uint8 * 16),
+                ("direction", C.c_uint32), ("rsvd", C.c_uint32 * 3)]
+
+
 class XdpGpuError(RuntimeError):
     pass
 
@@ -123,6 +138,7 @@ EXPORTS = (
     "xdpgpu_submit", "xdpgpu_wait", "xdpgpu_process_dev", "xdpgpu_stats",
     "xdpgpu_stats_reset", "xdpgpu_jhash_dev", "xdpgpu_ip_fast_csum_dev",
     "xdpgpu_sync", "xdpgpu_ceiling_dev", "xdpgpu_kernel_times",
+    "xdpgpu_nat64_setup", "xdpgpu_nat64_dev", "xdpgpu_nat64_pool_config",
     "xdpgpu_device_count", "xdpgpu_last_error",
     "xdpgpu_abi_version", "xdpgpu_pool_size", "xdpgpu_pool_generate",
     "xdpgpu_pool_spec_default",
@@ -154,6 +170,9 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.xdpgpu_sync.argtypes = [vp, vp]
     lib.xdpgpu_ceiling_dev.argtypes = [vp, vp, u64, vp, u32, vp, vp, vp, vp]
     lib.xdpgpu_kernel_times.argtypes = [vp, C.POINTER(KTimes)]
+    lib.xdpgpu_nat64_setup.argtypes = [vp, C.POINTER(Nat64Cfg), vp, u32]
+    lib.xdpgpu_nat64_dev.argtypes = [vp, vp, u64, vp, u32, vp, vp, vp]
+    lib.xdpgpu_nat64_pool_config.argtypes = [u32, C.POINTER(Nat64Cfg), vp, u32]
     lib.xdpgpu_device_count.argtypes = []
     lib.xdpgpu_last_error.argtypes = [vp]
     lib.xdpgpu_last_error.restype = C.c_char_p
@@ -278,6 +297,18 @@ class XdpGpu:
             self.h, _ptr(umem), umem_size, _ptr(descs), n, _ptr(verdict),
             _ptr(res), _ptr(tup), _stream_handle(stream)), "xdpgpu_process_dev")
 
+    def nat64_setup(self, cfg: Nat64Cfg, smap: np.ndarray) -> None:
+        smap = np.ascontiguousarray(smap, NAT64_MAP_DTYPE)
+        self._check(self.lib.xdpgpu_nat64_setup(
+            self.h, C.byref(cfg), smap.ctypes.data if len(smap) else None,
+            len(smap)), "xdpgpu_nat64_setup")
+
+    def nat64_dev(self, umem, umem_size: int, descs, n: int, action, out,
+                  stream=None) -> None:
+        self._check(self.lib.xdpgpu_nat64_dev(
+            self.h, _ptr(umem), umem_size, _ptr(descs), n, _ptr(action),
+            _ptr(out), _stream_handle(stream)), "xdpgpu_nat64_dev")
+
     def ceiling_dev(self, umem, umem_size: int, descs, n: int, verdict, res,
                     tup, stream=None) -> None:
         """Diagnostic memory-ceiling kernel (same traffic, no parse)."""
@@ -350,3 +381,15 @@ def pool_generate(n: int, kind: int = POOL_UDP4, frame_size: int = 64,
     if rc:
         raise XdpGpuError(f"xdpgpu_pool_generate: {os.strerror(-rc)} ({rc})")
     return umem, descs, expect
+
+
+def nat64_pool_config(direction: int = NAT64_INGRESS, nmap: int = 65533):
+    """(cfg, static map) the NAT64 pools are drawn from (xdpgpu.h)."""
+    lib = load_library()
+    cfg = Nat64Cfg()
+    smap = np.zeros(nmap, NAT64_MAP_DTYPE)
+    rc = lib.xdpgpu_nat64_pool_config(direction, C.byref(cfg),
+                                      smap.ctypes.data if nmap else None, nmap)
+    if rc:
+        raise XdpGpuError(f"xdpgpu_nat64_pool_config: {rc}")
+    return cfg, smap

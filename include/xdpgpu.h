@@ -234,6 +234,61 @@ const char *xdpgpu_last_error(struct xdpgpu_ctx *ctx);
 int xdpgpu_abi_version(void);
 
 /* ------------------------------------------------------------------ */
+/* nat64 (nat64-bpf/nat64_kern.c): the stateful NAT64 translator as a batch
+ * transform over UMEM frames, BASELINE config 4.                      */
+
+#define XDPGPU_NAT64_INGRESS 0 /* IPv6 -> IPv4: nat64_handle_v6 (nat64_kern.c:741-873) */
+#define XDPGPU_NAT64_EGRESS  1 /* IPv4 -> IPv6: nat64_handle_v4 (nat64_kern.c:443-541) */
+
+/* Per-frame result: the reference program's TC action (linux/pkt_cls.h),
+ * plus one build-defined value. */
+#define XDPGPU_TC_ACT_OK       0  /* not for the translator: untouched   */
+#define XDPGPU_TC_ACT_SHOT     2  /* in the prefix but not translatable  */
+#define XDPGPU_TC_ACT_REDIRECT 7  /* translated                          */
+/* An allowed IPv6 source with no mapping in the static table.  The
+ * reference allocates one (alloc_new_state, nat64_kern.c:576-622); that
+ * order-dependent allocation stays with the host: the frame is untouched. */
+#define XDPGPU_NAT64_NO_STATE  0x80
+
+/* struct nat64_config (nat64.h:6-12) plus the allowed_v6_src entry. */
+struct xdpgpu_nat64_cfg {
+	uint8_t  v6_prefix[16];    /* pref64; nat64.c default 64:ff9b::/96   */
+	uint32_t v6_plen;          /* 32, 40, 48, 56, 64 or 96               */
+	uint32_t v4_prefix;        /* host byte order (nat64.c:155-158)      */
+	uint32_t v4_mask;          /* host byte order                        */
+	uint32_t allow_plen;       /* allowed_v6_src LPM entry, 0: none      */
+	uint8_t  allow_prefix[16];
+	uint32_t direction;        /* XDPGPU_NAT64_*                         */
+	uint32_t rsvd[3];
+};
+
+/* A static v6_state_map entry (struct v6_addr_state with static_conf,
+ * nat64.h:15-19); v4_reversemap is its inverse. */
+struct xdpgpu_nat64_map {
+	uint8_t  v6[16];
+	uint32_t v4;               /* host byte order, inside the v4 prefix  */
+	uint32_t rsvd;
+};
+
+/* Configure the translator of a context and upload its static tables
+ * (replaces nat64.c's map setup, nat64.c:396-420). */
+int xdpgpu_nat64_setup(struct xdpgpu_ctx *ctx,
+		       const struct xdpgpu_nat64_cfg *cfg,
+		       const struct xdpgpu_nat64_map *map, uint32_t nmap);
+
+/* Translate frames in place (device pointers, stream as above).  Replaces
+ * the per-packet TC programs nat64_ingress / nat64_egress
+ * (nat64_kern.c:875-902).  d_action[i] gets the action; d_out[i] the
+ * translated frame: an IPv6->IPv4 frame starts 20 bytes later, an
+ * IPv4->IPv6 frame 20 bytes earlier (it needs 20 bytes of UMEM headroom),
+ * both as a plain UMEM offset.  Other frames keep their descriptor.  The
+ * L2 header moves with the frame; only headers and the L4 checksum (ICMP:
+ * type, code and rest-of-header) are written. */
+int xdpgpu_nat64_dev(struct xdpgpu_ctx *ctx, void *d_umem, uint64_t umem_size,
+		     const struct xdpgpu_desc *d_descs, uint32_t n,
+		     uint8_t *d_action, struct xdpgpu_desc *d_out, void *stream);
+
+/* ------------------------------------------------------------------ */
 /* Synthetic UMEM pool generator (host).  Replaces the reference's packet
  * generators gen_eth_hdr_data (xdpsock.c:893-971) and gen_base_pkt
  * (af_xdp_user.c:688-700) for pool mode.                              */
@@ -243,6 +298,8 @@ enum xdpgpu_pool_kind {
 	XDPGPU_POOL_IMIX       = 1, /* 64/570/1500 7:4:1, VLAN/QinQ, v4/v6, ... */
 	XDPGPU_POOL_XDPSOCK    = 2, /* xdpsock txonly base frame, replicated    */
 	XDPGPU_POOL_AFXDP_USER = 3, /* af_xdp_user base frame, replicated       */
+	XDPGPU_POOL_NAT64      = 4, /* config 4: IPv6 toward 64:ff9b::/96       */
+	XDPGPU_POOL_NAT64_V4   = 5, /* IPv4 toward the nat64 v4 pool (egress)   */
 };
 
 struct xdpgpu_pool_spec {
@@ -281,6 +338,13 @@ int xdpgpu_pool_generate(const struct xdpgpu_pool_spec *spec, uint8_t *umem,
 			 uint32_t n, uint8_t *expect);
 
 /* Set a spec to the defaults of BASELINE config kind (frame size S). */
+/* The translator configuration and static map the NAT64 pools are drawn
+ * from: pref64 64:ff9b::/96, v4 pool 10.99.0.0/16, allowed sources
+ * 2001:db8:1:2::/64, source k (1..nmap) = 2001:db8:1:2::k mapped to
+ * 10.99.0.0 + k.  map must hold nmap entries (at most 65533). */
+int xdpgpu_nat64_pool_config(uint32_t direction, struct xdpgpu_nat64_cfg *cfg,
+			     struct xdpgpu_nat64_map *map, uint32_t nmap);
+
 void xdpgpu_pool_spec_default(struct xdpgpu_pool_spec *spec, uint32_t kind,
 			      uint32_t frame_size, uint64_t seed);
 

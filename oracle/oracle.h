@@ -42,6 +42,18 @@ int oracle_process(uint8_t *umem, uint64_t umem_size,
 		   uint8_t *verdict, struct xdpgpu_result *res, void *tuples,
 		   struct xdpgpu_stats *stats);
 
+/* nat64 (nat64_oracle.c): same inputs and outputs as xdpgpu_nat64_dev;
+ * umem is translated in place. */
+int oracle_nat64(uint8_t *umem, uint64_t umem_size,
+		 const struct xdpgpu_desc *descs, uint32_t n,
+		 const struct xdpgpu_nat64_cfg *cfg,
+		 const struct xdpgpu_nat64_map *map, uint32_t nmap,
+		 uint8_t *action, struct xdpgpu_desc *out);
+int oracle_v4addr_to_v6(const uint8_t a4[4], uint8_t a6[16],
+			const uint8_t pref[16], int plen);
+int oracle_v6addr_to_v4(const uint8_t a6[16], int plen, uint8_t a4[4],
+			uint8_t pref[16]);
+
 /* CPU baseline: run oracle_process over descs[0..n) `reps` times on
  * `threads` threads, each on a contiguous slice.  Returns wall seconds. */
 double oracle_bench(uint8_t *umem, uint64_t umem_size,

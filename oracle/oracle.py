@@ -27,6 +27,15 @@ RESULT_DTYPE = np.dtype([
     ("l4_off", "<u2"), ("l4_len", "<u2"),
 ])
 TUPLE_BYTES = {0: 0, 1: 16, 2: 44}
+NAT64_MAP_DTYPE = np.dtype([("v6", "u1", (16,)), ("v4", "<u4"), ("rsvd", "<u4")])
+
+
+class Nat64Cfg(C.Structure):
+    """struct xdpgpu_nat64_cfg (include/xdpgpu.h)"""
+    _fields_ = [("v6_prefix", C.c_uint8 * 16), ("v6_plen", C.c_uint32),
+                ("v4_prefix", C.c_uint32), ("v4_mask", C.c_uint32),
+                ("allow_plen", C.c_uint32), ("allow_prefix", C.c_uint8 * 16),
+                ("direction", C.c_uint32), ("rsvd", C.c_uint32 * 3)]
 
 
 class OStats(C.Structure):
@@ -78,6 +87,10 @@ def lib() -> C.CDLL:
         o.oracle_bench.argtypes = [vp, u64, vp, u32, u32, u32, u32, vp, vp,
                                    vp, u32, u32]
         o.oracle_bench.restype = C.c_double
+        o.oracle_nat64.argtypes = [vp, u64, vp, u32, C.POINTER(Nat64Cfg), vp, u32,
+                                   vp, vp]
+        o.oracle_v4addr_to_v6.argtypes = [vp, vp, vp, C.c_int]
+        o.oracle_v6addr_to_v4.argtypes = [vp, C.c_int, vp, vp]
         del u8p
         _o = o
     return _o
@@ -165,3 +178,32 @@ def bench(umem: np.ndarray, descs: np.ndarray, threads: int, reps: int,
     return o.oracle_bench(umem.ctypes.data, umem.nbytes, descs.ctypes.data, n,
                           flags, initval, tuple_fmt, verdict.ctypes.data,
                           res.ctypes.data, tup.ctypes.data, threads, reps)
+
+
+def nat64(umem: np.ndarray, descs: np.ndarray, cfg: "Nat64Cfg", smap: np.ndarray):
+    """Run the nat64 oracle in place on umem: returns (action, out descs)."""
+    o = lib()
+    descs = np.ascontiguousarray(descs, DESC_DTYPE)
+    smap = np.ascontiguousarray(smap, NAT64_MAP_DTYPE)
+    n = len(descs)
+    action = np.zeros(n, np.uint8)
+    out = np.zeros(n, DESC_DTYPE)
+    o.oracle_nat64(umem.ctypes.data, umem.nbytes, descs.ctypes.data, n, C.byref(cfg),
+                   smap.ctypes.data if len(smap) else None, len(smap),
+                   action.ctypes.data, out.ctypes.data)
+    return action, out
+
+
+def v4addr_to_v6(a4: bytes, pref: bytes, plen: int):
+    o = lib()
+    out = C.create_string_buffer(16)
+    ok = o.oracle_v4addr_to_v6(buf(a4), out, buf(pref), plen)
+    return bytes(out.raw[:16]) if ok else None
+
+
+def v6addr_to_v4(a6: bytes, plen: int):
+    o = lib()
+    a4 = C.create_string_buffer(4)
+    pref = C.create_string_buffer(16)
+    ok = o.oracle_v6addr_to_v4(buf(a6), plen, a4, pref)
+    return (bytes(a4.raw[:4]), bytes(pref.raw[:16])) if ok else None
