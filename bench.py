@@ -21,7 +21,8 @@ is the HBM bytes per launch from the committed rocprofv3 PMC summary
 (profiles/r01_pmc.json, tools/pmc_profile.sh).  The CPU baseline is the
 oracle (oracle/xdp_oracle.c, a restatement of the reference C) timed on this
 host, rank 0 at N = 1 only, on a bounded sample.  Secondary lines: config 2
-geometry at 1500 B, and config 3 (16 M IMIX, 44 B network_tuple).
+geometry at 1500 B, config 3 (16 M IMIX, 44 B network_tuple) and config 4
+(16 M x 128 B nat64 ingress).
 """
 from __future__ import annotations
 
@@ -170,6 +171,46 @@ def side_run(ctx, tctx, dev, stream, n, kind, size, seed, fmt, steps, label, bpf
     return out
 
 
+def nat64_run(dev, stream, n, steps, local):
+    """Config 4: nat64 ingress (IPv6 -> IPv4) over n 128 B frames.  The
+    transform rewrites the UMEM, so every step restores the pool from a
+    pristine device copy first (device-to-device, outside the timed
+    region); each launch is timed with HIP events on its stream."""
+    cfg, smap = xdpgpu.nat64_pool_config(xdpgpu.NAT64_INGRESS)
+    u, ds, ex = xdpgpu.pool_generate(n, xdpgpu.POOL_NAT64, 128, 0x5EED0004)
+    pristine = to_dev(u, dev)
+    work = torch.empty_like(pristine)
+    d_desc = to_dev(ds, dev, 0)
+    d_act = torch.empty(n, dtype=torch.uint8, device=dev)
+    d_out = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    ms = []
+    with xdpgpu.XdpGpu(local) as g:
+        g.nat64_setup(cfg, smap)
+        for k in range(steps + 2):
+            with torch.cuda.stream(stream):
+                work.copy_(pristine, non_blocking=True)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            g.nat64_dev(work, u.nbytes, d_desc, n, d_act, d_out, stream)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            if k >= 2:
+                ms.append(e0.elapsed_time(e1))
+    ok = bool(np.array_equal(d_act.cpu().numpy(), ex))
+    t = float(np.mean(ms))
+    algo = n * 149          # SURVEY.md §8d config 4
+    out = {"workload": f"config4: {n} x 128B IPv6 frames, nat64 ingress (64:ff9b::/96, "
+                       "65533 static mappings)",
+           "frames": n, "mpps": round(n / t / 1e3, 1), "kernel_ms": round(t, 4),
+           "algorithmic_bytes_per_launch": algo,
+           "gbps": round(algo / t / 1e6, 1),
+           "roofline_frac": round(algo / t / 1e6 / HBM_PEAK_GBS, 4),
+           "actions_ok": ok}
+    del pristine, work, d_desc, d_act, d_out
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -181,6 +222,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--imix-frames", type=int, default=16 << 20)
+    ap.add_argument("--nat64-frames", type=int, default=16 << 20)
     ap.add_argument("--e2e", action="store_true", help="also time the host path")
     args = ap.parse_args()
 
@@ -246,6 +288,8 @@ def main():
             lambda ds: len(ds) * (16 + 16 + 44 + 1) + int(ds["len"].astype(np.int64).sum()))
         ctx3.close()
         tctx3.close()
+        secondary["config4_nat64"] = nat64_run(dev, stream, args.nat64_frames, steps2,
+                                               local)
 
     e2e = None
     if args.e2e and rank == 0 and world == 1:

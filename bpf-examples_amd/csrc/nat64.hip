@@ -587,11 +587,26 @@ __global__ __launch_bounds__(kBlockN) void xdp_nat64_kernel(Nat64Args a)
 	const Tables T = {a.v6map, a.v6mask, a.v4map, a.v4mask};
 	const uint64_t us16 = (a.usize + 15) & ~15ull;
 
-	const uint64_t ntiles = ((uint64_t)a.n + kWaveN - 1) / kWaveN;
+	/* work: every frame (a.xlist null) or the fast kernel's slow-frame
+	 * lists, one (region, batch of 64) item at a time */
 	const uint64_t nwaves = (uint64_t)gridDim.x * kWavesN;
-	for (uint64_t t = (uint64_t)blockIdx.x * kWavesN + wid; t < ntiles; t += nwaves) {
-		const uint64_t i = t * kWaveN + lane;
-		const bool active = i < a.n;
+	const uint64_t nitems = a.xlist ? (uint64_t)a.nregions * (a.xregion / kWaveN)
+				       : ((uint64_t)a.n + kWaveN - 1) / kWaveN;
+	for (uint64_t t = (uint64_t)blockIdx.x * kWavesN + wid; t < nitems; t += nwaves) {
+		uint64_t i;
+		bool active;
+		if (a.xlist) {
+			const uint32_t r = (uint32_t)(t % a.nregions);
+			const uint32_t b = (uint32_t)(t / a.nregions) * kWaveN;
+			const uint32_t cnt = a.xcount[r];
+			if (b >= cnt)
+				continue;
+			active = b + lane < cnt;
+			i = active ? a.xlist[(uint64_t)r * a.xregion + b + lane] : 0;
+		} else {
+			i = t * kWaveN + lane;
+			active = i < a.n;
+		}
 		const uint4 dv = active ? *reinterpret_cast<const uint4 *>(a.desc + i)
 					: make_uint4(0, 0, 0, 0);
 		const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
@@ -684,8 +699,332 @@ __global__ __launch_bounds__(kBlockN) void xdp_nat64_kernel(Nat64Args a)
 	}
 }
 
-hipError_t launch_nat64(const Nat64Args &a, uint32_t max_blocks, hipStream_t stream)
+/* ------------------------------------------------------------------ */
+/* Fast kernel: IPv6 -> IPv4 of untagged, 16-byte aligned frames with no
+ * extension header under a /96 prefix (config 4).  The 64-byte window of a
+ * tile is staged by LDS-DMA as in the RX fast kernel (conflict-free slot
+ * swizzle); everything else happens in registers: field extraction at
+ * fixed offsets, the static-map probe, the IPv4 header and its checksum,
+ * the incremental L4 update (TCP's check word at 70 is a second, narrow
+ * load) and three 16-byte stores of frame bytes [16, 64).  Frames of other
+ * shapes go to the wave's slow list (xdp_nat64_kernel). */
+
+typedef __attribute__((address_space(3))) void lds_void_n;
+
+__device__ __forceinline__ uint32_t halves2(uint32_t x)
 {
+	return (x & 0xffff) + (x >> 16);
+}
+
+__device__ __forceinline__ uint32_t bswap16n(uint32_t x)
+{
+	return ((x & 0xff) << 8) | ((x >> 8) & 0xff);
+}
+
+__global__ __launch_bounds__(kBlockN) void xdp_nat64_fast_kernel(Nat64Args a)
+{
+	__shared__ uint4 buf_all[kWavesN * 4 * kWaveN];
+	__shared__ uint64_t dtab_all[kWavesN * kWaveN];
+	__shared__ uint32_t xq_all[kWavesN * 2 * kWaveN];
+	const int lane = threadIdx.x & (kWaveN - 1);
+	const int wid = threadIdx.x / kWaveN;
+	uint4 *buf = buf_all + wid * 4 * kWaveN;
+	uint64_t *dtab = dtab_all + wid * kWaveN;
+	uint32_t *xq = xq_all + wid * 2 * kWaveN;
+	const Tables T = {a.v6map, a.v6mask, a.v4map, a.v4mask};
+
+	const uint64_t ntiles = ((uint64_t)a.n + kWaveN - 1) / kWaveN;
+	const uint64_t nwaves = (uint64_t)gridDim.x * kWavesN;
+	const uint64_t wgid = (uint64_t)blockIdx.x * kWavesN + wid;
+	uint32_t *xl = a.xlist + wgid * a.xregion;
+	uint32_t xq_n = 0, xout = 0;
+	const uint64_t us16 = (a.usize + 15) & ~15ull;
+	const bool dma = a.usize >= 64;
+
+	auto ld_desc = [&](uint64_t tt) -> uint4 {
+		uint64_t i = tt * kWaveN + lane;
+		i = i < a.n ? i : a.n - 1;
+		return *reinterpret_cast<const uint4 *>(a.desc + i);
+	};
+	auto issue = [&](uint4 dv, bool live) {
+		const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
+		const uint32_t len = dv.z;
+		const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
+		const bool ok = live & dma & ((uint64_t)len <= a.usize) &
+				(eff <= a.usize - len) & !(eff & 15) & (eff + 64 <= us16);
+		dtab[lane] = ok ? eff : 0ull;
+		__builtin_amdgcn_wave_barrier();
+#pragma unroll
+		for (int k = 0; k < 4; k++) {
+			const int f = 16 * k + (lane >> 2);
+			const int c = (lane & 3) ^ ((f >> 2) & 3);
+			__builtin_amdgcn_global_load_lds(
+				(const void *)(a.umem + dtab[f] + 16 * c),
+				(lds_void_n *)(buf + kWaveN * k), 16, 0, 2);
+		}
+	};
+
+	uint64_t t = wgid;
+	uint4 dcur = make_uint4(0, 0, 0, 0), dnext = dcur;
+	if (t < ntiles) {
+		dcur = ld_desc(t);
+		dnext = ld_desc(t + nwaves);
+		issue(dcur, true);
+	}
+	for (; t < ntiles; t += nwaves) {
+		const uint64_t i = t * kWaveN + lane;
+		const bool active = i < a.n;
+		const uint4 dv = dcur;
+		uint32_t F[16];
+		{
+			const int sw = (lane >> 2) & 3;
+#pragma unroll
+			for (int c = 0; c < 4; c++) {
+				const uint4 v = buf[4 * lane + (c ^ sw)];
+				F[4 * c] = v.x;
+				F[4 * c + 1] = v.y;
+				F[4 * c + 2] = v.z;
+				F[4 * c + 3] = v.w;
+			}
+		}
+		__builtin_amdgcn_s_waitcnt(0xc07f);   /* lgkmcnt(0) */
+		__builtin_amdgcn_wave_barrier();
+		dcur = dnext;
+		issue(dcur, t + nwaves < ntiles);
+		dnext = ld_desc(t + 2 * nwaves);
+
+		const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
+		const uint32_t len = dv.z;
+		const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
+		const bool valid = active & ((uint64_t)len <= a.usize) & (eff <= a.usize - len);
+		const bool staged = valid & dma & !(eff & 15) & (eff + 64 <= us16);
+
+		/* classification (nat64_handler, nat64_handle_v6 order) */
+		const uint32_t et = F[3] & 0xffff;
+		const bool vlan = (et == 0x0081u) | (et == 0xa888u);
+		const bool is6 = et == 0xdd86u;
+		const uint32_t nh = F[5] & 0xff;
+		const bool ext = (nh == 0) | (nh == 43) | (nh == 44) | (nh == 51) |
+				 (nh == 60) | (nh == 135);
+		const bool hdr_ok = (len >= 56) & (((F[3] >> 20) & 0xf) == 6);
+		uint32_t s[4], d[4];
+#pragma unroll
+		for (int k = 0; k < 4; k++) {
+			s[k] = (F[5 + k] >> 16) | (F[6 + k] << 16);
+			d[k] = (F[9 + k] >> 16) | (F[10 + k] << 16);
+		}
+		const bool inpref = (d[0] == a.pref_w[0]) & (d[1] == a.pref_w[1]) &
+				    (d[2] == a.pref_w[2]);
+		const uint32_t dst = __builtin_bswap32(d[3]);
+		const bool special = (dst == 0) | ((dst & 0xFF000000u) == 0x7F000000u) |
+				     ((dst & 0xF0000000u) == 0xE0000000u);
+		const bool allowed = (a.cfg.allow_plen != 0) &
+				     ((s[0] & a.allow_m[0]) == a.allow_w[0]) &
+				     ((s[1] & a.allow_m[1]) == a.allow_w[1]) &
+				     ((s[2] & a.allow_m[2]) == a.allow_w[2]) &
+				     ((s[3] & a.allow_m[3]) == a.allow_w[3]);
+		const uint32_t itype = (F[13] >> 16) & 0xff;
+		const bool icmp_ok = (itype == 128) | (itype == 129);
+
+		/* decided here: invalid (SHOT), len < 14 or not IPv6 (OK),
+		 * parse failure (OK), outside the prefix (OK), SHOT cases,
+		 * and the translatable shapes; the rest is slow */
+		bool slow = false;
+		uint32_t act = XDPGPU_TC_ACT_OK;
+		bool xlate = false;
+		if (!valid) {
+			act = XDPGPU_TC_ACT_SHOT;
+		} else if (len < 14) {
+			act = XDPGPU_TC_ACT_OK;
+		} else if (!staged) {
+			slow = true;
+		} else if (vlan) {
+			slow = true;
+		} else if (!is6 || !hdr_ok) {
+			act = XDPGPU_TC_ACT_OK;           /* also len < 56 */
+		} else if (len < 64) {
+			slow = true;   /* the 16-byte stores stay inside the frame */
+		} else if (ext) {
+			slow = true;
+		} else if (!inpref) {
+			act = XDPGPU_TC_ACT_OK;
+		} else if (special || !allowed) {
+			act = XDPGPU_TC_ACT_SHOT;
+		} else if (nh == 58 && (!icmp_ok || len < 62)) {
+			slow = true;
+		} else {
+			xlate = true;
+		}
+		uint32_t v4 = 0;
+		if (xlate) {
+			bool found;
+			v4 = lookup_v6(T, s, found);
+			if (!found) {
+				xlate = false;
+				act = XDPGPU_NAT64_NO_STATE;
+			} else {
+				act = XDPGPU_TC_ACT_REDIRECT;
+			}
+		}
+		/* TCP's check word (bytes 70-71) lies past the window */
+		uint32_t e68 = 0;
+		const bool tcp_upd = xlate && nh == 6 && len >= 72;
+		if (tcp_upd)
+			e68 = *reinterpret_cast<const uint32_t *>(a.umem + eff + 68);
+
+		/* slow frames to this wave's list */
+		{
+			const uint64_t dm = __ballot(active && slow);
+			if (dm) {
+				const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+					(uint32_t)(dm >> 32),
+					__builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0));
+				if (active && slow)
+					xq[xq_n + rank] = (uint32_t)i;
+				xq_n += (uint32_t)__popcll(dm);
+				if (xq_n >= (uint32_t)kWaveN) {
+					__builtin_amdgcn_wave_barrier();
+					xl[xout + lane] = xq[lane];
+					xout += kWaveN;
+					const uint32_t rest = xq[kWaveN + lane];
+					__builtin_amdgcn_wave_barrier();
+					xq[lane] = rest;
+					xq_n -= kWaveN;
+				}
+			}
+		}
+
+		if (xlate) {
+			const uint32_t h3 = __builtin_bswap32(v4);        /* src, LE word */
+			const uint32_t h4 = d[3];
+			const uint32_t tos = (((F[3] >> 16) & 0xf) << 4) | (F[3] >> 28);
+			const uint32_t tot = (bswap16n(F[4] >> 16) + 20) & 0xffff;
+			const uint32_t ttl = (F[5] >> 8) & 0xff;
+			const uint32_t p4 = nh == 58 ? 1u : nh;
+			/* IPv4 header checksum (csum_fold_helper of the header) */
+			uint32_t hs = halves2(0x45u | (tos << 8) | (bswap16n(tot) << 16)) +
+				      0x4000u + (ttl | (p4 << 8)) + halves2(h3) + halves2(h4);
+			hs = (hs & 0xffff) + (hs >> 16);
+			hs = (hs & 0xffff) + (hs >> 16);
+			const uint32_t chk4 = ~hs & 0xffff;
+			/* the pseudo header's address words, v6 and v4 */
+			uint32_t s6 = 0;
+#pragma unroll
+			for (int k = 0; k < 4; k++)
+				s6 += halves2(s[k]) + halves2(d[k]);
+			s6 = mod_ffff(s6);
+			const uint32_t s4 = mod_ffff(halves2(h3) + halves2(h4));
+			uint32_t o13 = (h4 >> 16) | (F[13] & 0xffff0000u);
+			uint32_t o14 = F[14], o15 = F[15];
+			if (nh == 17) {
+				/* update_l4_checksum, BPF_F_MARK_MANGLED_0 */
+				uint32_t c = F[15] & 0xffff;
+				if (c) {
+					c = csum_upd(c, diff_mod(s6, s4));
+					if (!c)
+						c = 0xffff;
+				}
+				o15 = (F[15] & 0xffff0000u) | c;
+			} else if (nh == 6) {
+				if (tcp_upd) {
+					const uint32_t c = csum_upd(e68 >> 16, diff_mod(s6, s4));
+					e68 = (e68 & 0xffff) | (c << 16);
+				}
+			} else if (nh == 58) {
+				/* rewrite_icmpv6, echo: pseudo header out, type word */
+				const uint32_t ph = mod_ffff(s6 + (F[4] >> 16) + (58u << 8));
+				const uint32_t code = (F[13] >> 24) & 0xff;
+				const uint32_t nt = itype == 128 ? 8u : 0u;
+				const uint32_t hb = itype | (code << 8), ha = nt | (code << 8);
+				const uint32_t delta = mod_ffff(diff_mod(ph, 0) + diff_mod(hb, ha));
+				const uint32_t c = csum_upd(F[14] & 0xffff, delta);
+				o13 = (h4 >> 16) | (ha << 16);
+				o14 = (F[14] & 0xffff0000u) | c;
+			}
+			/* frame bytes [16, 64): unchanged [16, 20), the L2 header
+			 * moved to 20 with h_proto 0x0800, the IPv4 header at
+			 * 34, the L4 bytes at 54 */
+			uint8_t *g = a.umem + eff;
+			const uint4 q0 = make_uint4(F[4], F[0], F[1], F[2]);
+			const uint4 q1 = make_uint4(0x0008u | (0x45u << 16) | (tos << 24),
+						    bswap16n(tot), 0x40u | (ttl << 16) | (p4 << 24),
+						    chk4 | (h3 << 16));
+			const uint4 q2 = make_uint4((h3 >> 16) | (h4 << 16), o13, o14, o15);
+			*reinterpret_cast<uint4 *>(g + 16) = q0;
+			*reinterpret_cast<uint4 *>(g + 32) = q1;
+			*reinterpret_cast<uint4 *>(g + 48) = q2;
+			if (tcp_upd)
+				*reinterpret_cast<uint32_t *>(g + 68) = e68;
+		}
+		if (active && !slow) {
+			a.action[i] = (uint8_t)act;
+			uint4 od = dv;
+			if (xlate) {
+				const uint64_t na = eff + 20;
+				od.x = (uint32_t)na;
+				od.y = (uint32_t)(na >> 32);
+				od.z = len - 20;
+			}
+			*reinterpret_cast<uint4 *>(a.out + i) = od;
+		}
+	}
+	__builtin_amdgcn_wave_barrier();
+	if ((uint32_t)lane < xq_n)
+		xl[xout + lane] = xq[lane];
+	if (lane == 0)
+		a.xcount[wgid] = xout + xq_n;
+}
+
+template <auto KERN>
+static uint32_t resident_n()
+{
+	static uint32_t cached = 0;
+	if (!cached) {
+		int per_cu = 0, dev = 0;
+		hipDeviceProp_t prop;
+		if (hipGetDevice(&dev) != hipSuccess ||
+		    hipGetDeviceProperties(&prop, dev) != hipSuccess ||
+		    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, KERN, kBlockN, 0) !=
+			    hipSuccess ||
+		    per_cu <= 0)
+			return 1024;
+		cached = (uint32_t)per_cu * (uint32_t)prop.multiProcessorCount;
+	}
+	return cached;
+}
+
+uint32_t nat64_grid(uint32_t n, uint32_t max_blocks)
+{
+	uint32_t cap = resident_n<xdp_nat64_fast_kernel>();
+	if (cap > max_blocks)
+		cap = max_blocks;
+	uint64_t tiles = ((uint64_t)n + kWaveN - 1) / kWaveN;
+	uint64_t blocks = (tiles + kWavesN - 1) / kWavesN;
+	if (blocks > cap)
+		blocks = cap;
+	return blocks ? (uint32_t)blocks : 1u;
+}
+
+hipError_t launch_nat64(const Nat64Args &a0, uint32_t max_blocks, hipStream_t stream)
+{
+	Nat64Args a = a0;
+	if (a.fast) {
+		const uint32_t blocks = nat64_grid(a.n, max_blocks);
+		a.nregions = blocks * kWavesN;
+		const uint64_t tiles = ((uint64_t)a.n + kWaveN - 1) / kWaveN;
+		a.xregion = (uint32_t)(((tiles + a.nregions - 1) / a.nregions) * kWaveN);
+		hipLaunchKernelGGL(xdp_nat64_fast_kernel, dim3(blocks), dim3(kBlockN), 0,
+				   stream, a);
+		hipError_t e = hipGetLastError();
+		if (e != hipSuccess)
+			return e;
+		uint32_t sb = resident_n<xdp_nat64_kernel>();
+		if (sb > max_blocks)
+			sb = max_blocks;
+		hipLaunchKernelGGL(xdp_nat64_kernel, dim3(sb), dim3(kBlockN), 0, stream, a);
+		return hipGetLastError();
+	}
+	a.xlist = nullptr;
 	uint64_t tiles = ((uint64_t)a.n + kWaveN - 1) / kWaveN;
 	uint64_t blocks = (tiles + kWavesN - 1) / kWavesN;
 	if (blocks > max_blocks)

@@ -472,6 +472,30 @@ int xdpgpu_nat64_dev(xdpgpu_ctx *ctx, void *d_umem, uint64_t umem_size,
 	a.v6mask = ctx->v6mask;
 	a.v4map = ctx->d_v4map;
 	a.v4mask = ctx->v4mask;
+	/* the fast kernel covers ingress under a /96 prefix; it shares slot
+	 * 0's deferral-list scratch with the RX path (a context runs one
+	 * launch sequence at a time) */
+	a.fast = ctx->ncfg.direction == XDPGPU_NAT64_INGRESS && ctx->ncfg.v6_plen == 96;
+	if (a.fast) {
+		int rc = ensure_xlist(ctx, ctx->slot[0], n);
+		if (rc)
+			return rc;
+		a.xlist = ctx->slot[0].d_xlist;
+		a.xcount = ctx->slot[0].d_xcount;
+		for (int k = 0; k < 4; k++) {
+			uint8_t m[4], w[4];
+			for (int j = 0; j < 4; j++) {
+				const uint32_t bit0 = 8 * (4 * k + j);
+				const uint32_t pl = ctx->ncfg.allow_plen;
+				const uint32_t nb = pl <= bit0 ? 0 : pl - bit0 >= 8 ? 8 : pl - bit0;
+				m[j] = (uint8_t)(nb ? (0xff00u >> nb) & 0xff : 0);
+				w[j] = ctx->ncfg.allow_prefix[4 * k + j] & m[j];
+			}
+			memcpy(&a.allow_m[k], m, 4);
+			memcpy(&a.allow_w[k], w, 4);
+		}
+		memcpy(a.pref_w, ctx->ncfg.v6_prefix, 12);
+	}
 	hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
 	HIP_TRY(ctx, launch_nat64(a, ctx->max_blocks, st));
 	return 0;

@@ -74,6 +74,13 @@ struct Nat64Args {
 	uint32_t v6mask;
 	const uint4 *v4map;
 	uint32_t v4mask;
+	/* fast path (ingress, /96 prefix): allowed-source words and masks,
+	 * the prefix's first 12 bytes, as LE u32 of the wire bytes */
+	uint32_t allow_w[4], allow_m[4], pref_w[3];
+	uint32_t fast;             /* 1: fast kernel + list of slow frames */
+	uint32_t *xlist;           /* slow frames, xregion per fast wave    */
+	uint32_t *xcount;
+	uint32_t xregion, nregions;
 };
 
 hipError_t launch_nat64(const Nat64Args &a, uint32_t max_blocks,
