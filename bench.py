@@ -221,6 +221,8 @@ def main():
     ap.add_argument("--window", type=int, default=64)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--legs", default="1500,imix,nat64",
+                    help="secondary workloads: comma list of 1500, imix, nat64")
     ap.add_argument("--imix-frames", type=int, default=16 << 20)
     ap.add_argument("--nat64-frames", type=int, default=16 << 20)
     ap.add_argument("--e2e", action="store_true", help="also time the host path")
@@ -271,25 +273,29 @@ def main():
         del d_umem
         torch.cuda.empty_cache()
         steps2 = max(5, args.steps // 5)
-        # 1500 B frames (BASELINE metric names both sizes), config 2 geometry
-        secondary["secondary_1500B"] = side_run(
-            ctx, tctx, dev, stream, 2 << 20, xdpgpu.POOL_UDP4, 1500, 0x5EED0012,
-            xdpgpu.TUPLE_V4, steps2, "config2-geometry 2M x 1500B IPv4/UDP, V4 tuple",
-            lambda ds: len(ds) * (16 + 16 + 16 + 1) + int(ds["len"].astype(np.int64).sum()))
-        # config 3: IMIX with the 44 B network_tuple (429.3 B/frame)
-        ctx3 = xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT, 0, xdpgpu.TUPLE_NET, 64)
-        tctx3 = xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT | xdpgpu.CFG_TIMING, 0,
-                              xdpgpu.TUPLE_NET, 64)
-        secondary["config3_imix"] = side_run(
-            ctx3, tctx3, dev, stream, args.imix_frames, xdpgpu.POOL_IMIX, 64, 0x5EED0003,
-            xdpgpu.TUPLE_NET, steps2,
-            f"config3: {args.imix_frames} IMIX frames (64/570/1500 7:4:1, VLAN, IPv6), "
-            "network_tuple",
-            lambda ds: len(ds) * (16 + 16 + 44 + 1) + int(ds["len"].astype(np.int64).sum()))
-        ctx3.close()
-        tctx3.close()
-        secondary["config4_nat64"] = nat64_run(dev, stream, args.nat64_frames, steps2,
-                                               local)
+        legs = set(args.legs.split(","))
+        if "1500" in legs:
+            # 1500 B frames (BASELINE metric names both sizes), config 2 geometry
+            secondary["secondary_1500B"] = side_run(
+                ctx, tctx, dev, stream, 2 << 20, xdpgpu.POOL_UDP4, 1500, 0x5EED0012,
+                xdpgpu.TUPLE_V4, steps2, "config2-geometry 2M x 1500B IPv4/UDP, V4 tuple",
+                lambda ds: len(ds) * (16 + 16 + 16 + 1) + int(ds["len"].astype(np.int64).sum()))
+        if "imix" in legs:
+            # config 3: IMIX with the 44 B network_tuple (429.3 B/frame)
+            ctx3 = xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT, 0, xdpgpu.TUPLE_NET, 64)
+            tctx3 = xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT | xdpgpu.CFG_TIMING, 0,
+                                  xdpgpu.TUPLE_NET, 64)
+            secondary["config3_imix"] = side_run(
+                ctx3, tctx3, dev, stream, args.imix_frames, xdpgpu.POOL_IMIX, 64, 0x5EED0003,
+                xdpgpu.TUPLE_NET, steps2,
+                f"config3: {args.imix_frames} IMIX frames (64/570/1500 7:4:1, VLAN, IPv6), "
+                "network_tuple",
+                lambda ds: len(ds) * (16 + 16 + 44 + 1) + int(ds["len"].astype(np.int64).sum()))
+            ctx3.close()
+            tctx3.close()
+        if "nat64" in legs:
+            secondary["config4_nat64"] = nat64_run(dev, stream, args.nat64_frames, steps2,
+                                                   local)
 
     e2e = None
     if args.e2e and rank == 0 and world == 1:

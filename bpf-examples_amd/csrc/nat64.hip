@@ -901,9 +901,11 @@ __global__ __launch_bounds__(kBlockN) void xdp_nat64_fast_kernel(Nat64Args a)
 			const uint32_t tot = (bswap16n(F[4] >> 16) + 20) & 0xffff;
 			const uint32_t ttl = (F[5] >> 8) & 0xff;
 			const uint32_t p4 = nh == 58 ? 1u : nh;
-			/* IPv4 header checksum (csum_fold_helper of the header) */
+			/* IPv4 header checksum (csum_fold_helper of the header):
+			 * LE 16-bit words; frag_off is the wire bytes 0x40 0x00
+			 * (DF), the LE word 0x0040 */
 			uint32_t hs = halves2(0x45u | (tos << 8) | (bswap16n(tot) << 16)) +
-				      0x4000u + (ttl | (p4 << 8)) + halves2(h3) + halves2(h4);
+				      0x0040u + (ttl | (p4 << 8)) + halves2(h3) + halves2(h4);
 			hs = (hs & 0xffff) + (hs >> 16);
 			hs = (hs & 0xffff) + (hs >> 16);
 			const uint32_t chk4 = ~hs & 0xffff;

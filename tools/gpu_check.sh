@@ -23,7 +23,7 @@ step() {  # name timeout cmd...
 for s in $STEPS; do
 	case $s in
 	smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-	pytest) step pytest 900 python -m pytest tests -m gpu -x -q ;;
+	pytest) step pytest 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
 	bench)  step bench 600 python bench.py ;;
 	prof)   cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 		step prof 600 rocprofv3 --kernel-trace --stats --output-format csv \
