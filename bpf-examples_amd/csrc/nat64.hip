@@ -16,8 +16,9 @@
  * edge is not).  Headers past the staged window (long IPv6 extension
  * chains) are read from HBM.
  *
- * The static v6_state_map / v4_reversemap are open-addressing tables in
- * HBM (32 B slots, linear probing), built by the host (xdpgpu.cpp).
+ * The static v6_state_map / v4_reversemap are hash tables in HBM of
+ * 4-way, 128-byte buckets (one line per lookup), built by the host
+ * (xdpgpu.cpp, xdpgpu_internal.h).
  *
  * Checksum arithmetic: bpf_csum_diff and bpf_l4_csum_replace restated mod
  * 0xffff (see oracle/nat64_oracle.c for the derivation): each update is
@@ -299,26 +300,37 @@ __device__ __forceinline__ bool v4pos(uint32_t plen, int (&pos)[4], int &pref_en
 }
 
 struct Tables {
-	const uint4 *v6map;    /* slots: {v6 w0..w3} then {v4, used, 0, 0} */
-	uint32_t v6mask;
-	const uint4 *v4map;    /* slots: {v4, used, 0, 0} then {v6 w0..w3} */
-	uint32_t v4mask;
+	const Nat64V6Bucket *v6map;
+	uint32_t v6nb;
+	const Nat64V4Bucket *v4map;
+	uint32_t v4nb;
 };
 
-/* v6_state_map lookup: v4 (host order) or 0 */
+/* v6_state_map lookup: v4 (host order) or 0.  One 128-byte bucket per
+ * probe: the four keys and the value word are 16-byte loads of one line. */
 __device__ uint32_t lookup_v6(const Tables &T, const uint32_t (&w)[4], bool &found)
 {
-	uint32_t s = slot_hash(w[0], w[1], w[2], w[3]) & T.v6mask;
-	for (uint32_t probe = 0; probe <= T.v6mask; probe++) {
-		const uint4 k = T.v6map[2 * s];
-		const uint4 v = T.v6map[2 * s + 1];
-		if (!v.y)
-			break;
-		if (k.x == w[0] && k.y == w[1] && k.z == w[2] && k.w == w[3]) {
-			found = true;
-			return v.x;
+	uint32_t b = nat64_home(slot_hash(w[0], w[1], w[2], w[3]), T.v6nb);
+	for (uint32_t probe = 0; probe < T.v6nb; probe++) {
+		const Nat64V6Bucket *B = T.v6map + b;
+		uint4 k[4];
+#pragma unroll
+		for (int j = 0; j < 4; j++)
+			k[j] = B->key[j];
+		const uint4 v = *reinterpret_cast<const uint4 *>(B->val);
+		const uint32_t cnt = B->n;
+		const uint32_t vals[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+		for (int j = 0; j < 4; j++) {
+			if ((uint32_t)j < cnt && k[j].x == w[0] && k[j].y == w[1] &&
+			    k[j].z == w[2] && k[j].w == w[3]) {
+				found = true;
+				return vals[j];
+			}
 		}
-		s = (s + 1) & T.v6mask;
+		if (cnt < 4)
+			break;
+		b = b + 1 == T.v6nb ? 0 : b + 1;
 	}
 	found = false;
 	return 0;
@@ -326,20 +338,26 @@ __device__ uint32_t lookup_v6(const Tables &T, const uint32_t (&w)[4], bool &fou
 
 __device__ bool lookup_v4(const Tables &T, uint32_t v4, uint32_t (&w)[4])
 {
-	uint32_t s = slot_hash(v4, 0, 0, 0) & T.v4mask;
-	for (uint32_t probe = 0; probe <= T.v4mask; probe++) {
-		const uint4 k = T.v4map[2 * s];
-		if (!k.y)
-			break;
-		if (k.x == v4) {
-			const uint4 v = T.v4map[2 * s + 1];
-			w[0] = v.x;
-			w[1] = v.y;
-			w[2] = v.z;
-			w[3] = v.w;
-			return true;
+	uint32_t b = nat64_home(slot_hash(v4, 0, 0, 0), T.v4nb);
+	for (uint32_t probe = 0; probe < T.v4nb; probe++) {
+		const Nat64V4Bucket *B = T.v4map + b;
+		const uint4 k = *reinterpret_cast<const uint4 *>(B->key);
+		const uint32_t cnt = B->n;
+		const uint32_t keys[4] = {k.x, k.y, k.z, k.w};
+#pragma unroll
+		for (int j = 0; j < 4; j++) {
+			if ((uint32_t)j < cnt && keys[j] == v4) {
+				const uint4 v = B->val[j];
+				w[0] = v.x;
+				w[1] = v.y;
+				w[2] = v.z;
+				w[3] = v.w;
+				return true;
+			}
 		}
-		s = (s + 1) & T.v4mask;
+		if (cnt < 4)
+			break;
+		b = b + 1 == T.v4nb ? 0 : b + 1;
 	}
 	return false;
 }
@@ -584,7 +602,7 @@ __global__ __launch_bounds__(kBlockN) void xdp_nat64_kernel(Nat64Args a)
 	uint32_t *rows = rows_all + wid * kWaveN * kRowDw;
 	uint64_t *dtab = dtab_all + wid * kWaveN;
 	uint8_t *rb = reinterpret_cast<uint8_t *>(rows + lane * kRowDw);
-	const Tables T = {a.v6map, a.v6mask, a.v4map, a.v4mask};
+	const Tables T = {a.v6map, a.v6nb, a.v4map, a.v4nb};
 	const uint64_t us16 = (a.usize + 15) & ~15ull;
 
 	/* work: every frame (a.xlist null) or the fast kernel's slow-frame
@@ -706,7 +724,8 @@ __global__ __launch_bounds__(kBlockN) void xdp_nat64_kernel(Nat64Args a)
  * swizzle); everything else happens in registers: field extraction at
  * fixed offsets, the static-map probe, the IPv4 header and its checksum,
  * the incremental L4 update (TCP's check word at 70 is a second, narrow
- * load) and three 16-byte stores of frame bytes [16, 64).  Frames of other
+ * load).  The frame's new first 64 bytes are staged in LDS and written
+ * back transposed (four lanes per frame, whole 64-byte sectors).  Frames of other
  * shapes go to the wave's slow list (xdp_nat64_kernel). */
 
 typedef __attribute__((address_space(3))) void lds_void_n;
@@ -726,12 +745,18 @@ __global__ __launch_bounds__(kBlockN) void xdp_nat64_fast_kernel(Nat64Args a)
 	__shared__ uint4 buf_all[kWavesN * 4 * kWaveN];
 	__shared__ uint64_t dtab_all[kWavesN * kWaveN];
 	__shared__ uint32_t xq_all[kWavesN * 2 * kWaveN];
+	/* translated first 64 bytes of each frame, stored transposed */
+	__shared__ uint4 obuf_all[kWavesN * 4 * kWaveN];
+	__shared__ uint64_t otab_all[kWavesN * kWaveN];
 	const int lane = threadIdx.x & (kWaveN - 1);
 	const int wid = threadIdx.x / kWaveN;
 	uint4 *buf = buf_all + wid * 4 * kWaveN;
 	uint64_t *dtab = dtab_all + wid * kWaveN;
 	uint32_t *xq = xq_all + wid * 2 * kWaveN;
-	const Tables T = {a.v6map, a.v6mask, a.v4map, a.v4mask};
+	uint4 *obuf = obuf_all + wid * 4 * kWaveN;
+	uint64_t *otab = otab_all + wid * kWaveN;
+	const int osw = (lane >> 2) & 3;
+	const Tables T = {a.v6map, a.v6nb, a.v4map, a.v4nb};
 
 	const uint64_t ntiles = ((uint64_t)a.n + kWaveN - 1) / kWaveN;
 	const uint64_t nwaves = (uint64_t)gridDim.x * kWavesN;
@@ -858,7 +883,12 @@ __global__ __launch_bounds__(kBlockN) void xdp_nat64_fast_kernel(Nat64Args a)
 		uint32_t v4 = 0;
 		if (xlate) {
 			bool found;
-			v4 = lookup_v6(T, s, found);
+			if (a.diag & 1) {
+				found = true;
+				v4 = 0x0A630001u;
+			} else {
+				v4 = lookup_v6(T, s, found);
+			}
 			if (!found) {
 				xlate = false;
 				act = XDPGPU_NAT64_NO_STATE;
@@ -894,7 +924,9 @@ __global__ __launch_bounds__(kBlockN) void xdp_nat64_fast_kernel(Nat64Args a)
 			}
 		}
 
-		if (xlate) {
+		const bool put = xlate && !(a.diag & 2);
+		otab[lane] = put ? eff : ~0ull;
+		if (put) {
 			const uint32_t h3 = __builtin_bswap32(v4);        /* src, LE word */
 			const uint32_t h4 = d[3];
 			const uint32_t tos = (((F[3] >> 16) & 0xf) << 4) | (F[3] >> 28);
@@ -943,21 +975,36 @@ __global__ __launch_bounds__(kBlockN) void xdp_nat64_fast_kernel(Nat64Args a)
 				o13 = (h4 >> 16) | (ha << 16);
 				o14 = (F[14] & 0xffff0000u) | c;
 			}
-			/* frame bytes [16, 64): unchanged [16, 20), the L2 header
-			 * moved to 20 with h_proto 0x0800, the IPv4 header at
-			 * 34, the L4 bytes at 54 */
-			uint8_t *g = a.umem + eff;
-			const uint4 q0 = make_uint4(F[4], F[0], F[1], F[2]);
-			const uint4 q1 = make_uint4(0x0008u | (0x45u << 16) | (tos << 24),
-						    bswap16n(tot), 0x40u | (ttl << 16) | (p4 << 24),
-						    chk4 | (h3 << 16));
-			const uint4 q2 = make_uint4((h3 >> 16) | (h4 << 16), o13, o14, o15);
-			*reinterpret_cast<uint4 *>(g + 16) = q0;
-			*reinterpret_cast<uint4 *>(g + 32) = q1;
-			*reinterpret_cast<uint4 *>(g + 48) = q2;
+			/* frame bytes [0, 64): unchanged [0, 20) (rewritten so
+			 * that the stores are whole 64-byte sectors), the L2
+			 * header moved to 20 with h_proto 0x0800, the IPv4
+			 * header at 34, the L4 bytes at 54; staged in LDS in the
+			 * swizzled slots of the header buffer's layout */
+			obuf[4 * lane + (0 ^ osw)] = make_uint4(F[0], F[1], F[2], F[3]);
+			obuf[4 * lane + (1 ^ osw)] = make_uint4(F[4], F[0], F[1], F[2]);
+			obuf[4 * lane + (2 ^ osw)] =
+				make_uint4(0x0008u | (0x45u << 16) | (tos << 24),
+					   bswap16n(tot), 0x40u | (ttl << 16) | (p4 << 24),
+					   chk4 | (h3 << 16));
+			obuf[4 * lane + (3 ^ osw)] =
+				make_uint4((h3 >> 16) | (h4 << 16), o13, o14, o15);
 			if (tcp_upd)
-				*reinterpret_cast<uint32_t *>(g + 68) = e68;
+				*reinterpret_cast<uint32_t *>(a.umem + eff + 68) = e68;
 		}
+		/* transposed stores: in store k lane l writes chunk l & 3 of
+		 * frame 16k + l / 4, so four lanes write one frame's 64 bytes
+		 * as a whole sector */
+		__builtin_amdgcn_wave_barrier();
+#pragma unroll
+		for (int k = 0; k < 4; k++) {
+			const int f = 16 * k + (lane >> 2);
+			const int c = lane & 3;
+			const uint64_t e = otab[f];
+			if (e != ~0ull)
+				*reinterpret_cast<uint4 *>(a.umem + e + 16 * c) =
+					obuf[4 * f + (c ^ ((f >> 2) & 3))];
+		}
+		__builtin_amdgcn_wave_barrier();
 		if (active && !slow) {
 			a.action[i] = (uint8_t)act;
 			uint4 od = dv;

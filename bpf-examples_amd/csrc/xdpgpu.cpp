@@ -65,8 +65,9 @@ struct xdpgpu_ctx {
 	/* nat64 translator (xdpgpu_nat64_setup) */
 	bool nat64 = false;
 	xdpgpu_nat64_cfg ncfg;
-	uint4 *d_v6map = nullptr, *d_v4map = nullptr;
-	uint32_t v6mask = 0, v4mask = 0;
+	Nat64V6Bucket *d_v6map = nullptr;
+	Nat64V4Bucket *d_v4map = nullptr;
+	uint32_t nb = 0;           /* buckets of each table */
 	uint32_t tn = 0;
 	char err[256];
 };
@@ -389,15 +390,11 @@ int xdpgpu_process_dev(xdpgpu_ctx *ctx, void *d_umem, uint64_t umem_size,
 
 /* ---- nat64 ---- */
 
-/* Open-addressing table of 2 x uint4 per slot, power-of-two capacity of at
- * least twice the entries, linear probing (nat64.hip lookup_v6/lookup_v4).
- * kv: per entry the probe key words and the two slot halves. */
-static uint32_t nat64_cap(uint32_t n)
+/* Buckets of the static tables: 4 slots each, 3 entries per bucket on
+ * average, so that an overflow into the next bucket is rare. */
+static uint32_t nat64_buckets(uint32_t n)
 {
-	uint32_t cap = 64;
-	while (cap < 2 * n)
-		cap <<= 1;
-	return cap;
+	return n < 3 ? 1u : (n + 2) / 3;
 }
 
 int xdpgpu_nat64_setup(xdpgpu_ctx *ctx, const xdpgpu_nat64_cfg *cfg,
@@ -411,39 +408,61 @@ int xdpgpu_nat64_setup(xdpgpu_ctx *ctx, const xdpgpu_nat64_cfg *cfg,
 	if (cfg->direction > XDPGPU_NAT64_EGRESS || cfg->allow_plen > 128 ||
 	    (cfg->v4_prefix & ~cfg->v4_mask) || nmap > (1u << 30))
 		return -EINVAL;
-	const uint32_t cap = nat64_cap(nmap);
-	std::vector<uint4> v6t((size_t)cap * 2, make_uint4(0, 0, 0, 0));
-	std::vector<uint4> v4t((size_t)cap * 2, make_uint4(0, 0, 0, 0));
+	const uint32_t nb = nat64_buckets(nmap);
+	std::vector<Nat64V6Bucket> v6t(nb);
+	std::vector<Nat64V4Bucket> v4t(nb);
+	memset(v6t.data(), 0, nb * sizeof(Nat64V6Bucket));
+	memset(v4t.data(), 0, nb * sizeof(Nat64V4Bucket));
 	for (uint32_t e = 0; e < nmap; e++) {
 		uint32_t w[4];
 		memcpy(w, map[e].v6, 16);
-		uint32_t sl = nat64_slot_hash(w[0], w[1], w[2], w[3]) & (cap - 1);
-		while (v6t[2 * sl + 1].y &&
-		       !(v6t[2 * sl].x == w[0] && v6t[2 * sl].y == w[1] &&
-			 v6t[2 * sl].z == w[2] && v6t[2 * sl].w == w[3]))
-			sl = (sl + 1) & (cap - 1);
-		v6t[2 * sl] = make_uint4(w[0], w[1], w[2], w[3]);
-		v6t[2 * sl + 1] = make_uint4(map[e].v4, 1, 0, 0);
-		sl = nat64_slot_hash(map[e].v4, 0, 0, 0) & (cap - 1);
-		while (v4t[2 * sl].y && v4t[2 * sl].x != map[e].v4)
-			sl = (sl + 1) & (cap - 1);
-		v4t[2 * sl] = make_uint4(map[e].v4, 1, 0, 0);
-		v4t[2 * sl + 1] = make_uint4(w[0], w[1], w[2], w[3]);
+		/* a repeated key keeps the last value, as a map update would */
+		uint32_t b = nat64_home(nat64_slot_hash(w[0], w[1], w[2], w[3]), nb);
+		for (;;) {
+			Nat64V6Bucket &B = v6t[b];
+			uint32_t j = 0;
+			while (j < B.n && !(B.key[j].x == w[0] && B.key[j].y == w[1] &&
+					    B.key[j].z == w[2] && B.key[j].w == w[3]))
+				j++;
+			if (j < 4) {
+				B.key[j] = make_uint4(w[0], w[1], w[2], w[3]);
+				B.val[j] = map[e].v4;
+				B.n = std::max(B.n, j + 1);
+				break;
+			}
+			b = b + 1 == nb ? 0 : b + 1;
+		}
+		b = nat64_home(nat64_slot_hash(map[e].v4, 0, 0, 0), nb);
+		for (;;) {
+			Nat64V4Bucket &B = v4t[b];
+			uint32_t j = 0;
+			while (j < B.n && B.key[j] != map[e].v4)
+				j++;
+			if (j < 4) {
+				B.key[j] = map[e].v4;
+				B.val[j] = make_uint4(w[0], w[1], w[2], w[3]);
+				B.n = std::max(B.n, j + 1);
+				break;
+			}
+			b = b + 1 == nb ? 0 : b + 1;
+		}
 	}
 	HIP_TRY(ctx, hipSetDevice(ctx->cfg.device));
 	if (ctx->d_v6map)
 		(void)hipFree(ctx->d_v6map);
 	if (ctx->d_v4map)
 		(void)hipFree(ctx->d_v4map);
-	ctx->d_v6map = ctx->d_v4map = nullptr;
+	ctx->d_v6map = nullptr;
+	ctx->d_v4map = nullptr;
 	ctx->nat64 = false;
-	const size_t bytes = (size_t)cap * 2 * sizeof(uint4);
-	if (hipMalloc(&ctx->d_v6map, bytes) != hipSuccess ||
-	    hipMalloc(&ctx->d_v4map, bytes) != hipSuccess)
-		return set_err(ctx, -ENOMEM, "nat64 tables of %u slots", cap);
-	HIP_TRY(ctx, hipMemcpy(ctx->d_v6map, v6t.data(), bytes, hipMemcpyHostToDevice));
-	HIP_TRY(ctx, hipMemcpy(ctx->d_v4map, v4t.data(), bytes, hipMemcpyHostToDevice));
-	ctx->v6mask = ctx->v4mask = cap - 1;
+	if (hipMalloc(&ctx->d_v6map, nb * sizeof(Nat64V6Bucket)) != hipSuccess ||
+	    hipMalloc(&ctx->d_v4map, nb * sizeof(Nat64V4Bucket)) != hipSuccess)
+		return set_err(ctx, -ENOMEM, "nat64 tables of %u buckets", nb);
+	HIP_TRY(ctx, hipMemcpy(ctx->d_v6map, v6t.data(), nb * sizeof(Nat64V6Bucket),
+			       hipMemcpyHostToDevice));
+	HIP_TRY(ctx, hipMemcpy(ctx->d_v4map, v4t.data(), nb * sizeof(Nat64V4Bucket),
+			       hipMemcpyHostToDevice));
+	ctx->nb = nb;
 	ctx->ncfg = *cfg;
 	ctx->nat64 = true;
 	return 0;
@@ -469,13 +488,14 @@ int xdpgpu_nat64_dev(xdpgpu_ctx *ctx, void *d_umem, uint64_t umem_size,
 	a.out = d_out;
 	a.cfg = ctx->ncfg;
 	a.v6map = ctx->d_v6map;
-	a.v6mask = ctx->v6mask;
+	a.v6nb = ctx->nb;
 	a.v4map = ctx->d_v4map;
-	a.v4mask = ctx->v4mask;
+	a.v4nb = ctx->nb;
 	/* the fast kernel covers ingress under a /96 prefix; it shares slot
 	 * 0's deferral-list scratch with the RX path (a context runs one
 	 * launch sequence at a time) */
 	a.fast = ctx->ncfg.direction == XDPGPU_NAT64_INGRESS && ctx->ncfg.v6_plen == 96;
+	a.diag = (ctx->cfg.tune >> 12) & 3;
 	if (a.fast) {
 		int rc = ensure_xlist(ctx, ctx->slot[0], n);
 		if (rc)

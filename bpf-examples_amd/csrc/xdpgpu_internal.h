@@ -62,6 +62,31 @@ uint32_t rx_grid_blocks(uint32_t n, uint32_t max_blocks);
 uint32_t rx_xregion(uint32_t n, uint32_t blocks);
 hipError_t launch_ceiling(const RxArgs &a, uint32_t blocks, hipStream_t stream);
 
+/* nat64 static tables (v6_state_map and v4_reversemap, nat64_kern.c:17-46):
+ * 4-way buckets of one 128-byte line, so a lookup touches one line; the
+ * home bucket is fastrange(nat64_slot_hash(key), nbuckets), a full bucket
+ * overflows into the next (linear probing over buckets). */
+struct Nat64V6Bucket {
+	uint4 key[4];              /* IPv6 address words as stored          */
+	uint32_t val[4];           /* IPv4 address, host order              */
+	uint32_t n;                /* slots used (0..4)                     */
+	uint32_t pad[11];
+};
+struct Nat64V4Bucket {
+	uint32_t key[4];           /* IPv4 address, host order              */
+	uint32_t n;
+	uint32_t pad[3];
+	uint4 val[4];              /* IPv6 address words                    */
+	uint4 pad2[2];
+};
+static_assert(sizeof(Nat64V6Bucket) == 128 && sizeof(Nat64V4Bucket) == 128,
+	      "one cache line per bucket");
+
+__host__ __device__ inline uint32_t nat64_home(uint32_t h, uint32_t nbuckets)
+{
+	return (uint32_t)(((uint64_t)h * nbuckets) >> 32);
+}
+
 struct Nat64Args {
 	uint8_t *umem;
 	uint64_t usize;
@@ -70,14 +95,16 @@ struct Nat64Args {
 	uint8_t *action;
 	xdpgpu_desc *out;
 	xdpgpu_nat64_cfg cfg;
-	const uint4 *v6map;        /* 2 x uint4 per slot, v6mask + 1 slots */
-	uint32_t v6mask;
-	const uint4 *v4map;
-	uint32_t v4mask;
+	const Nat64V6Bucket *v6map;
+	uint32_t v6nb;             /* buckets */
+	const Nat64V4Bucket *v4map;
+	uint32_t v4nb;
 	/* fast path (ingress, /96 prefix): allowed-source words and masks,
 	 * the prefix's first 12 bytes, as LE u32 of the wire bytes */
 	uint32_t allow_w[4], allow_m[4], pref_w[3];
 	uint32_t fast;             /* 1: fast kernel + list of slow frames */
+	uint32_t diag;             /* cfg.tune bits 12-13 (diagnostic A/B):
+				    * 1 no map probe, 2 no frame stores */
 	uint32_t *xlist;           /* slow frames, xregion per fast wave    */
 	uint32_t *xcount;
 	uint32_t xregion, nregions;
