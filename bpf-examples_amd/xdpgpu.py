@@ -30,7 +30,8 @@ except Exception:  # pragma: no cover - torch is optional for host-only use
     torch = None
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "csrc", "libxdpgpu.so")
+# XDPGPU_LIB: another build of the same ABI (A/B timing of kernel versions)
+LIB_PATH = os.environ.get("XDPGPU_LIB") or os.path.join(HERE, "csrc", "libxdpgpu.so")
 
 # enum xdp_action values
 ABORTED, DROP, PASS, TX, REDIRECT = 0, 1, 2, 3, 4

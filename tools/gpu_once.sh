@@ -1,9 +1,11 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_nat64.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest.log
-[ $rc -eq 0 ] || exit $rc
-for t in 0 0x1000 0x2000; do
-timeout -k 10 120 python3 tools/nat64_probe.py --tune $t > gpurun_out/probe.log 2>&1; rc=$?; tail -1 gpurun_out/probe.log
-[ $rc -eq 0 ] || exit $rc
+OLD=build/ab_01e11cb/libxdpgpu.so
+for rep in 1 2; do
+for lib in $OLD bpf-examples_amd/csrc/libxdpgpu.so; do
+  echo "== $lib"
+  XDPGPU_LIB=$lib timeout -k 10 300 python3 tools/tune_rx.py --variants ceil,64:0 --rounds 5 > gpurun_out/t64.log 2>&1 || exit 3; grep -v amdgpu.ids gpurun_out/t64.log
+  XDPGPU_LIB=$lib timeout -k 10 300 python3 tools/tune_rx.py --variants 64:0 --rounds 5 --frames 2097152 --size 1500 > gpurun_out/t1500.log 2>&1 || exit 3; grep -v amdgpu.ids gpurun_out/t1500.log
+done
 done

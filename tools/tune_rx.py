@@ -23,11 +23,12 @@ def main():
     ap.add_argument("--size", type=int, default=64)
     ap.add_argument("--kind", type=int, default=xdpgpu.POOL_UDP4)
     ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EED0002)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--variants", default="ceil,64:0,64:256,64:512,128:0")
     args = ap.parse_args()
     n = args.frames
-    umem, descs, expect = xdpgpu.pool_generate(n, args.kind, args.size, 0x5EED0002)
+    umem, descs, expect = xdpgpu.pool_generate(n, args.kind, args.size, args.seed)
     dev = torch.device("cuda:0")
     d_umem = torch.zeros(umem.nbytes + 64, dtype=torch.uint8, device=dev)
     d_umem[: umem.nbytes].copy_(torch.from_numpy(umem))
@@ -59,6 +60,21 @@ def main():
             times[v].append(ev[0].elapsed_time(ev[1]) / args.reps)
             if v != "ceil" and r == 0:
                 ok[v] = bool(np.array_equal(d_v.cpu().numpy(), expect))
+    splits = {}
+    for v in ctxs:
+        if v == "ceil":
+            continue
+        w, t = (int(x) for x in v.split(":"))
+        with xdpgpu.XdpGpu(0, xdpgpu.CFG_DEFAULT | xdpgpu.CFG_TIMING, 0, xdpgpu.TUPLE_V4, w,
+                           tune=t) as tc:
+            tc.process_dev(d_umem, umem.nbytes, d_desc, n, d_v, d_res, d_tup, s)
+            torch.cuda.synchronize()
+            tc.kernel_times()
+            for _ in range(args.reps):
+                tc.process_dev(d_umem, umem.nbytes, d_desc, n, d_v, d_res, d_tup, s)
+            torch.cuda.synchronize()
+            kt = tc.kernel_times()
+            splits[v] = {k: round(kt[k], 4) for k in ("fast_ms", "exception_ms", "bulk_ms")}
     for v, ts in times.items():
         med = float(np.median(ts))
         print(json.dumps({"variant": v, "ms_median": round(med, 4),
@@ -66,7 +82,7 @@ def main():
                           "gbps": round(n * bpf / med / 1e6, 1),
                           "gpps": round(n / med / 1e6, 2),
                           "frac": round(n * bpf / med / 1e6 / 8000, 4),
-                          "verdicts_ok": ok.get(v)}), flush=True)
+                          "verdicts_ok": ok.get(v), "split": splits.get(v)}), flush=True)
 
 
 if __name__ == "__main__":
