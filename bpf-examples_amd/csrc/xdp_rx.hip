@@ -893,10 +893,8 @@ __device__ __forceinline__ void generic_batch(const RxArgs &a, uint32_t *win,
 	const uint64_t ym = __ballot(active && ydef);
 	if (ym) {
 		uint32_t base = 0;
-		if (lane == 0) {
+		if (lane == 0)
 			base = atomicAdd(yc, (uint32_t)__popcll(ym));
-			atomicMax(a.gmax + 2, (base + (uint32_t)__popcll(ym) + kWave - 1) / kWave);
-		}
 		base = __builtin_amdgcn_readfirstlane(base);
 		if (active && ydef) {
 			const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
@@ -1188,7 +1186,7 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
  * payload sum here and go to the bulk list; every other frame is deferred
  * to the exception kernel.
  */
-template <int MINW, bool TRIV>
+template <int MINW>
 __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 {
 	constexpr int XQ = 2 * kWave;      /* deferral queues per wave */
@@ -1218,15 +1216,13 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 	uint64_t my_bytes = 0;
 	/* queued / flushed deferrals (uniform): exception and bulk lists */
 	uint32_t xq_n = 0, xout = 0, bq_n = 0, bout = 0;
-	/* the previous launch's follow-up kernels are done with the other
-	 * maxima set (stream order): zero it for the next launch */
-	if (blockIdx.x == 0 && threadIdx.x < 3)
-		a.gmax_next[threadIdx.x] = 0;
 
-	/* append the frames of the lanes with want set to this wave's region
-	 * of a list: LDS queue in lane order, flushed 64 entries at a time */
+	/* append the frames of the lanes with want set to a list: LDS queue
+	 * in lane order, flushed 64 entries at a time either to this wave's
+	 * region (ctr null) or to a device-wide compact list whose length ctr
+	 * counts (one atomic per 64 entries) */
 	auto defer = [&](bool want, uint64_t i, uint32_t *q, uint32_t &qn,
-			 uint32_t *gl, uint32_t &gout) {
+			 uint32_t *gl, uint32_t &gout, uint32_t *ctr) {
 		const uint64_t dm = __ballot(want);
 		if (!dm)
 			return;
@@ -1237,7 +1233,14 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 		qn += (uint32_t)__popcll(dm);
 		if (qn >= (uint32_t)kWave) {
 			__builtin_amdgcn_wave_barrier();
-			gl[gout + lane] = q[lane];
+			uint32_t at = gout;
+			if (ctr) {
+				uint32_t base = 0;
+				if (lane == 0)
+					base = atomicAdd(ctr, (uint32_t)kWave);
+				at = __builtin_amdgcn_readfirstlane(base);
+			}
+			gl[at + lane] = q[lane];
 			gout += kWave;
 			const uint32_t rest = q[kWave + lane];
 			__builtin_amdgcn_wave_barrier();
@@ -1352,41 +1355,10 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 		fast = shape & (l4 + cl + (cl & 1) <= 64u);
 		const bool bulk = shape & !fast & (a.res != nullptr);
 
-		/* trivial verdicts, decided here with an all-zero record: ARP and
-		 * NDP pass (af_xdp_kern.c:114-148), and frames the parse aborts
-		 * on (parsing_helpers.h:174-318) in the order the exception
-		 * path checks them: runts, IPv4 header bounds / version / ihl /
-		 * tot_len, UDP length, TCP data offset, IPv6 header bounds /
-		 * version, a truncated ICMPv6 header.  Only with the VLAN tags
-		 * all consumed (len >= l3) and no IPv4 options or fragment in
-		 * the L4 tests. */
-		const bool valid_d = active & ((uint64_t)len <= a.usize) & (eff <= a.usize - len);
-		const bool tg = (!a.force_generic) & staged & (len >= l3);
-		const uint32_t et = r[3] & 0xffff;
-		const bool arp = tg & (et == 0x0608u);
-		const uint32_t vihl = (r[3] >> 16) & 0xff, hl = (vihl & 0xf) * 4;
-		const bool a4 = (len < l3 + 20) | ((vihl >> 4) != 4) | (hl < 20) |
-				(l3 + hl > len) | (tot < hl) | (l3 + tot > len);
-		const bool b_udp = (len < l4 + 8) | (cl < 8) | (l4 + cl > l3 + tot);
-		const bool b_tcp = (len < l4 + 20) | (thl < 20) | (l4 + thl > len) |
-				   (tot - 20 < thl);
-		const bool plain4 = (hl == 20) & ((r[5] & 0xff3fu) == 0);
-		const bool abort4 = tg & (et == 0x0008u) &
-				    (a4 | (plain4 & ((udp & b_udp) | ((proto == 6) & b_tcp))));
-		const uint32_t nh6 = r[5] & 0xff, type6 = (r[13] >> 16) & 0xff;
-		const bool a6 = (len < l3 + 40) | (((r[3] >> 20) & 0xf) != 6);
-		const bool ip6 = tg & (et == 0xdd86u);
-		const bool abort6 = ip6 & (a6 | ((nh6 == 58) & (len < l3 + 48)));
-		const bool ndp = ip6 & !a6 & (nh6 == 58) & (len >= l3 + 48) &
-				 (type6 - 133u <= 4u);
-		const bool runt = (!a.force_generic) & valid_d & (len < 14);
-		const bool triv = TRIV & (arp | ndp | abort4 | abort6 | runt);
-		const bool tpass = arp | ndp;
-
 		/* 3. defer the frames of other shapes to the exception list and
-		 * the long ones to the bulk list */
-		defer(active && !fast && !bulk && !triv, i, xq, xq_n, xl, xout);
-		defer(bulk, i, bq, bq_n, bl, bout);
+		 * the long ones to the bulk list of this wave */
+		defer(active && !fast && !bulk, i, xq, xq_n, xl, xout, nullptr);
+		defer(bulk, i, bq, bq_n, bl, bout, nullptr);
 
 		/* 4. fast frames: flow key, hash, tuple, checksums, verdict */
 		const uint32_t sa = (r[6] >> 16) | (r[7] << 16);
@@ -1455,27 +1427,10 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 				}
 			}
 			my_bytes += fast ? len : 0;
-		} else if (triv) {
-			a.verdict[i] = (uint8_t)(tpass ? XDPGPU_PASS : XDPGPU_ABORTED);
-			if (a.res)
-				st_nt16(a.res + i, make_uint4(0, 0, 0, 0));
-			if (a.tup) {
-				if (a.tuple_fmt == XDPGPU_TUPLE_V4) {
-					st_nt16(a.tup + 16 * i, make_uint4(0, 0, 0, 0));
-				} else if (a.tuple_fmt == XDPGPU_TUPLE_NET) {
-					uint32_t *tp = reinterpret_cast<uint32_t *>(a.tup + 44 * i);
-#pragma unroll
-					for (int j = 0; j < 11; j++)
-						tp[j] = 0;
-				}
-			}
-			my_bytes += len;
 		}
 		/* counters (wave-uniform: ballots outside divergent code) */
 		if (a.stats) {
-			cnt[CNT_FRAMES] += __popcll(__ballot(fast || triv));
-			cnt[CNT_VERDICT0 + XDPGPU_PASS] += __popcll(__ballot(triv && tpass));
-			cnt[CNT_VERDICT0 + XDPGPU_ABORTED] += __popcll(__ballot(triv && !tpass));
+			cnt[CNT_FRAMES] += __popcll(__ballot(fast));
 			cnt[CNT_VERDICT0 + XDPGPU_DROP] += __popcll(__ballot(fast && drop));
 			cnt[CNT_VERDICT0 + XDPGPU_REDIRECT] += __popcll(__ballot(fast && !drop));
 			cnt[CNT_L3_BAD] += __popcll(__ballot(fast && !l3_ok));
@@ -1489,20 +1444,30 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 	if ((uint32_t)lane < bq_n)
 		bl[bout + lane] = bq[lane];
 	if (lane == 0) {
-		const uint32_t nx = xout + xq_n, nb = bout + bq_n;
-		a.xcount[wgid] = nx;
-		a.bcount[wgid] = nb;
+		a.xcount[wgid] = xout + xq_n;
+		a.bcount[wgid] = bout + bq_n;
 		a.ycount[wgid] = 0;   /* filled by the exception kernel */
-		/* no-return atomics (executed at the memory side) */
-		if (nx)
-			atomicMax(a.gmax + 0, (nx + kWave - 1) / kWave);
-		if (nb)
-			atomicMax(a.gmax + 1, (nb + kWave - 1) / kWave);
 	}
 
 	block_stats_flush(a, blk_cnt, cnt, my_bytes, lane);
 }
 
+
+/* Assignment of the fast kernel's wave regions to the waves of a
+ * follow-up kernel: with at least as many waves as regions, m = W / R waves
+ * share a region and take its batches round robin; otherwise waves stride
+ * over regions.  Each wave reads a region's count once. */
+struct RegionWalk {
+	uint32_t first, rstep, bfirst, bstep;
+	__device__ RegionWalk(uint32_t regions, uint32_t waves, uint32_t w)
+	{
+		const uint32_t m = waves >= regions ? waves / regions : 1;
+		first = w / m;
+		rstep = waves / m;
+		bfirst = (w % m) * kWave;
+		bstep = m * kWave;
+	}
+};
 
 /* Bulk kernel: the bulk pass as a kernel of its own (cfg.tune bit 8). */
 template <int MINW, int U, bool NT>
@@ -1523,34 +1488,26 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_bulk_kernel(RxArgs a)
 	const uint32_t nwaves = gridDim.x * kWavesPerBlock;
 	uint32_t cnt[CNT_FRAG + 1] = {};
 	uint64_t my_bytes = 0;
-	/* (region, batch) items, batch-major so that consecutive items are
-	 * different regions, dealt round robin: the bulk lists' batches, then
-	 * the exception kernel's deferred payload sums */
-	const uint32_t R = a.nregions;
-	const uint32_t mb = a.gmax[1], my = a.gmax[2];
-	const uint32_t items = (mb + my) * R;
-	for (uint32_t k = blockIdx.x * kWavesPerBlock + wid; k < items; k += nwaves) {
-		const uint32_t j = k / R, r = k - j * R;
-		if (j < mb) {
-			const uint32_t count = a.bcount[r], b = j * kWave;
-			if (b < count)
-				bulk_batch<U, NT, false>(
-					a, meta, part4, lane, a.blist + (uint64_t)r * a.xregion + b,
-					count - b < (uint32_t)kWave ? count - b : kWave, cnt, my_bytes);
-		} else {
-			const uint32_t count = a.ycount[r], b = (j - mb) * kWave;
-			if (b < count)
-				bulk_batch<U, NT, true>(
-					a, meta, part4, lane, a.ylist + (uint64_t)r * a.xregion + b,
-					count - b < (uint32_t)kWave ? count - b : kWave, cnt, my_bytes);
-		}
+	const RegionWalk w(a.nregions, nwaves, blockIdx.x * kWavesPerBlock + wid);
+	for (uint32_t r = w.first; r < a.nregions; r += w.rstep) {
+		const uint32_t count = a.bcount[r];
+		const uint32_t *bl = a.blist + (uint64_t)r * a.xregion;
+		for (uint32_t b = w.bfirst; b < count; b += w.bstep)
+			bulk_batch<U, NT, false>(a, meta, part4, lane, bl + b,
+						 count - b < (uint32_t)kWave ? count - b : kWave,
+						 cnt, my_bytes);
+		const uint32_t ycount = a.ycount[r];
+		const uint4 *yl = a.ylist + (uint64_t)r * a.xregion;
+		for (uint32_t b = w.bfirst; b < ycount; b += w.bstep)
+			bulk_batch<U, NT, true>(a, meta, part4, lane, yl + b,
+						ycount - b < (uint32_t)kWave ? ycount - b : kWave,
+						cnt, my_bytes);
 	}
 	block_stats_flush(a, blk_cnt, cnt, my_bytes, lane);
 }
 
 /* Exception kernel: the generic pipeline on the frames the fast kernel
- * deferred, 64 frames per batch, (region, batch) items dealt round
- * robin. */
+ * deferred, one wave per fast-kernel wave region, 64 frames per batch. */
 template <int WIN>
 __global__ __launch_bounds__(kBlock) void xdp_rx_generic_kernel(RxArgs a)
 {
@@ -1570,19 +1527,17 @@ __global__ __launch_bounds__(kBlock) void xdp_rx_generic_kernel(RxArgs a)
 	const uint32_t nwaves = gridDim.x * kWavesPerBlock;
 	uint32_t cnt[CNT_FRAG + 1] = {};
 	uint64_t my_bytes = 0;
-	/* (region, batch) items, batch-major, dealt round robin */
-	const uint32_t R = a.nregions;
-	const uint32_t items = a.gmax[0] * R;
-	for (uint32_t k = blockIdx.x * kWavesPerBlock + wid; k < items; k += nwaves) {
-		const uint32_t j = k / R, r = k - j * R;
-		const uint32_t count = a.xcount[r], b = j * kWave;
-		if (b >= count)
-			continue;
-		const bool act = b + lane < count;
-		const uint64_t i = act ? a.xlist[(uint64_t)r * a.xregion + b + lane] : 0;
-		generic_batch<WIN>(a, win, dtab, lane, i, act,
-				   a.ylist + (uint64_t)r * a.xregion, a.ycount + r, cnt,
-				   my_bytes);
+	const RegionWalk w(a.nregions, nwaves, blockIdx.x * kWavesPerBlock + wid);
+	for (uint32_t r = w.first; r < a.nregions; r += w.rstep) {
+		const uint32_t count = a.xcount[r];
+		const uint32_t *xl = a.xlist + (uint64_t)r * a.xregion;
+		for (uint32_t b = w.bfirst; b < count; b += w.bstep) {
+			const bool act = b + lane < count;
+			const uint64_t i = act ? xl[b + lane] : 0;
+			generic_batch<WIN>(a, win, dtab, lane, i, act,
+					   a.ylist + (uint64_t)r * a.xregion,
+					   a.ycount + r, cnt, my_bytes);
+		}
 	}
 
 	block_stats_flush(a, blk_cnt, cnt, my_bytes, lane);
@@ -1645,7 +1600,7 @@ uint32_t rx_grid_blocks(uint32_t n, uint32_t max_blocks)
 
 /* Kernel variants selectable by cfg.tune (diagnostic A/B): bits 0-7 =
  * waves per SIMD the fast kernel's register allocation is held to (0:
- * compiler's choice, 5, 6, 8), bit 9 = every frame through the exception
+ * compiler's choice, 6, 8), bit 9 = every frame through the exception
  * kernel (bulk pass off for it), bits 10-11 = bulk-kernel variant. */
 /* Blocks of a kernel resident at once on the device (occupancy x CUs). */
 template <auto KERN>
@@ -1669,10 +1624,9 @@ static uint32_t resident_blocks()
 }
 
 /* Launch the fast kernel on a grid of resident blocks (no partial second
- * round), then the exception and bulk kernels, each on its own resident
- * grid, over the fast kernel's wave regions.  a.xlist, a.blist and a.ylist
- * must each hold blocks * kWavesPerBlock * rx_xregion(a.n, blocks)
- * entries. */
+ * round), then the bulk and exception kernels, each on its own resident
+ * grid, over the fast kernel's wave regions.  a.xlist and a.blist must each
+ * hold blocks * kWavesPerBlock * rx_xregion(a.n, blocks) entries. */
 template <auto KERN>
 static hipError_t launch_resident(const RxArgs &a, uint32_t cap,
 				  hipStream_t stream)
@@ -1684,12 +1638,12 @@ static hipError_t launch_resident(const RxArgs &a, uint32_t cap,
 	return hipGetLastError();
 }
 
-template <int WIN, int MINW, bool TRIV = true>
+template <int WIN, int MINW>
 static hipError_t launch_sized(RxArgs a, uint32_t max_blocks,
 			       hipStream_t stream, uint32_t bulk_variant,
 			       hipEvent_t *ev)
 {
-	uint32_t cap = resident_blocks<xdp_rx_kernel<MINW, TRIV>>();
+	uint32_t cap = resident_blocks<xdp_rx_kernel<MINW>>();
 	if (cap < max_blocks)
 		max_blocks = cap;
 	const uint32_t blocks = rx_grid_blocks(a.n, max_blocks);
@@ -1697,7 +1651,7 @@ static hipError_t launch_sized(RxArgs a, uint32_t max_blocks,
 	a.nregions = blocks * kWavesPerBlock;
 	if (ev)
 		(void)hipEventRecord(ev[0], stream);
-	hipLaunchKernelGGL((xdp_rx_kernel<MINW, TRIV>), dim3(blocks),
+	hipLaunchKernelGGL((xdp_rx_kernel<MINW>), dim3(blocks),
 			   dim3(kBlock), 0, stream, a);
 	hipError_t e = hipGetLastError();
 	if (e != hipSuccess)
@@ -1746,10 +1700,6 @@ hipError_t launch_rx(const RxArgs &a, uint32_t window, uint32_t max_blocks,
 	const uint32_t bu = (tune >> 10) & 3;
 	if (window == 128)
 		return launch_sized<128, 1>(a, max_blocks, stream, bu, ev);
-	if ((tune >> 15) & 1)   /* trivial verdicts left to the exception kernel */
-		return launch_sized<64, 1, false>(a, max_blocks, stream, bu, ev);
-	if (waves == 5)
-		return launch_sized<64, 5>(a, max_blocks, stream, bu, ev);
 	if (waves == 6)
 		return launch_sized<64, 6>(a, max_blocks, stream, bu, ev);
 	if (waves == 8)

@@ -39,13 +39,10 @@ struct Slot {
 	uint8_t *d_verdict = nullptr;
 	xdpgpu_result *d_res = nullptr;
 	uint8_t *d_tup = nullptr;
-	uint32_t *d_xlist = nullptr;  /* exception list (fast -> generic kernel),
-				       * then the bulk list                     */
+	uint32_t *d_xlist = nullptr;  /* exception list (fast -> generic kernel) */
 	uint4 *d_ylist = nullptr;     /* exception payload sums (generic -> bulk) */
 	uint64_t xcap = 0;
-	uint32_t *d_xcount = nullptr; /* per-region counts of the three lists    */
-	uint32_t *d_gmax = nullptr;   /* RX list maxima: two sets of 4           */
-	uint32_t parity = 0;          /* the set the next RX launch uses         */
+	uint32_t *d_xcount = nullptr;
 	bool busy = false;
 	/* pending host copies for xdpgpu_wait() */
 	uint32_t n = 0;
@@ -135,8 +132,6 @@ static void free_slot(Slot &s)
 		(void)hipFree(s.d_xlist);
 	if (s.d_xcount)
 		(void)hipFree(s.d_xcount);
-	if (s.d_gmax)
-		(void)hipFree(s.d_gmax);
 	if (s.d_ylist)
 		(void)hipFree(s.d_ylist);
 	if (s.done)
@@ -291,8 +286,7 @@ static int ensure_slot_buffers(xdpgpu_ctx *ctx, Slot &s, uint32_t n)
 
 /* Deferred-frame list scratch for a launch of n frames (any grid up to
  * kMaxRxBlocks): two lists (exception, bulk) of per-wave regions of whole
- * tiles, xcap entries each, the deferred payload sums, their per-wave
- * counts and the two alternating sets of per-list maxima. */
+ * tiles, xcap entries each, and their per-wave counts. */
 static int ensure_xlist(xdpgpu_ctx *ctx, Slot &s, uint32_t n)
 {
 	const uint64_t need = (uint64_t)n + 64ull * 4 * kMaxRxBlocks + 64;
@@ -301,9 +295,6 @@ static int ensure_xlist(xdpgpu_ctx *ctx, Slot &s, uint32_t n)
 	if (!s.d_xcount && (hipMalloc(&s.d_xcount, cbytes) != hipSuccess ||
 			    hipMemset(s.d_xcount, 0, cbytes) != hipSuccess))
 		return set_err(ctx, -ENOMEM, "exception counts");
-	if (!s.d_gmax && (hipMalloc(&s.d_gmax, 8 * sizeof(uint32_t)) != hipSuccess ||
-			  hipMemset(s.d_gmax, 0, 8 * sizeof(uint32_t)) != hipSuccess))
-		return set_err(ctx, -ENOMEM, "list maxima");
 	if (s.xcap >= need)
 		return 0;
 	if (s.d_xlist || s.d_ylist) {
@@ -348,8 +339,6 @@ static int enqueue_rx(xdpgpu_ctx *ctx, Slot &s, uint8_t *d_umem, uint64_t usize,
 	a.bcount = s.d_xcount + kMaxRxBlocks * 4;
 	a.ylist = s.d_ylist;
 	a.ycount = s.d_xcount + kMaxRxBlocks * 4 * 2;
-	a.gmax = s.d_gmax + 4 * s.parity;
-	a.gmax_next = s.d_gmax + 4 * (s.parity ^ 1);
 	a.ydefer = !((ctx->cfg.tune >> 8) & 1);
 	a.force_generic = (ctx->cfg.tune >> 9) & 1;
 	hipEvent_t *ev = nullptr;
@@ -357,7 +346,6 @@ static int enqueue_rx(xdpgpu_ctx *ctx, Slot &s, uint8_t *d_umem, uint64_t usize,
 		ev = ctx->tev + 4 * ctx->tn++;
 	HIP_TRY(ctx, launch_rx(a, ctx->cfg.window, ctx->max_blocks, stream,
 			       ctx->cfg.tune, ev));
-	s.parity ^= 1;   /* the fast kernel zeroed the other set */
 	return 0;
 }
 

@@ -38,26 +38,19 @@ struct RxArgs {
 	uint32_t flags;
 	uint32_t initval;
 	unsigned long long *stats; /* [kMaxRxBlocks][CNT_SLOT] or null */
-	/* deferral lists: one region of xregion entries per fast-kernel wave
-	 * (nregions of them), each written in order by that wave alone */
-	uint32_t *xlist;           /* exception list (fast -> generic)      */
-	uint32_t *xcount;          /* exception frames per region           */
-	uint32_t *blist;           /* bulk list: fast-shape frames whose
-				    * payload runs past the header window  */
-	uint32_t *bcount;          /* bulk frames per region                */
+	uint32_t *xlist;           /* exception list, xregion per wave      */
+	uint32_t *xcount;          /* exception frames per wave             */
+	uint32_t *blist;           /* bulk list (payload beyond the header
+				    * window), xregion per wave            */
+	uint32_t *bcount;          /* bulk frames per wave                  */
 	uint4 *ylist;              /* exception frames whose payload sum the
-				    * bulk kernel adds: 16 B entries, one
-				    * region per fast-kernel wave region   */
+				    * bulk kernel adds: 16 B entries,
+				    * xregion per fast-kernel wave region   */
 	uint32_t *ycount;          /* entries per region (atomic)           */
-	/* the largest batch count (64 entries) of any region, per list
-	 * (x, b, y): the follow-up kernels deal (region, batch) items round
-	 * robin up to it, and exit at once when a list is empty.  Two sets
-	 * per slot, alternating: the fast kernel zeroes the next launch's */
-	uint32_t *gmax;
-	uint32_t *gmax_next;
-	uint32_t xregion;          /* set by the launcher: entries per region */
-	uint32_t nregions;         /* set by the launcher: fast-kernel waves */
 	uint32_t ydefer;           /* exception kernel may defer payload sums */
+	uint32_t xregion;          /* set by the launcher: entries per wave
+				    * region of both lists                  */
+	uint32_t nregions;         /* set by the launcher: fast-kernel waves */
 	uint32_t force_generic;    /* 1: defer every frame (diagnostic)     */
 };
 
