@@ -1,0 +1,502 @@
+// SPDX-License-Identifier: GPL-2.0
+/*
+ * rxapp.c - frame sources, the batched RX loop and the statistics of the
+ * drop-in front-ends (rxapp.h).  Everything per frame happens on the GPU
+ * behind the C ABI; this file only moves descriptors and applies verdicts,
+ * as the reference's RX loops do with the per-packet results
+ * (af_xdp_user.c:1079-1113, xdpsock.c:1462-1506 and 1718-1784).
+ */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <locale.h>
+#include <signal.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "rxapp.h"
+
+static volatile sig_atomic_t rx_done;
+
+static void on_signal(int sig)
+{
+	(void)sig;
+	rx_done = 1;
+}
+
+static uint64_t now_ns(void)
+{
+	struct timespec ts;
+
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+static uint64_t desc_off(const struct xdpgpu_desc *d)
+{
+	/* XSK_UNALIGNED_BUF_OFFSET_SHIFT, headers/linux/if_xdp.h:104-106 */
+	return (d->addr & ((1ull << 48) - 1)) + (d->addr >> 48);
+}
+
+bool rx_parse_mac(const char *s, uint8_t mac[6])
+{
+	unsigned int v[6];
+	char tail;
+
+	if (sscanf(s, "%x:%x:%x:%x:%x:%x%c", &v[0], &v[1], &v[2], &v[3], &v[4],
+		   &v[5], &tail) != 6)
+		return false;
+	for (int i = 0; i < 6; i++) {
+		if (v[i] > 0xff)
+			return false;
+		mac[i] = (uint8_t)v[i];
+	}
+	return true;
+}
+
+/* ------------------------------------------------------------------ */
+/* sources                                                             */
+
+static void *umem_alloc(uint64_t size)
+{
+	void *p = NULL;
+
+	/* page aligned (posix_memalign, af_xdp_user.c:1574), +64: the GPU
+	 * loads 16-byte chunks of a frame's last line */
+	if (posix_memalign(&p, 4096, (size + 64 + 4095) & ~4095ull))
+		return NULL;
+	memset(p, 0, (size + 64 + 4095) & ~4095ull);
+	return p;
+}
+
+int rx_source_pool(struct rx_source *src, const struct xdpgpu_pool_spec *spec,
+		   uint32_t n)
+{
+	memset(src, 0, sizeof(*src));
+	if (!n)
+		return -EINVAL;
+	uint64_t size = (xdpgpu_pool_size(spec, n) + 63) & ~63ull;
+
+	src->umem = umem_alloc(size);
+	src->descs = calloc(n, sizeof(*src->descs));
+	if (!src->umem || !src->descs) {
+		rx_source_free(src);
+		return -ENOMEM;
+	}
+	src->umem_size = size;
+	src->n = n;
+	src->headroom = spec->headroom;
+	int rc = xdpgpu_pool_generate(spec, src->umem, size, src->descs, n, NULL);
+	if (rc)
+		rx_source_free(src);
+	return rc;
+}
+
+static uint32_t rd32(const uint8_t *p, bool swap)
+{
+	uint32_t v;
+
+	memcpy(&v, p, 4);
+	return swap ? __builtin_bswap32(v) : v;
+}
+
+int rx_source_pcap(struct rx_source *src, const char *path, uint32_t chunk_size,
+		   uint32_t headroom, bool unaligned, uint32_t max_frames)
+{
+	memset(src, 0, sizeof(*src));
+	FILE *f = fopen(path, "rb");
+	if (!f)
+		return -errno;
+	uint8_t gh[24];
+	if (fread(gh, 1, 24, f) != 24) {
+		fclose(f);
+		return -EPROTO;
+	}
+	uint32_t magic;
+	memcpy(&magic, gh, 4);
+	bool swap;
+	if (magic == 0xa1b2c3d4u || magic == 0xa1b23c4du)
+		swap = false;
+	else if (magic == 0xd4c3b2a1u || magic == 0x4d3cb2a1u)
+		swap = true;
+	else {
+		fclose(f);
+		return -EPROTO;
+	}
+	if ((rd32(gh + 20, swap) & 0x0fffffff) != 1) { /* LINKTYPE_ETHERNET */
+		fclose(f);
+		return -EPROTO;
+	}
+	if (!unaligned && (chunk_size < 128 || (chunk_size & (chunk_size - 1)) ||
+			   headroom >= chunk_size)) {
+		fclose(f);
+		return -EINVAL;
+	}
+
+	/* pass 1: sizes */
+	uint64_t n = 0, size = 0;
+	long body = ftell(f);
+	uint8_t rh[16];
+	while (fread(rh, 1, 16, f) == 16) {
+		uint32_t incl = rd32(rh + 8, swap);
+		if (incl > 262144 || fseek(f, incl, SEEK_CUR)) {
+			fclose(f);
+			return -EPROTO;
+		}
+		if (max_frames && n >= max_frames)
+			break;
+		if (!unaligned && incl > chunk_size - headroom) {
+			src->skipped++;
+			continue;
+		}
+		if (incl > 65535) {
+			src->skipped++;
+			continue;
+		}
+		size += unaligned ? ((headroom + incl + 63) & ~63ull) : chunk_size;
+		n++;
+	}
+	if (!n || n > 0xffffffffull) {
+		fclose(f);
+		return n ? -E2BIG : -ENODATA;
+	}
+	uint64_t skipped = src->skipped;
+	src->umem = umem_alloc(size);
+	src->descs = calloc(n, sizeof(*src->descs));
+	if (!src->umem || !src->descs) {
+		fclose(f);
+		rx_source_free(src);
+		return -ENOMEM;
+	}
+	src->umem_size = size;
+	src->n = (uint32_t)n;
+	src->skipped = skipped;
+	src->chunk_size = unaligned ? 0 : chunk_size;
+	src->headroom = headroom;
+	src->umem_flags = unaligned ? XDPGPU_UMEM_UNALIGNED_CHUNK_FLAG : 0;
+
+	/* pass 2: frames */
+	fseek(f, body, SEEK_SET);
+	uint64_t off = 0;
+	uint32_t k = 0;
+	while (k < n && fread(rh, 1, 16, f) == 16) {
+		uint32_t incl = rd32(rh + 8, swap);
+		if ((!unaligned && incl > chunk_size - headroom) || incl > 65535) {
+			fseek(f, incl, SEEK_CUR);
+			continue;
+		}
+		if (fread(src->umem + off + headroom, 1, incl, f) != incl) {
+			fclose(f);
+			rx_source_free(src);
+			return -EPROTO;
+		}
+		src->descs[k].addr = off + headroom;
+		src->descs[k].len = incl;
+		src->descs[k].options = 0;
+		off += unaligned ? ((headroom + incl + 63) & ~63ull) : chunk_size;
+		k++;
+	}
+	fclose(f);
+	return 0;
+}
+
+int rx_source_write_pcap(const struct rx_source *src, const uint8_t *select,
+			 uint8_t want, const char *path)
+{
+	FILE *f = fopen(path, "wb");
+	if (!f)
+		return -errno;
+	const uint32_t gh[6] = { 0xa1b2c3d4u, 0x00040002u, 0, 0, 65535, 1 };
+	int rc = fwrite(gh, 4, 6, f) == 6 ? 0 : -EIO;
+	for (uint32_t i = 0; i < src->n && !rc; i++) {
+		if (select && select[i] != want)
+			continue;
+		const uint32_t rh[4] = { i, 0, src->descs[i].len, src->descs[i].len };
+		if (fwrite(rh, 4, 4, f) != 4 ||
+		    fwrite(src->umem + desc_off(&src->descs[i]), 1, src->descs[i].len, f) !=
+			    src->descs[i].len)
+			rc = -EIO;
+	}
+	if (fclose(f) && !rc)
+		rc = -EIO;
+	return rc;
+}
+
+void rx_source_free(struct rx_source *src)
+{
+	free(src->umem);
+	free(src->descs);
+	src->umem = NULL;
+	src->descs = NULL;
+	src->n = 0;
+}
+
+void rx_source_describe(const struct rx_source *src, const char *what)
+{
+	uint64_t bytes = 0;
+	uint32_t lo = UINT32_MAX, hi = 0;
+
+	for (uint32_t i = 0; i < src->n; i++) {
+		uint32_t l = src->descs[i].len;
+		bytes += l;
+		lo = l < lo ? l : lo;
+		hi = l > hi ? l : hi;
+	}
+	printf("%s: %u frames, %llu bytes (len %u..%u), UMEM %llu bytes, "
+	       "chunk %u, headroom %u%s",
+	       what, src->n, (unsigned long long)bytes, src->n ? lo : 0, hi,
+	       (unsigned long long)src->umem_size, src->chunk_size, src->headroom,
+	       src->umem_flags & XDPGPU_UMEM_UNALIGNED_CHUNK_FLAG ? ", unaligned" : "");
+	if (src->skipped)
+		printf(", %llu records skipped (larger than a chunk)",
+		       (unsigned long long)src->skipped);
+	printf("\n");
+}
+
+/* ------------------------------------------------------------------ */
+/* statistics                                                          */
+
+struct rx_stats_state {
+	uint64_t t_prev;
+	uint64_t rx_prev, tx_prev, rxb_prev, txb_prev;
+};
+
+static void print_stats(const struct rx_opts *o, const struct rx_totals *t,
+			struct rx_stats_state *st, const char *label, uint64_t now)
+{
+	const double dt = (double)(now - st->t_prev) / 1e9;
+	const double period = dt > 0 ? dt : 1;
+
+	if (o->stats_fmt == RX_STATS_XDPSOCK) {
+		/* dump_stats, xdpsock.c:478-582 */
+		const char *fmt = "%-18s %'-14.0f %'-14lu\n";
+		printf("\n sock0@%s\n", label);
+		printf("%-18s %-14s %-14s %-14.2f\n", "", "pps", "pkts", dt);
+		printf(fmt, "rx", (double)(t->rx_pkts - st->rx_prev) / period,
+		       (unsigned long)t->rx_pkts);
+		printf(fmt, "tx", (double)(t->tx_pkts - st->tx_prev) / period,
+		       (unsigned long)t->tx_pkts);
+		if (o->cfg_flags & XDPGPU_CFG_STATS) {
+			/* extra: the GPU verdict histogram (enum xdp_action) */
+			printf(fmt, "gpu aborted", 0.0, (unsigned long)t->verdict[XDPGPU_ABORTED]);
+			printf(fmt, "gpu drop", 0.0, (unsigned long)t->verdict[XDPGPU_DROP]);
+			printf(fmt, "gpu pass", 0.0, (unsigned long)t->verdict[XDPGPU_PASS]);
+			printf(fmt, "gpu tx", 0.0, (unsigned long)t->verdict[XDPGPU_TX]);
+			printf(fmt, "gpu redirect", 0.0,
+			       (unsigned long)t->verdict[XDPGPU_REDIRECT]);
+		}
+	} else {
+		/* stats_print, af_xdp_user.c:1360-1397 */
+		const char *fmt = "%-12s %'11lld pkts (%'10.0f pps) %'11lld Kbytes "
+				  "(%'6.0f Mbits/s) period:%f\n";
+		printf(fmt, "AF_XDP RX:", (long long)t->rx_pkts,
+		       (double)(t->rx_pkts - st->rx_prev) / period,
+		       (long long)(t->rx_bytes / 1000),
+		       (double)(t->rx_bytes - st->rxb_prev) * 8 / period / 1e6, period);
+		printf(fmt, "       TX:", (long long)t->tx_pkts,
+		       (double)(t->tx_pkts - st->tx_prev) / period,
+		       (long long)(t->tx_bytes / 1000),
+		       (double)(t->tx_bytes - st->txb_prev) * 8 / period / 1e6, period);
+		printf("\n");
+	}
+	fflush(stdout);
+	st->t_prev = now;
+	st->rx_prev = t->rx_pkts;
+	st->tx_prev = t->tx_pkts;
+	st->rxb_prev = t->rx_bytes;
+	st->txb_prev = t->tx_bytes;
+}
+
+/* ------------------------------------------------------------------ */
+/* the RX loop                                                          */
+
+struct rx_slot {
+	struct xdpgpu_desc *d;
+	uint8_t *v;
+	uint32_t n;
+	uint64_t first;     /* ring position of d[0] */
+	bool busy;
+};
+
+/* swap_mac_addresses, xdpsock.c:1700-1716 */
+static void swap_macs(uint8_t *p)
+{
+	uint8_t t[6];
+
+	memcpy(t, p, 6);
+	memcpy(p, p + 6, 6);
+	memcpy(p + 6, t, 6);
+}
+
+static void apply(const struct rx_source *src, const struct rx_opts *o,
+		  const struct rx_slot *s, struct rx_totals *t, uint8_t *first_pass)
+{
+	for (uint32_t i = 0; i < s->n; i++) {
+		const uint8_t v = s->v[i];
+		const uint32_t len = s->d[i].len;
+		t->rx_pkts++;
+		t->rx_bytes += len;
+		if (v < XDPGPU_NUM_VERDICTS)
+			t->verdict[v]++;
+		if (first_pass && s->first + i < src->n)
+			first_pass[s->first + i] = v;
+		bool tx = false;
+		if (o->mode == RX_MODE_L2FWD && v == XDPGPU_REDIRECT) {
+			swap_macs(src->umem + desc_off(&s->d[i]));
+			tx = true;
+		} else if (v == XDPGPU_TX) {
+			/* process_packet returned true: the reply goes out
+			 * (af_xdp_user.c:1023-1036) */
+			tx = o->mode != RX_MODE_DROP;
+		}
+		if (tx) {
+			t->tx_pkts++;
+			t->tx_bytes += len;
+		}
+	}
+}
+
+int rx_run(const struct rx_source *src, const struct rx_opts *o,
+	   struct rx_totals *out)
+{
+	struct xdpgpu_cfg cfg = {
+		.device = o->device,
+		.flags = o->cfg_flags,
+		.max_batch = o->batch,
+		.jhash_initval = o->initval,
+		.tuple_fmt = o->tuple_fmt,
+		.window = 64,
+	};
+	struct xdpgpu_ctx *ctx = NULL;
+	struct rx_slot slot[2];
+	uint8_t *first_pass = NULL;
+	int rc;
+
+	memset(out, 0, sizeof(*out));
+	memset(slot, 0, sizeof(slot));
+	if (!o->batch || !src->n)
+		return -EINVAL;
+	rc = xdpgpu_init(&cfg, &ctx);
+	if (rc) {
+		fprintf(stderr, "%s: xdpgpu_init: %s%s\n", o->prog, strerror(-rc),
+			rc == -ENODEV ? " (no GPU: this build has no CPU fallback)" : "");
+		return rc;
+	}
+	rc = xdpgpu_register_umem(ctx, src->umem, src->umem_size, src->chunk_size,
+				  src->headroom, src->umem_flags);
+	if (rc) {
+		fprintf(stderr, "%s: xdpgpu_register_umem: %s %s\n", o->prog,
+			strerror(-rc), xdpgpu_last_error(ctx));
+		xdpgpu_fini(ctx);
+		return rc;
+	}
+	for (int k = 0; k < 2; k++) {
+		slot[k].d = malloc((size_t)o->batch * sizeof(*slot[k].d));
+		slot[k].v = malloc(o->batch);
+		if (!slot[k].d || !slot[k].v)
+			rc = -ENOMEM;
+	}
+	if (!rc && (o->verdict_out || o->tx_pcap)) {
+		first_pass = malloc(src->n);
+		if (!first_pass)
+			rc = -ENOMEM;
+		else
+			memset(first_pass, 0xff, src->n);
+	}
+
+	rx_done = 0;
+	signal(SIGINT, on_signal);
+	signal(SIGTERM, on_signal);
+	setlocale(LC_NUMERIC, "en_US");
+
+	const uint64_t limit = o->count ? o->count :
+			       o->duration_ns ? UINT64_MAX : (uint64_t)src->n;
+	const uint64_t t0 = now_ns();
+	struct rx_stats_state st = { .t_prev = t0 };
+	uint64_t pos = 0;           /* frames peeked from the ring */
+	uint32_t k = 0;
+	const char *label = o->label ? o->label : o->prog;
+
+	while (!rc) {
+		struct rx_slot *s = &slot[k & 1];
+		/* peek the next batch (xsk_ring_cons__peek) */
+		uint64_t want = limit - pos;
+		const bool stop = rx_done || !want ||
+				  (o->duration_ns && now_ns() - t0 >= o->duration_ns);
+		if (!stop) {
+			s->n = (uint32_t)(want < o->batch ? want : o->batch);
+			s->first = pos;
+			for (uint32_t i = 0; i < s->n; i++)
+				s->d[i] = src->descs[(pos + i) % src->n];
+			rc = xdpgpu_submit(ctx, k & 1, s->d, s->n, s->v, NULL, NULL);
+			if (rc)
+				break;
+			s->busy = true;
+			pos += s->n;
+		}
+		/* the previous batch: wait, apply its verdicts, release */
+		struct rx_slot *p = &slot[(k + 1) & 1];
+		if (p->busy) {
+			rc = xdpgpu_wait(ctx, (k + 1) & 1);
+			if (rc)
+				break;
+			p->busy = false;
+			apply(src, o, p, out, first_pass);
+			out->batches++;
+		}
+		if (stop)
+			break;
+		k++;
+		if (o->interval_s && !o->quiet) {
+			const uint64_t t = now_ns();
+			if (t - st.t_prev >= (uint64_t)o->interval_s * 1000000000ull)
+				print_stats(o, out, &st, label, t);
+		}
+	}
+	for (int j = 0; j < 2 && rc; j++)
+		if (slot[j].busy)
+			(void)xdpgpu_wait(ctx, j);
+	const uint64_t t1 = now_ns();
+	out->seconds = (double)(t1 - t0) / 1e9;
+	if (rc)
+		fprintf(stderr, "%s: GPU batch failed: %s %s\n", o->prog, strerror(-rc),
+			xdpgpu_last_error(ctx));
+	else if (!o->quiet)
+		print_stats(o, out, &st, label, t1);   /* xdpsock_cleanup */
+
+	if (!rc && o->verdict_out) {
+		FILE *f = fopen(o->verdict_out, "wb");
+		if (!f || fwrite(first_pass, 1, src->n, f) != src->n)
+			rc = -EIO;
+		if (f && fclose(f))
+			rc = -EIO;
+	}
+	if (!rc && o->tx_pcap)
+		rc = rx_source_write_pcap(src, first_pass,
+					  o->mode == RX_MODE_L2FWD ? XDPGPU_REDIRECT : XDPGPU_TX,
+					  o->tx_pcap);
+	if (!rc && o->json) {
+		const double mpps = out->seconds > 0 ? out->rx_pkts / out->seconds / 1e6 : 0;
+		printf("{\"prog\": \"%s\", \"frames\": %llu, \"seconds\": %.6f, \"mpps\": %.3f, "
+		       "\"rx_pkts\": %llu, \"rx_bytes\": %llu, \"tx_pkts\": %llu, "
+		       "\"tx_bytes\": %llu, \"batch\": %u, \"batches\": %llu, "
+		       "\"verdict\": {\"ABORTED\": %llu, \"DROP\": %llu, \"PASS\": %llu, "
+		       "\"TX\": %llu, \"REDIRECT\": %llu}}\n",
+		       o->prog, (unsigned long long)out->rx_pkts, out->seconds, mpps,
+		       (unsigned long long)out->rx_pkts, (unsigned long long)out->rx_bytes,
+		       (unsigned long long)out->tx_pkts, (unsigned long long)out->tx_bytes,
+		       o->batch, (unsigned long long)out->batches,
+		       (unsigned long long)out->verdict[0], (unsigned long long)out->verdict[1],
+		       (unsigned long long)out->verdict[2], (unsigned long long)out->verdict[3],
+		       (unsigned long long)out->verdict[4]);
+		fflush(stdout);
+	}
+	for (int j = 0; j < 2; j++) {
+		free(slot[j].d);
+		free(slot[j].v);
+	}
+	free(first_pass);
+	xdpgpu_fini(ctx);
+	return rc;
+}

@@ -1,0 +1,103 @@
+/* SPDX-License-Identifier: GPL-2.0 */
+/*
+ * rxapp.h - shared host side of the drop-in front-ends xdpsock-gpu and
+ * af_xdp_user-gpu: frame sources that fill a UMEM (synthetic pools, pcap
+ * files), the batched RX loop over the C ABI (include/xdpgpu.h) and the
+ * reference programs' statistics output.
+ *
+ * The RX ring of the reference (xsk_ring_cons__peek / __release,
+ * AF_XDP-interaction/af_xdp_user.c:1079-1113, AF_XDP-example/xdpsock.c:
+ * 1462-1506) is modelled by replaying the source's descriptor array: each
+ * batch "peeks" the next -b descriptors, hands them to the GPU with
+ * xdpgpu_submit on one of two slots and applies the verdicts of the batch
+ * before it (double buffering).  Plain C.
+ */
+#ifndef RXAPP_H
+#define RXAPP_H
+
+#include <stdbool.h>
+#include <stdint.h>
+
+#include "xdpgpu.h"
+
+/* A UMEM and the descriptors of the frames in it. */
+struct rx_source {
+	uint8_t *umem;
+	uint64_t umem_size;
+	struct xdpgpu_desc *descs;
+	uint32_t n;
+	uint32_t chunk_size;     /* registration: 0 for a packed pool      */
+	uint32_t headroom;
+	uint32_t umem_flags;     /* XDPGPU_UMEM_UNALIGNED_CHUNK_FLAG       */
+	uint64_t skipped;        /* pcap records that did not fit a chunk */
+};
+
+/* Synthetic pool (xdpgpu_pool_generate) of n frames.  0 or -errno. */
+int rx_source_pool(struct rx_source *src, const struct xdpgpu_pool_spec *spec,
+		   uint32_t n);
+
+/* Frames of a classic pcap file (LINKTYPE_ETHERNET; either byte order,
+ * micro- or nanosecond timestamps), at most max_frames (0: all).  Aligned
+ * mode: one chunk of chunk_size bytes per frame, the frame at headroom
+ * (xdpsock's UMEM geometry, xdpsock.c:2062); unaligned: packed at 64-byte
+ * rounded strides.  0 or -errno (-EPROTO: not a usable pcap). */
+int rx_source_pcap(struct rx_source *src, const char *path, uint32_t chunk_size,
+		   uint32_t headroom, bool unaligned, uint32_t max_frames);
+
+void rx_source_free(struct rx_source *src);
+
+/* Write the frames of a source as a classic pcap file (LINKTYPE_ETHERNET,
+ * microseconds), e.g. the echo replies an af_xdp_user-gpu run sent. */
+int rx_source_write_pcap(const struct rx_source *src, const uint8_t *select,
+			 uint8_t want, const char *path);
+
+/* What the application does with the frames the GPU delivers. */
+enum rx_mode {
+	RX_MODE_DROP = 0,   /* xdpsock rx_drop: count and recycle           */
+	RX_MODE_L2FWD = 1,  /* xdpsock l2fwd: MAC swap, back out (TX count)   */
+	RX_MODE_ECHO = 2,   /* af_xdp_user process_packet: ICMPv6 echo -> TX  */
+};
+
+enum rx_stats_fmt {
+	RX_STATS_XDPSOCK = 0,   /* dump_stats, xdpsock.c:478-582        */
+	RX_STATS_AFXDP = 1,     /* stats_print, af_xdp_user.c:1360-1397 */
+};
+
+struct rx_opts {
+	int device;
+	uint32_t cfg_flags;      /* XDPGPU_CFG_*                              */
+	uint32_t tuple_fmt;
+	uint32_t initval;
+	uint32_t batch;          /* descriptors per GPU batch (-b)            */
+	uint64_t count;          /* frames to receive, 0: by duration         */
+	uint64_t duration_ns;    /* 0 with count 0: one pass over the source  */
+	uint32_t interval_s;     /* stats period, 0: none                     */
+	enum rx_mode mode;
+	enum rx_stats_fmt stats_fmt;
+	bool quiet;
+	bool json;               /* final JSON summary line on stdout         */
+	const char *verdict_out; /* per-frame verdicts of the first pass      */
+	const char *tx_pcap;     /* frames sent on TX in the first pass       */
+	const char *prog;        /* program name for messages                 */
+	const char *label;       /* socket label of the stats ("if:q bench")  */
+};
+
+struct rx_totals {
+	uint64_t rx_pkts, rx_bytes, tx_pkts, tx_bytes;
+	uint64_t verdict[XDPGPU_NUM_VERDICTS];
+	uint64_t batches;
+	double seconds;
+};
+
+/* The RX loop: runs until opts.count frames, opts.duration_ns, one pass,
+ * or SIGINT / SIGTERM, printing statistics.  0 or -errno (the ABI's). */
+int rx_run(const struct rx_source *src, const struct rx_opts *opts,
+	   struct rx_totals *out);
+
+/* Parse "aa:bb:cc:dd:ee:ff". */
+bool rx_parse_mac(const char *s, uint8_t mac[6]);
+
+/* Print the frames of a source (count, bytes, sizes) without a GPU. */
+void rx_source_describe(const struct rx_source *src, const char *what);
+
+#endif /* RXAPP_H */

@@ -1,0 +1,259 @@
+# SPDX-License-Identifier: GPL-2.0
+"""The drop-in front-ends xdpsock-gpu and af_xdp_user-gpu
+(bpf-examples_amd/apps): the reference CLIs (AF_XDP-example/xdpsock.c:
+1084-1377, AF_XDP-interaction/af_xdp_user.c:225-309 with
+common_params.c:103-284) over the C ABI.
+
+CPU: option handling and exit codes, the UMEM sources (synthetic pools,
+pcap files in both byte orders and timestamp resolutions) described
+without a GPU, and the loud failure without one.  GPU: every frame's
+verdict of a run, the verdict histogram, the l2fwd MAC swap and the
+af_xdp_user echo replies, against the oracle on the same UMEM layout.
+"""
+import json
+import os
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+import xdpgpu
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+APPS = os.path.join(ROOT, "bpf-examples_amd", "apps")
+XDPSOCK = os.path.join(APPS, "xdpsock-gpu")
+AFXDP = os.path.join(APPS, "af_xdp_user-gpu")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def built():
+    if not (os.path.exists(XDPSOCK) and os.path.exists(AFXDP)):
+        subprocess.run(["make", "-s", "-C", APPS], check=True)
+
+
+def run(*args, timeout=120):
+    return subprocess.run(list(args), capture_output=True, text=True, timeout=timeout)
+
+
+def write_pcap(path, frames, big_endian=False, nsec=False):
+    e = ">" if big_endian else "<"
+    magic = 0xa1b23c4d if nsec else 0xa1b2c3d4
+    with open(path, "wb") as f:
+        f.write(struct.pack(e + "IHHiIII", magic, 2, 4, 0, 0, 65535, 1))
+        for k, fr in enumerate(frames):
+            f.write(struct.pack(e + "IIII", k, 0, len(fr), len(fr)))
+            f.write(fr)
+
+
+def golden_frames(golden, limit=4096):
+    """The golden fixture frames that fit a default 4096-byte chunk."""
+    fx, _ = golden
+    descs = fx["descs"].view(xdpgpu.DESC_DTYPE)
+    u = fx["umem"]
+    out = []
+    for d in descs:
+        off = (int(d["addr"]) & ((1 << 48) - 1)) + (int(d["addr"]) >> 48)
+        ln = int(d["len"])
+        if off + ln <= len(u) and ln <= limit:
+            out.append(u[off:off + ln].tobytes())
+    return out
+
+
+def chunked(frames, chunk=4096):
+    """The UMEM the front-ends build from a pcap: one chunk per frame."""
+    umem = np.zeros(len(frames) * chunk + 64, np.uint8)
+    descs = np.zeros(len(frames), xdpgpu.DESC_DTYPE)
+    for k, fr in enumerate(frames):
+        umem[k * chunk:k * chunk + len(fr)] = np.frombuffer(fr, np.uint8)
+        descs[k] = (k * chunk, len(fr), 0)
+    return umem, descs
+
+
+# ------------------------------------------------------------------ CPU tests
+def test_option_errors():
+    assert run(XDPSOCK).returncode == 2                         # no source
+    assert run(XDPSOCK, "-t", "--pool", "8").returncode == 2    # txonly
+    assert run(XDPSOCK, "--pool", "8", "-s", "63").returncode == 2
+    assert run(XDPSOCK, "--pool", "8", "-s", "9729").returncode == 2
+    r = run(XDPSOCK, "--pcap", "x.pcap", "-f", "3000")
+    assert r.returncode == 2 and "not a power of two" in r.stderr
+    assert run(XDPSOCK, "--pool", "8", "--pool-kind", "nope").returncode == 2
+    assert run(XDPSOCK, "--pool", "8", "--pcap", "x").returncode == 2
+    assert run(XDPSOCK, "--pool", "8", "-G", "zz:00:00:00:00:00").returncode == 2
+    assert run(AFXDP, "--bogus").returncode == 2
+    assert run(AFXDP).returncode == 2
+    r = run(AFXDP, "-h")
+    assert r.returncode == 2 and "--batch-pkts" in r.stdout and "--dev" in r.stdout
+    assert run(AFXDP, "--pool", "8", "--src-ip", "1.2.3").returncode == 2
+
+
+@pytest.mark.parametrize("kind,size,flags", [
+    ("xdpsock", 64, []), ("xdpsock", 1500, ["-V", "-J", "7"]), ("udp4", 64, []),
+    ("imix", 64, [])])
+def test_dry_run_pool(kind, size, flags):
+    r = run(XDPSOCK, "--pool", "5000", "--pool-kind", kind, "-s", str(size), "--dry-run",
+            *flags)
+    assert r.returncode == 0, r.stderr
+    kinds = {"xdpsock": xdpgpu.POOL_XDPSOCK, "udp4": xdpgpu.POOL_UDP4,
+             "imix": xdpgpu.POOL_IMIX}
+    over = {"vlan": 1, "vlan_id": 7} if flags else {}
+    _, d, _ = xdpgpu.pool_generate(5000, kinds[kind], size, 0x5EED0002, **over)
+    assert f"5000 frames, {int(d['len'].astype(np.int64).sum())} bytes" in r.stdout
+
+
+@pytest.mark.parametrize("big_endian,nsec", [(False, False), (True, False), (False, True)])
+def test_pcap_source(tmp_path, golden, big_endian, nsec):
+    frames = golden_frames(golden)
+    p = str(tmp_path / "g.pcap")
+    write_pcap(p, frames, big_endian, nsec)
+    r = run(XDPSOCK, "--pcap", p, "--dry-run")
+    assert r.returncode == 0, r.stderr
+    total = sum(len(f) for f in frames)
+    assert f"{len(frames)} frames, {total} bytes" in r.stdout
+    assert f"UMEM {len(frames) * 4096} bytes, chunk 4096" in r.stdout
+    # frames longer than a chunk are skipped and counted
+    r = run(XDPSOCK, "--pcap", p, "-f", "128", "--dry-run")
+    big = sum(1 for f in frames if len(f) > 128)
+    assert f"{len(frames) - big} frames" in r.stdout
+    if big:
+        assert f"{big} records skipped" in r.stdout
+    # unaligned: packed at 64-byte strides
+    r = run(XDPSOCK, "--pcap", p, "-u", "--dry-run")
+    packed = sum((len(f) + 63) & ~63 for f in frames)
+    assert f"UMEM {packed} bytes, chunk 0" in r.stdout and "unaligned" in r.stdout
+
+
+def test_pcap_rejects(tmp_path):
+    p = tmp_path / "bad.pcap"
+    p.write_bytes(b"\x00" * 40)
+    assert run(XDPSOCK, "--pcap", str(p), "--dry-run").returncode == 1
+    with open(p, "wb") as f:   # LINKTYPE_RAW
+        f.write(struct.pack("<IHHiIII", 0xa1b2c3d4, 2, 4, 0, 0, 65535, 101))
+    assert run(XDPSOCK, "--pcap", str(p), "--dry-run").returncode == 1
+
+
+def test_no_gpu_fails_loudly():
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("a GPU is present")
+    except ImportError:
+        pass
+    r = run(XDPSOCK, "--pool", "100")
+    assert r.returncode == 1 and "no CPU fallback" in r.stderr
+
+
+# ------------------------------------------------------------------ GPU tests
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,size,batch", [("udp4", 64, 65536), ("imix", 64, 4096),
+                                             ("udp4", 1500, 1000)])
+def test_xdpsock_verdicts(tmp_path, kind, size, batch):
+    """Every frame's verdict of an rxdrop run equals the oracle's, and the
+    histogram and counters add up."""
+    n = 300000 if size == 64 else 20000
+    vf = str(tmp_path / "v.bin")
+    r = run(XDPSOCK, "--pool", str(n), "--pool-kind", kind, "-s", str(size), "-b", str(batch),
+            "--json", "-x", "--verdicts", vf, "-Q", timeout=300)
+    assert r.returncode == 0, r.stderr
+    js = json.loads(r.stdout.strip().splitlines()[-1])
+    kinds = {"udp4": xdpgpu.POOL_UDP4, "imix": xdpgpu.POOL_IMIX}
+    umem, descs, _ = xdpgpu.pool_generate(n, kinds[kind], size, 0x5EED0002)
+    ov, _, _, _ = oracle.process(umem, descs, 0x5, 0, 0)
+    got = np.fromfile(vf, np.uint8)
+    np.testing.assert_array_equal(got, ov)
+    hist = np.bincount(ov, minlength=5)
+    assert [js["verdict"][k] for k in ("ABORTED", "DROP", "PASS", "TX", "REDIRECT")] == \
+        hist.tolist()
+    assert js["rx_pkts"] == n and js["tx_pkts"] == 0
+    assert js["rx_bytes"] == int(descs["len"].astype(np.int64).sum())
+    assert js["batches"] == (n + batch - 1) // batch
+
+
+@pytest.mark.gpu
+def test_xdpsock_count_replays():
+    """-C larger than the pool replays the ring; the histogram scales."""
+    r = run(XDPSOCK, "--pool", "10000", "--pool-kind", "udp4", "-b", "3000", "-C", "25000",
+            "--json", "-Q")
+    assert r.returncode == 0, r.stderr
+    js = json.loads(r.stdout.strip().splitlines()[-1])
+    umem, descs, _ = xdpgpu.pool_generate(10000, xdpgpu.POOL_UDP4, 64, 0x5EED0002)
+    ov, _, _, _ = oracle.process(umem, descs, 0x5, 0, 0)
+    idx = np.arange(25000) % 10000
+    hist = np.bincount(ov[idx], minlength=5)
+    assert [js["verdict"][k] for k in ("ABORTED", "DROP", "PASS", "TX", "REDIRECT")] == \
+        hist.tolist()
+    assert js["rx_pkts"] == 25000
+
+
+@pytest.mark.gpu
+def test_xdpsock_l2fwd_pcap(tmp_path, golden):
+    """l2fwd: delivered frames go back out with their MACs swapped
+    (swap_mac_addresses, xdpsock.c:1700-1716)."""
+    frames = golden_frames(golden)
+    p, out = str(tmp_path / "in.pcap"), str(tmp_path / "out.pcap")
+    write_pcap(p, frames)
+    vf = str(tmp_path / "v.bin")
+    r = run(XDPSOCK, "-l", "--pcap", p, "--verdicts", vf, "--tx-pcap", out, "--json", "-Q")
+    assert r.returncode == 0, r.stderr
+    umem, descs = chunked(frames)
+    ov, _, _, _ = oracle.process(umem, descs, 0x5, 0, 0)
+    np.testing.assert_array_equal(np.fromfile(vf, np.uint8), ov)
+    js = json.loads(r.stdout.strip().splitlines()[-1])
+    assert js["tx_pkts"] == int((ov == xdpgpu.REDIRECT).sum())
+    sent = read_pcap(out)
+    want = [f[6:12] + f[0:6] + f[12:] for f, v in zip(frames, ov) if v == xdpgpu.REDIRECT]
+    assert sent == want
+
+
+@pytest.mark.gpu
+def test_af_xdp_user_echo_pcap(tmp_path, golden):
+    """process_packet (af_xdp_user.c:968-1040): ICMPv6 echo requests come
+    back rewritten into replies, byte for byte as the oracle rewrites them;
+    no checksum verification unless --verify."""
+    frames = golden_frames(golden)
+    p, out = str(tmp_path / "in.pcap"), str(tmp_path / "out.pcap")
+    write_pcap(p, frames)
+    for verify, flags in ((False, 0x6), (True, 0x7)):
+        vf = str(tmp_path / "v.bin")
+        args = [AFXDP, "--pcap", p, "--verdicts", vf, "--tx-pcap", out, "--json", "-q"]
+        if verify:
+            args.append("--verify")
+        r = run(*args)
+        assert r.returncode == 0, r.stderr
+        umem, descs = chunked(frames)
+        ov, _, _, _ = oracle.process(umem, descs, flags, 0, 0)
+        np.testing.assert_array_equal(np.fromfile(vf, np.uint8), ov)
+        replies = [umem[int(d["addr"]):int(d["addr"]) + int(d["len"])].tobytes()
+                   for d, v in zip(descs, ov) if v == xdpgpu.TX]
+        assert read_pcap(out) == replies
+        js = json.loads(r.stdout.strip().splitlines()[-1])
+        assert js["tx_pkts"] == len(replies) and js["rx_pkts"] == len(frames)
+    assert len(replies) > 0
+
+
+@pytest.mark.gpu
+def test_af_xdp_user_pool_stats():
+    """An echo-heavy pool through af_xdp_user-gpu: stats_print lines and the
+    TX count of the oracle."""
+    r = run(AFXDP, "--pool", "50000", "--pool-kind", "udp4", "--echo-ppm", "200000",
+            "-b", "8192", "--json")
+    assert r.returncode == 0, r.stderr
+    assert "AF_XDP RX:" in r.stdout and "TX:" in r.stdout
+    js = json.loads(r.stdout.strip().splitlines()[-1])
+    umem, descs, _ = xdpgpu.pool_generate(50000, xdpgpu.POOL_UDP4, 64, 0x5EED0003,
+                                          ppm_echo6=200000)
+    ov, _, _, _ = oracle.process(umem, descs, 0x6, 0, 0)
+    assert js["tx_pkts"] == int((ov == xdpgpu.TX).sum()) > 0
+
+
+def read_pcap(path):
+    data = open(path, "rb").read()
+    assert struct.unpack("<I", data[:4])[0] == 0xa1b2c3d4
+    out, off = [], 24
+    while off < len(data):
+        _, _, incl, _ = struct.unpack("<IIII", data[off:off + 16])
+        out.append(data[off + 16:off + 16 + incl])
+        off += 16 + incl
+    return out
