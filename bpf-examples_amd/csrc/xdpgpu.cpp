@@ -209,6 +209,10 @@ int xdpgpu_init(const xdpgpu_cfg *cfg, xdpgpu_ctx **out)
 			    hipMemset(s.d_stats, 0, stat_bytes) != hipSuccess)
 				rc = set_err(ctx, -ENOMEM, "slot %u allocation failed", i);
 		}
+		/* the counter memsets ran on the null stream, which does not
+		 * order against the slots' non-blocking streams */
+		if (!rc && hipDeviceSynchronize() != hipSuccess)
+			rc = set_err(ctx, -EIO, "hipDeviceSynchronize failed");
 		if (!rc && (cfg->flags & XDPGPU_CFG_TIMING)) {
 			ctx->tev = new (std::nothrow) hipEvent_t[4 * XDPGPU_TIMING_MAX]();
 			if (!ctx->tev) {
@@ -293,7 +297,8 @@ static int ensure_xlist(xdpgpu_ctx *ctx, Slot &s, uint32_t n)
 	/* per-wave exception, bulk and deferred-payload counts */
 	const size_t cbytes = (size_t)kMaxRxBlocks * 4 * 3 * sizeof(uint32_t);
 	if (!s.d_xcount && (hipMalloc(&s.d_xcount, cbytes) != hipSuccess ||
-			    hipMemset(s.d_xcount, 0, cbytes) != hipSuccess))
+			    hipMemset(s.d_xcount, 0, cbytes) != hipSuccess ||
+			    hipDeviceSynchronize() != hipSuccess))
 		return set_err(ctx, -ENOMEM, "exception counts");
 	if (s.xcap >= need)
 		return 0;
@@ -688,6 +693,7 @@ int xdpgpu_stats_reset(xdpgpu_ctx *ctx)
 	for (uint32_t i = 0; i < kSlots; i++)
 		HIP_TRY(ctx, hipMemset(ctx->slot[i].d_stats, 0,
 				       (size_t)kMaxRxBlocks * CNT_SLOT * 8));
+	HIP_TRY(ctx, hipDeviceSynchronize());
 	return 0;
 }
 

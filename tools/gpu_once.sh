@@ -1,9 +1,12 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_apps.py -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/pytest.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -12 gpurun_out/pytest.log
+timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread > gpurun_out/pytest.log 2>&1; rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|^FAILED" gpurun_out/pytest.log | head -8
 [ $rc -eq 0 ] || exit $rc
-for b in 65536 1048576; do
-timeout -k 10 120 bpf-examples_amd/apps/xdpsock-gpu --pool 16777216 --pool-kind udp4 -b $b -C 67108864 --json -Q > gpurun_out/cli.log 2>&1; rc=$?; echo "cli b=$b rc=$rc"; tail -1 gpurun_out/cli.log
-[ $rc -eq 0 ] || exit $rc
+OLD=build/ab_01e11cb/libxdpgpu.so
+for lib in $OLD bpf-examples_amd/csrc/libxdpgpu.so build/ab_norfl/libxdpgpu.so $OLD bpf-examples_amd/csrc/libxdpgpu.so build/ab_norfl/libxdpgpu.so; do
+  echo "== $lib"
+  XDPGPU_LIB=$lib timeout -k 10 300 python3 tools/tune_rx.py --variants 64:0 --rounds 5 > gpurun_out/t64.log 2>&1 || exit 3; grep -v amdgpu.ids gpurun_out/t64.log | cut -c1-60,120-300
+  XDPGPU_LIB=$lib timeout -k 10 300 python3 tools/tune_rx.py --variants 64:0 --rounds 5 --frames 2097152 --size 1500 > gpurun_out/t1500.log 2>&1 || exit 3; grep -v amdgpu.ids gpurun_out/t1500.log | cut -c1-60,120-300
+  XDPGPU_LIB=$lib timeout -k 10 300 python3 tools/tune_rx.py --variants 64:0 --rounds 3 --kind 1 --seed 0x5EED0003 > gpurun_out/timix.log 2>&1 || exit 3; grep -v amdgpu.ids gpurun_out/timix.log | cut -c1-60,120-300
 done
