@@ -718,8 +718,9 @@ __global__ __launch_bounds__(kBlockN) void xdp_nat64_kernel(Nat64Args a)
 }
 
 /* ------------------------------------------------------------------ */
-/* Fast kernel: IPv6 -> IPv4 of untagged, 16-byte aligned frames with no
- * extension header under a /96 prefix (config 4).  The 64-byte window of a
+/* Fast kernels (EG false: IPv6 -> IPv4, config 4; EG true: IPv4 -> IPv6)
+ * for untagged, 16-byte aligned frames of the common shapes under a /96
+ * prefix.  Ingress: no extension header.  The 64-byte window of a
  * tile is staged by LDS-DMA as in the RX fast kernel (conflict-free slot
  * swizzle); everything else happens in registers: field extraction at
  * fixed offsets, the static-map probe, the IPv4 header and its checksum,
@@ -740,6 +741,293 @@ __device__ __forceinline__ uint32_t bswap16n(uint32_t x)
 	return ((x & 0xff) << 8) | ((x >> 8) & 0xff);
 }
 
+/* IPv6 -> IPv4 of one lane's frame (nat64_handle_v6 order): decides the
+ * action or sends the frame to the slow list; a translated frame's new
+ * bytes [0, 64) go to its swizzled LDS slots */
+__device__ __forceinline__ void ingress_tile(const Nat64Args &a, const Tables &T,
+					     const uint32_t (&F)[16], uint64_t eff,
+					     uint32_t len, bool valid, bool staged,
+					     uint4 *obuf, uint64_t *otab, int lane,
+					     uint32_t &act, bool &slow, bool &xlate)
+{
+	const int osw = (lane >> 2) & 3;
+	/* classification (nat64_handler, nat64_handle_v6 order) */
+	const uint32_t et = F[3] & 0xffff;
+	const bool vlan = (et == 0x0081u) | (et == 0xa888u);
+	const bool is6 = et == 0xdd86u;
+	const uint32_t nh = F[5] & 0xff;
+	const bool ext = (nh == 0) | (nh == 43) | (nh == 44) | (nh == 51) |
+			 (nh == 60) | (nh == 135);
+	const bool hdr_ok = (len >= 56) & (((F[3] >> 20) & 0xf) == 6);
+	uint32_t s[4], d[4];
+#pragma unroll
+	for (int k = 0; k < 4; k++) {
+		s[k] = (F[5 + k] >> 16) | (F[6 + k] << 16);
+		d[k] = (F[9 + k] >> 16) | (F[10 + k] << 16);
+	}
+	const bool inpref = (d[0] == a.pref_w[0]) & (d[1] == a.pref_w[1]) &
+			    (d[2] == a.pref_w[2]);
+	const uint32_t dst = __builtin_bswap32(d[3]);
+	const bool special = (dst == 0) | ((dst & 0xFF000000u) == 0x7F000000u) |
+			     ((dst & 0xF0000000u) == 0xE0000000u);
+	const bool allowed = (a.cfg.allow_plen != 0) &
+			     ((s[0] & a.allow_m[0]) == a.allow_w[0]) &
+			     ((s[1] & a.allow_m[1]) == a.allow_w[1]) &
+			     ((s[2] & a.allow_m[2]) == a.allow_w[2]) &
+			     ((s[3] & a.allow_m[3]) == a.allow_w[3]);
+	const uint32_t itype = (F[13] >> 16) & 0xff;
+	const bool icmp_ok = (itype == 128) | (itype == 129);
+
+	/* decided here: invalid (SHOT), len < 14 or not IPv6 (OK),
+	 * parse failure (OK), outside the prefix (OK), SHOT cases,
+	 * and the translatable shapes; the rest is slow */
+	slow = false;
+	act = XDPGPU_TC_ACT_OK;
+	xlate = false;
+	if (!valid) {
+		act = XDPGPU_TC_ACT_SHOT;
+	} else if (len < 14) {
+		act = XDPGPU_TC_ACT_OK;
+	} else if (!staged) {
+		slow = true;
+	} else if (vlan) {
+		slow = true;
+	} else if (!is6 || !hdr_ok) {
+		act = XDPGPU_TC_ACT_OK;           /* also len < 56 */
+	} else if (len < 64) {
+		slow = true;   /* the 16-byte stores stay inside the frame */
+	} else if (ext) {
+		slow = true;
+	} else if (!inpref) {
+		act = XDPGPU_TC_ACT_OK;
+	} else if (special || !allowed) {
+		act = XDPGPU_TC_ACT_SHOT;
+	} else if (nh == 58 && (!icmp_ok || len < 62)) {
+		slow = true;
+	} else {
+		xlate = true;
+	}
+	uint32_t v4 = 0;
+	if (xlate) {
+		bool found;
+		if (a.diag & 1) {
+			found = true;
+			v4 = 0x0A630001u;
+		} else {
+			v4 = lookup_v6(T, s, found);
+		}
+		if (!found) {
+			xlate = false;
+			act = XDPGPU_NAT64_NO_STATE;
+		} else {
+			act = XDPGPU_TC_ACT_REDIRECT;
+		}
+	}
+	/* TCP's check word (bytes 70-71) lies past the window */
+	uint32_t e68 = 0;
+	const bool tcp_upd = xlate && nh == 6 && len >= 72;
+	if (tcp_upd)
+		e68 = *reinterpret_cast<const uint32_t *>(a.umem + eff + 68);
+
+	const bool put = xlate && !(a.diag & 2);
+	otab[lane] = put ? eff : ~0ull;
+	if (put) {
+		const uint32_t h3 = __builtin_bswap32(v4);        /* src, LE word */
+		const uint32_t h4 = d[3];
+		const uint32_t tos = (((F[3] >> 16) & 0xf) << 4) | (F[3] >> 28);
+		const uint32_t tot = (bswap16n(F[4] >> 16) + 20) & 0xffff;
+		const uint32_t ttl = (F[5] >> 8) & 0xff;
+		const uint32_t p4 = nh == 58 ? 1u : nh;
+		/* IPv4 header checksum (csum_fold_helper of the header):
+		 * LE 16-bit words; frag_off is the wire bytes 0x40 0x00
+		 * (DF), the LE word 0x0040 */
+		uint32_t hs = halves2(0x45u | (tos << 8) | (bswap16n(tot) << 16)) +
+			      0x0040u + (ttl | (p4 << 8)) + halves2(h3) + halves2(h4);
+		hs = (hs & 0xffff) + (hs >> 16);
+		hs = (hs & 0xffff) + (hs >> 16);
+		const uint32_t chk4 = ~hs & 0xffff;
+		/* the pseudo header's address words, v6 and v4 */
+		uint32_t s6 = 0;
+#pragma unroll
+		for (int k = 0; k < 4; k++)
+			s6 += halves2(s[k]) + halves2(d[k]);
+		s6 = mod_ffff(s6);
+		const uint32_t s4 = mod_ffff(halves2(h3) + halves2(h4));
+		uint32_t o13 = (h4 >> 16) | (F[13] & 0xffff0000u);
+		uint32_t o14 = F[14], o15 = F[15];
+		if (nh == 17) {
+			/* update_l4_checksum, BPF_F_MARK_MANGLED_0 */
+			uint32_t c = F[15] & 0xffff;
+			if (c) {
+				c = csum_upd(c, diff_mod(s6, s4));
+				if (!c)
+					c = 0xffff;
+			}
+			o15 = (F[15] & 0xffff0000u) | c;
+		} else if (nh == 6) {
+			if (tcp_upd) {
+				const uint32_t c = csum_upd(e68 >> 16, diff_mod(s6, s4));
+				e68 = (e68 & 0xffff) | (c << 16);
+			}
+		} else if (nh == 58) {
+			/* rewrite_icmpv6, echo: pseudo header out, type word */
+			const uint32_t ph = mod_ffff(s6 + (F[4] >> 16) + (58u << 8));
+			const uint32_t code = (F[13] >> 24) & 0xff;
+			const uint32_t nt = itype == 128 ? 8u : 0u;
+			const uint32_t hb = itype | (code << 8), ha = nt | (code << 8);
+			const uint32_t delta = mod_ffff(diff_mod(ph, 0) + diff_mod(hb, ha));
+			const uint32_t c = csum_upd(F[14] & 0xffff, delta);
+			o13 = (h4 >> 16) | (ha << 16);
+			o14 = (F[14] & 0xffff0000u) | c;
+		}
+		/* frame bytes [0, 64): unchanged [0, 20) (rewritten so
+		 * that the stores are whole 64-byte sectors), the L2
+		 * header moved to 20 with h_proto 0x0800, the IPv4
+		 * header at 34, the L4 bytes at 54; staged in LDS in the
+		 * swizzled slots of the header buffer's layout */
+		obuf[4 * lane + (0 ^ osw)] = make_uint4(F[0], F[1], F[2], F[3]);
+		obuf[4 * lane + (1 ^ osw)] = make_uint4(F[4], F[0], F[1], F[2]);
+		obuf[4 * lane + (2 ^ osw)] =
+			make_uint4(0x0008u | (0x45u << 16) | (tos << 24),
+				   bswap16n(tot), 0x40u | (ttl << 16) | (p4 << 24),
+				   chk4 | (h3 << 16));
+		obuf[4 * lane + (3 ^ osw)] =
+			make_uint4((h3 >> 16) | (h4 << 16), o13, o14, o15);
+		if (tcp_upd)
+			*reinterpret_cast<uint32_t *>(a.umem + eff + 68) = e68;
+	}
+}
+
+/* IPv4 -> IPv6 of one lane's frame (nat64_handle_v4, nat64_kern.c:443-541,
+ * under a /96 prefix): untagged, ihl 5, at least 64 bytes and 32 bytes of
+ * headroom.  ICMP echo request/reply is rewritten here, other ICMP types go
+ * to the slow list.  The frame grows 20 bytes to the front: its new bytes
+ * [-20, 0) are stored by the lane (a dword and a 16-byte chunk), the new
+ * bytes [0, 64) go to its swizzled LDS slots.  Position p of the new frame
+ * layout, relative to the old frame start: [-20, -8) the MACs, [-8, -6)
+ * h_proto 0x86DD, [-6, 34) the IPv6 header, [34, ...) the L4 bytes in
+ * place (the L4 header does not move). */
+__device__ __forceinline__ void egress_tile(const Nat64Args &a, const Tables &T,
+					    const uint32_t (&F)[16], uint64_t eff,
+					    uint32_t len, bool valid, bool staged,
+					    uint4 *obuf, uint64_t *otab, int lane,
+					    uint32_t &act, bool &slow, bool &xlate)
+{
+	const int osw = (lane >> 2) & 3;
+	const uint32_t et = F[3] & 0xffff;
+	const bool vlan = (et == 0x0081u) | (et == 0xa888u);
+	const bool is4 = et == 0x0008u;
+	const uint32_t vihl = (F[3] >> 16) & 0xff;
+	const uint32_t s4 = (F[6] >> 16) | (F[7] << 16);   /* saddr, LE word */
+	const uint32_t d4 = (F[7] >> 16) | (F[8] << 16);   /* daddr */
+	const uint32_t dst = __builtin_bswap32(d4);
+	const bool inpref = (dst & a.cfg.v4_mask) == a.cfg.v4_prefix;
+	/* frag_off other than DF: the LE word of wire bytes 20-21 */
+	const bool frag = (F[5] & 0xffbfu) != 0;
+	const uint32_t proto = F[5] >> 24;
+	const uint32_t itype = (F[8] >> 16) & 0xff;
+	const bool echo = (itype == 8) | (itype == 0);
+
+	slow = false;
+	act = XDPGPU_TC_ACT_OK;
+	xlate = false;
+	if (!valid) {
+		act = XDPGPU_TC_ACT_SHOT;
+	} else if (len < 14) {
+		act = XDPGPU_TC_ACT_OK;
+	} else if (!staged || vlan) {
+		slow = true;
+	} else if (!is4) {
+		act = XDPGPU_TC_ACT_OK;
+	} else if (vihl != 0x45 || len < 64 || eff < 32) {
+		slow = true;   /* options / other versions; short; no room */
+	} else if (!inpref) {
+		act = XDPGPU_TC_ACT_OK;
+	} else if (frag) {
+		act = XDPGPU_TC_ACT_SHOT;
+	} else if (proto == 1 && !echo) {
+		slow = true;
+	} else {
+		xlate = true;
+	}
+	uint32_t w[4] = {0, 0, 0, 0};
+	if (xlate) {
+		bool found = true;
+		if (a.diag & 1) {
+			w[0] = 0x20010db8u;
+			w[3] = dst;
+		} else {
+			found = lookup_v4(T, dst, w);
+		}
+		if (found) {
+			act = XDPGPU_TC_ACT_REDIRECT;
+		} else {
+			xlate = false;
+			act = XDPGPU_TC_ACT_SHOT;
+		}
+	}
+
+	const bool put = xlate && !(a.diag & 2);
+	otab[lane] = put ? eff : ~0ull;
+	if (!put)
+		return;
+	const uint32_t tos = F[3] >> 24;
+	const uint32_t pl = (bswap16n(F[4] & 0xffff) - 20) & 0xffff;
+	const uint32_t ttl = (F[5] >> 16) & 0xff;
+	const uint32_t nh = proto == 1 ? 58u : proto;
+	/* priority and flow label as v4addr_to_v6's caller writes them */
+	const uint32_t b0 = 0x60u | ((tos & 0x70u) >> 4), b1 = (tos << 4) & 0xff;
+	/* the pseudo header's address words, v4 and v6 */
+	const uint32_t from = mod_ffff(halves2(s4) + halves2(d4));
+	uint32_t to = halves2(a.pref_w[0]) + halves2(a.pref_w[1]) +
+		      halves2(a.pref_w[2]) + halves2(s4);
+#pragma unroll
+	for (int k = 0; k < 4; k++)
+		to += halves2(w[k]);
+	to = mod_ffff(to);
+	const uint32_t delta = diff_mod(from, to);
+	uint32_t n13 = (w[3] >> 16) | (F[8] & 0xffff0000u);
+	uint32_t n14 = F[9], n15 = F[10], n17 = F[12];
+	if (proto == 17) {
+		/* update_l4_checksum, BPF_F_MARK_MANGLED_0 */
+		uint32_t c = F[10] & 0xffff;
+		if (c) {
+			c = csum_upd(c, delta);
+			if (!c)
+				c = 0xffff;
+		}
+		n15 = (F[10] & 0xffff0000u) | c;
+	} else if (proto == 6) {
+		n17 = (F[12] & 0xffff) | (csum_upd(F[12] >> 16, delta) << 16);
+	} else if (proto == 1) {
+		/* rewrite_icmp, echo: type word, pseudo header in */
+		const uint32_t ph = mod_ffff(to + bswap16n(pl) + (58u << 8));
+		const uint32_t code = F[8] >> 24;
+		const uint32_t nt = itype == 8 ? 128u : 129u;
+		const uint32_t hb = itype | (code << 8), ha = nt | (code << 8);
+		const uint32_t c = csum_upd(F[9] & 0xffff, mod_ffff(ph + diff_mod(hb, ha)));
+		n13 = (w[3] >> 16) | (ha << 16);
+		n14 = (F[9] & 0xffff0000u) | c;
+	}
+	/* new bytes [-20, 0): MACs, h_proto, version/priority/flow label,
+	 * payload_len */
+	*reinterpret_cast<uint32_t *>(a.umem + eff - 20) = F[0];
+	*reinterpret_cast<uint4 *>(a.umem + eff - 16) =
+		make_uint4(F[1], F[2], 0xDD86u | (b0 << 16) | (b1 << 24), bswap16n(pl) << 16);
+	/* new bytes [0, 64): nexthdr, hop limit, the addresses, the L4 header */
+	obuf[4 * lane + (0 ^ osw)] =
+		make_uint4(nh | (ttl << 8) | (a.pref_w[0] << 16),
+			   (a.pref_w[0] >> 16) | (a.pref_w[1] << 16),
+			   (a.pref_w[1] >> 16) | (a.pref_w[2] << 16),
+			   (a.pref_w[2] >> 16) | (s4 << 16));
+	obuf[4 * lane + (1 ^ osw)] =
+		make_uint4((s4 >> 16) | (w[0] << 16), (w[0] >> 16) | (w[1] << 16),
+			   (w[1] >> 16) | (w[2] << 16), (w[2] >> 16) | (w[3] << 16));
+	obuf[4 * lane + (2 ^ osw)] = make_uint4(n13, n14, n15, F[11]);
+	obuf[4 * lane + (3 ^ osw)] = make_uint4(n17, F[13], F[14], F[15]);
+}
+
+template <bool EG>
 __global__ __launch_bounds__(kBlockN) void xdp_nat64_fast_kernel(Nat64Args a)
 {
 	__shared__ uint4 buf_all[kWavesN * 4 * kWaveN];
@@ -755,7 +1043,6 @@ __global__ __launch_bounds__(kBlockN) void xdp_nat64_fast_kernel(Nat64Args a)
 	uint32_t *xq = xq_all + wid * 2 * kWaveN;
 	uint4 *obuf = obuf_all + wid * 4 * kWaveN;
 	uint64_t *otab = otab_all + wid * kWaveN;
-	const int osw = (lane >> 2) & 3;
 	const Tables T = {a.v6map, a.v6nb, a.v4map, a.v4nb};
 
 	const uint64_t ntiles = ((uint64_t)a.n + kWaveN - 1) / kWaveN;
@@ -824,83 +1111,14 @@ __global__ __launch_bounds__(kBlockN) void xdp_nat64_fast_kernel(Nat64Args a)
 		const bool valid = active & ((uint64_t)len <= a.usize) & (eff <= a.usize - len);
 		const bool staged = valid & dma & !(eff & 15) & (eff + 64 <= us16);
 
-		/* classification (nat64_handler, nat64_handle_v6 order) */
-		const uint32_t et = F[3] & 0xffff;
-		const bool vlan = (et == 0x0081u) | (et == 0xa888u);
-		const bool is6 = et == 0xdd86u;
-		const uint32_t nh = F[5] & 0xff;
-		const bool ext = (nh == 0) | (nh == 43) | (nh == 44) | (nh == 51) |
-				 (nh == 60) | (nh == 135);
-		const bool hdr_ok = (len >= 56) & (((F[3] >> 20) & 0xf) == 6);
-		uint32_t s[4], d[4];
-#pragma unroll
-		for (int k = 0; k < 4; k++) {
-			s[k] = (F[5 + k] >> 16) | (F[6 + k] << 16);
-			d[k] = (F[9 + k] >> 16) | (F[10 + k] << 16);
-		}
-		const bool inpref = (d[0] == a.pref_w[0]) & (d[1] == a.pref_w[1]) &
-				    (d[2] == a.pref_w[2]);
-		const uint32_t dst = __builtin_bswap32(d[3]);
-		const bool special = (dst == 0) | ((dst & 0xFF000000u) == 0x7F000000u) |
-				     ((dst & 0xF0000000u) == 0xE0000000u);
-		const bool allowed = (a.cfg.allow_plen != 0) &
-				     ((s[0] & a.allow_m[0]) == a.allow_w[0]) &
-				     ((s[1] & a.allow_m[1]) == a.allow_w[1]) &
-				     ((s[2] & a.allow_m[2]) == a.allow_w[2]) &
-				     ((s[3] & a.allow_m[3]) == a.allow_w[3]);
-		const uint32_t itype = (F[13] >> 16) & 0xff;
-		const bool icmp_ok = (itype == 128) | (itype == 129);
-
-		/* decided here: invalid (SHOT), len < 14 or not IPv6 (OK),
-		 * parse failure (OK), outside the prefix (OK), SHOT cases,
-		 * and the translatable shapes; the rest is slow */
-		bool slow = false;
-		uint32_t act = XDPGPU_TC_ACT_OK;
-		bool xlate = false;
-		if (!valid) {
-			act = XDPGPU_TC_ACT_SHOT;
-		} else if (len < 14) {
-			act = XDPGPU_TC_ACT_OK;
-		} else if (!staged) {
-			slow = true;
-		} else if (vlan) {
-			slow = true;
-		} else if (!is6 || !hdr_ok) {
-			act = XDPGPU_TC_ACT_OK;           /* also len < 56 */
-		} else if (len < 64) {
-			slow = true;   /* the 16-byte stores stay inside the frame */
-		} else if (ext) {
-			slow = true;
-		} else if (!inpref) {
-			act = XDPGPU_TC_ACT_OK;
-		} else if (special || !allowed) {
-			act = XDPGPU_TC_ACT_SHOT;
-		} else if (nh == 58 && (!icmp_ok || len < 62)) {
-			slow = true;
-		} else {
-			xlate = true;
-		}
-		uint32_t v4 = 0;
-		if (xlate) {
-			bool found;
-			if (a.diag & 1) {
-				found = true;
-				v4 = 0x0A630001u;
-			} else {
-				v4 = lookup_v6(T, s, found);
-			}
-			if (!found) {
-				xlate = false;
-				act = XDPGPU_NAT64_NO_STATE;
-			} else {
-				act = XDPGPU_TC_ACT_REDIRECT;
-			}
-		}
-		/* TCP's check word (bytes 70-71) lies past the window */
-		uint32_t e68 = 0;
-		const bool tcp_upd = xlate && nh == 6 && len >= 72;
-		if (tcp_upd)
-			e68 = *reinterpret_cast<const uint32_t *>(a.umem + eff + 68);
+		uint32_t act;
+		bool slow, xlate;
+		if constexpr (EG)
+			egress_tile(a, T, F, eff, len, valid, staged, obuf, otab, lane, act,
+				    slow, xlate);
+		else
+			ingress_tile(a, T, F, eff, len, valid, staged, obuf, otab, lane, act,
+				     slow, xlate);
 
 		/* slow frames to this wave's list */
 		{
@@ -924,73 +1142,6 @@ __global__ __launch_bounds__(kBlockN) void xdp_nat64_fast_kernel(Nat64Args a)
 			}
 		}
 
-		const bool put = xlate && !(a.diag & 2);
-		otab[lane] = put ? eff : ~0ull;
-		if (put) {
-			const uint32_t h3 = __builtin_bswap32(v4);        /* src, LE word */
-			const uint32_t h4 = d[3];
-			const uint32_t tos = (((F[3] >> 16) & 0xf) << 4) | (F[3] >> 28);
-			const uint32_t tot = (bswap16n(F[4] >> 16) + 20) & 0xffff;
-			const uint32_t ttl = (F[5] >> 8) & 0xff;
-			const uint32_t p4 = nh == 58 ? 1u : nh;
-			/* IPv4 header checksum (csum_fold_helper of the header):
-			 * LE 16-bit words; frag_off is the wire bytes 0x40 0x00
-			 * (DF), the LE word 0x0040 */
-			uint32_t hs = halves2(0x45u | (tos << 8) | (bswap16n(tot) << 16)) +
-				      0x0040u + (ttl | (p4 << 8)) + halves2(h3) + halves2(h4);
-			hs = (hs & 0xffff) + (hs >> 16);
-			hs = (hs & 0xffff) + (hs >> 16);
-			const uint32_t chk4 = ~hs & 0xffff;
-			/* the pseudo header's address words, v6 and v4 */
-			uint32_t s6 = 0;
-#pragma unroll
-			for (int k = 0; k < 4; k++)
-				s6 += halves2(s[k]) + halves2(d[k]);
-			s6 = mod_ffff(s6);
-			const uint32_t s4 = mod_ffff(halves2(h3) + halves2(h4));
-			uint32_t o13 = (h4 >> 16) | (F[13] & 0xffff0000u);
-			uint32_t o14 = F[14], o15 = F[15];
-			if (nh == 17) {
-				/* update_l4_checksum, BPF_F_MARK_MANGLED_0 */
-				uint32_t c = F[15] & 0xffff;
-				if (c) {
-					c = csum_upd(c, diff_mod(s6, s4));
-					if (!c)
-						c = 0xffff;
-				}
-				o15 = (F[15] & 0xffff0000u) | c;
-			} else if (nh == 6) {
-				if (tcp_upd) {
-					const uint32_t c = csum_upd(e68 >> 16, diff_mod(s6, s4));
-					e68 = (e68 & 0xffff) | (c << 16);
-				}
-			} else if (nh == 58) {
-				/* rewrite_icmpv6, echo: pseudo header out, type word */
-				const uint32_t ph = mod_ffff(s6 + (F[4] >> 16) + (58u << 8));
-				const uint32_t code = (F[13] >> 24) & 0xff;
-				const uint32_t nt = itype == 128 ? 8u : 0u;
-				const uint32_t hb = itype | (code << 8), ha = nt | (code << 8);
-				const uint32_t delta = mod_ffff(diff_mod(ph, 0) + diff_mod(hb, ha));
-				const uint32_t c = csum_upd(F[14] & 0xffff, delta);
-				o13 = (h4 >> 16) | (ha << 16);
-				o14 = (F[14] & 0xffff0000u) | c;
-			}
-			/* frame bytes [0, 64): unchanged [0, 20) (rewritten so
-			 * that the stores are whole 64-byte sectors), the L2
-			 * header moved to 20 with h_proto 0x0800, the IPv4
-			 * header at 34, the L4 bytes at 54; staged in LDS in the
-			 * swizzled slots of the header buffer's layout */
-			obuf[4 * lane + (0 ^ osw)] = make_uint4(F[0], F[1], F[2], F[3]);
-			obuf[4 * lane + (1 ^ osw)] = make_uint4(F[4], F[0], F[1], F[2]);
-			obuf[4 * lane + (2 ^ osw)] =
-				make_uint4(0x0008u | (0x45u << 16) | (tos << 24),
-					   bswap16n(tot), 0x40u | (ttl << 16) | (p4 << 24),
-					   chk4 | (h3 << 16));
-			obuf[4 * lane + (3 ^ osw)] =
-				make_uint4((h3 >> 16) | (h4 << 16), o13, o14, o15);
-			if (tcp_upd)
-				*reinterpret_cast<uint32_t *>(a.umem + eff + 68) = e68;
-		}
 		/* transposed stores: in store k lane l writes chunk l & 3 of
 		 * frame 16k + l / 4, so four lanes write one frame's 64 bytes
 		 * as a whole sector */
@@ -1009,10 +1160,12 @@ __global__ __launch_bounds__(kBlockN) void xdp_nat64_fast_kernel(Nat64Args a)
 			a.action[i] = (uint8_t)act;
 			uint4 od = dv;
 			if (xlate) {
-				const uint64_t na = eff + 20;
+				/* the frame starts 20 bytes later (IPv4) or
+				 * earlier (IPv6) */
+				const uint64_t na = EG ? eff - 20 : eff + 20;
 				od.x = (uint32_t)na;
 				od.y = (uint32_t)(na >> 32);
-				od.z = len - 20;
+				od.z = EG ? len + 20 : len - 20;
 			}
 			*reinterpret_cast<uint4 *>(a.out + i) = od;
 		}
@@ -1044,7 +1197,7 @@ static uint32_t resident_n()
 
 uint32_t nat64_grid(uint32_t n, uint32_t max_blocks)
 {
-	uint32_t cap = resident_n<xdp_nat64_fast_kernel>();
+	uint32_t cap = resident_n<xdp_nat64_fast_kernel<false>>();
 	if (cap > max_blocks)
 		cap = max_blocks;
 	uint64_t tiles = ((uint64_t)n + kWaveN - 1) / kWaveN;
@@ -1062,8 +1215,12 @@ hipError_t launch_nat64(const Nat64Args &a0, uint32_t max_blocks, hipStream_t st
 		a.nregions = blocks * kWavesN;
 		const uint64_t tiles = ((uint64_t)a.n + kWaveN - 1) / kWaveN;
 		a.xregion = (uint32_t)(((tiles + a.nregions - 1) / a.nregions) * kWaveN);
-		hipLaunchKernelGGL(xdp_nat64_fast_kernel, dim3(blocks), dim3(kBlockN), 0,
-				   stream, a);
+		if (a.cfg.direction == XDPGPU_NAT64_EGRESS)
+			hipLaunchKernelGGL(xdp_nat64_fast_kernel<true>, dim3(blocks),
+					   dim3(kBlockN), 0, stream, a);
+		else
+			hipLaunchKernelGGL(xdp_nat64_fast_kernel<false>, dim3(blocks),
+					   dim3(kBlockN), 0, stream, a);
 		hipError_t e = hipGetLastError();
 		if (e != hipSuccess)
 			return e;

@@ -681,8 +681,11 @@ void xdpgpu_pool_spec_default(xdpgpu_pool_spec *spec, uint32_t kind,
 		spec->ppm_ndp = 5000;
 		spec->ppm_arp = 1000;
 		spec->ppm_malformed = 5000;
+		/* the IPv6 header grows the frame 20 bytes to the front: 64
+		 * bytes of headroom, frames 64-byte aligned as at an AF_XDP
+		 * chunk's XDP_PACKET_HEADROOM */
 		if (kind == XDPGPU_POOL_NAT64_V4)
-			spec->headroom = 32;   /* the IPv6 header grows the frame */
+			spec->headroom = 64;
 	}
 	spec->vlan_id = 1;
 }

@@ -496,10 +496,10 @@ int xdpgpu_nat64_dev(xdpgpu_ctx *ctx, void *d_umem, uint64_t umem_size,
 	a.v6nb = ctx->nb;
 	a.v4map = ctx->d_v4map;
 	a.v4nb = ctx->nb;
-	/* the fast kernel covers ingress under a /96 prefix; it shares slot
-	 * 0's deferral-list scratch with the RX path (a context runs one
-	 * launch sequence at a time) */
-	a.fast = ctx->ncfg.direction == XDPGPU_NAT64_INGRESS && ctx->ncfg.v6_plen == 96;
+	/* the fast kernels cover both directions under a /96 prefix; they
+	 * share slot 0's deferral-list scratch with the RX path (a context
+	 * runs one launch sequence at a time) */
+	a.fast = ctx->ncfg.v6_plen == 96;
 	a.diag = (ctx->cfg.tune >> 12) & 3;
 	if (a.fast) {
 		int rc = ensure_xlist(ctx, ctx->slot[0], n);

@@ -367,6 +367,22 @@ def test_gpu_cases(direction, skew):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("direction", [IN, EG])
+@pytest.mark.parametrize("headroom", [64, 32, 24, 16])
+def test_gpu_cases_padded(direction, headroom):
+    """The cases padded to 96 bytes: the fast kernels' shapes (>= 64 bytes,
+    16-byte aligned, at headroom 64 and 32); headroom 24 is unaligned and 16
+    leaves an egress frame too little room, both for the slow kernel."""
+    cases = ingress_cases() if direction == IN else egress_cases()
+    frames = [c[1] + bytes(max(0, 96 - len(c[1]))) for c in cases]
+    umem, descs = place(frames, headroom=headroom)
+    want = run_oracle(umem, descs, direction)
+    assert (want[0] == REDIR).sum() > len(cases) // 2
+    got = gpu_nat64(umem, descs, direction)
+    assert_nat64_same(got, want, f"padded/{direction}/{headroom}")
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("plen", [32, 40, 48, 56, 64, 96])
 def test_gpu_prefix_lengths(plen):
     cfg, smap = xdpgpu.nat64_pool_config(IN, 16)

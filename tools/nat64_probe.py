@@ -21,10 +21,13 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--direction", type=int, default=xdpgpu.NAT64_INGRESS)
     ap.add_argument("--tune", type=lambda x: int(x, 0), default=0)
+    ap.add_argument("--headroom", type=int, default=None)
+    ap.add_argument("--stride", type=int, default=None)
     args = ap.parse_args()
     kind = xdpgpu.POOL_NAT64 if args.direction == xdpgpu.NAT64_INGRESS else xdpgpu.POOL_NAT64_V4
     cfg, smap = xdpgpu.nat64_pool_config(args.direction)
-    u, ds, ex = xdpgpu.pool_generate(args.frames, kind, args.size, 0x5EED0004)
+    kw = {k: v for k, v in (("headroom", args.headroom), ("stride", args.stride)) if v is not None}
+    u, ds, ex = xdpgpu.pool_generate(args.frames, kind, args.size, 0x5EED0004, **kw)
     dev = torch.device("cuda:0")
     pristine = torch.empty(u.nbytes + 64, dtype=torch.uint8, device=dev)
     pristine[u.nbytes:].zero_()
