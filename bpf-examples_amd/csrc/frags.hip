@@ -1,0 +1,245 @@
+// SPDX-License-Identifier: GPL-2.0
+/*
+ * frags.hip - multi-buffer packets (XDPGPU_CFG_FRAGS, include/xdpgpu.h).
+ *
+ * A packet of several descriptors (XDP_PKT_CONTD on all but the last,
+ * headers/linux/if_xdp.h:122; IS_EOP_DESC, xdpsock.c:67) cannot be read in
+ * place: its bytes are spread over UMEM chunks.  The RX fast kernel skips
+ * its descriptors, and these kernels handle it as one frame:
+ *  - frag_count: the packets' first descriptors (lane per descriptor) walk
+ *    their fragments; complete packets are counted with the bounce bytes
+ *    they need, the others (the batch ends inside them, or a fragment lies
+ *    outside the UMEM) are finished as ABORTED;
+ *  - frag_gather: each complete packet, and the byte after its last
+ *    fragment (udp_csum's over-read byte), is copied to a bounce UMEM at a
+ *    16-byte aligned offset, one wave per packet with coalesced copies, and
+ *    gets a bounce descriptor; the RX kernels then run over the bounce
+ *    batch, one frame per packet;
+ *  - frag_scatter: the packet's verdict goes to each of its descriptors,
+ *    its record and tuple to the first (all-zero ones to the others), and
+ *    an ICMPv6 echo reply's first 64 bytes back into the fragments (the
+ *    rewrite of process_packet, af_xdp_user.c:968-1040, touches bytes
+ *    0-61).
+ */
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "xdpgpu_internal.h"
+
+namespace xdpgpu {
+
+namespace {
+
+constexpr int kFragWave = 64;
+constexpr int kFragBlock = 256;
+constexpr uint64_t kFragMaxBlocks = 4096;
+
+__device__ __forceinline__ uint64_t frag_eff(const xdpgpu_desc &d)
+{
+	return (d.addr & ((1ull << 48) - 1)) + (d.addr >> 48);
+}
+
+__device__ __forceinline__ uint32_t rl32(uint32_t v, int l)
+{
+	return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int l)
+{
+	return ((uint64_t)rl32((uint32_t)(v >> 32), l) << 32) | rl32((uint32_t)v, l);
+}
+
+/* the first descriptor of a packet of several */
+__device__ __forceinline__ bool packet_head(const FragArgs &a, uint32_t i)
+{
+	return (a.desc[i].options & XDPGPU_PKT_CONTD) &&
+	       !(i && (a.desc[i - 1].options & XDPGPU_PKT_CONTD));
+}
+
+/* The packet whose first descriptor is i: its last descriptor and bytes.
+ * False when the batch ends inside it, a fragment lies outside the UMEM or
+ * the packet does not fit a descriptor's length field. */
+__device__ bool packet_walk(const FragArgs &a, uint32_t i, uint32_t &last,
+			    uint64_t &total)
+{
+	bool ok = true;
+	total = 0;
+	for (uint32_t j = i;; j++) {
+		const xdpgpu_desc d = a.desc[j];
+		const uint64_t eff = frag_eff(d);
+		ok = ok && (uint64_t)d.len <= a.usize && eff <= a.usize - d.len;
+		total += d.len;
+		last = j;
+		if (!(d.options & XDPGPU_PKT_CONTD))
+			return ok && total <= 0xffffffffull;
+		if (j + 1 == a.n)
+			return false;
+	}
+}
+
+/* bounce bytes of a packet: its bytes and the over-read byte, rounded up
+ * to 16 */
+__device__ __forceinline__ uint64_t bounce_size(uint64_t total)
+{
+	return (total + 16) & ~15ull;
+}
+
+/* the all-zero record and tuple of descriptor k */
+__device__ void zero_outputs(const FragArgs &a, uint32_t k)
+{
+	if (a.res)
+		*reinterpret_cast<uint4 *>(a.res + k) = make_uint4(0, 0, 0, 0);
+	for (uint32_t b = 0; b < a.tb; b++)
+		a.tup[(uint64_t)k * a.tb + b] = 0;
+}
+
+/* Wave-cooperative copy of n bytes: dwords when source and destination
+ * share their alignment mod 4 (256 bytes per step), bytes otherwise. */
+__device__ void wave_copy(uint8_t *dst, const uint8_t *src, uint64_t n, int lane)
+{
+	uint64_t o = 0;
+	if (!(((uintptr_t)dst ^ (uintptr_t)src) & 3)) {
+		const uint64_t head = (4 - ((uintptr_t)dst & 3)) & 3;
+		o = head < n ? head : n;
+		if ((uint64_t)lane < o)
+			dst[lane] = src[lane];
+		const uint64_t words = (n - o) / 4;
+		uint32_t *dw = reinterpret_cast<uint32_t *>(dst + o);
+		const uint32_t *sw = reinterpret_cast<const uint32_t *>(src + o);
+		for (uint64_t w = lane; w < words; w += kFragWave)
+			dw[w] = sw[w];
+		o += 4 * words;
+	}
+	for (uint64_t b = o + lane; b < n; b += kFragWave)
+		dst[b] = src[b];
+}
+
+__global__ __launch_bounds__(kFragBlock) void frag_count_kernel(FragArgs a)
+{
+	const uint64_t step = (uint64_t)gridDim.x * kFragBlock;
+	for (uint64_t i = (uint64_t)blockIdx.x * kFragBlock + threadIdx.x; i < a.n;
+	     i += step) {
+		if (!packet_head(a, (uint32_t)i))
+			continue;
+		uint32_t last;
+		uint64_t total;
+		if (packet_walk(a, (uint32_t)i, last, total)) {
+			atomicAdd(&a.fc[0], 1ull);
+			atomicAdd(&a.fc[1], (unsigned long long)bounce_size(total));
+			continue;
+		}
+		for (uint32_t k = (uint32_t)i; k <= last; k++) {
+			a.verdict[k] = XDPGPU_ABORTED;
+			zero_outputs(a, k);
+		}
+		if (a.stats) {
+			atomicAdd(&a.stats[CNT_FRAMES], 1ull);
+			atomicAdd(&a.stats[CNT_BYTES], (unsigned long long)total);
+			atomicAdd(&a.stats[CNT_VERDICT0 + XDPGPU_ABORTED], 1ull);
+		}
+	}
+}
+
+__global__ __launch_bounds__(kFragBlock) void frag_gather_kernel(FragArgs a)
+{
+	const int lane = threadIdx.x & (kFragWave - 1);
+	const uint64_t w0 = ((uint64_t)blockIdx.x * kFragBlock + threadIdx.x) / kFragWave;
+	const uint64_t nw = (uint64_t)gridDim.x * (kFragBlock / kFragWave);
+	for (uint64_t base = w0 * kFragWave; base < a.n; base += nw * kFragWave) {
+		const uint64_t i = base + lane;
+		uint32_t last = 0;
+		uint64_t total = 0, off = 0;
+		const bool mine = i < a.n && packet_head(a, (uint32_t)i) &&
+				  packet_walk(a, (uint32_t)i, last, total);
+		if (mine) {
+			const uint32_t k = (uint32_t)atomicAdd(&a.fc[2], 1ull);
+			off = atomicAdd(&a.fc[3], (unsigned long long)bounce_size(total));
+			*reinterpret_cast<uint4 *>(a.bdesc + k) =
+				make_uint4((uint32_t)off, (uint32_t)(off >> 32), (uint32_t)total, 0u);
+			a.bmap[k] = make_uint2((uint32_t)i, last - (uint32_t)i + 1);
+		}
+		/* the wave copies its packets one after the other */
+		for (uint64_t m = __ballot(mine); m; m &= m - 1) {
+			const int src = __builtin_ctzll(m);
+			const uint32_t first = rl32((uint32_t)i, src), lst = rl32(last, src);
+			uint8_t *dst = a.bounce + rl64(off, src);
+			uint64_t at = 0, end = 0;
+			for (uint32_t j = first; j <= lst; j++) {
+				const xdpgpu_desc d = a.desc[j];
+				const uint64_t eff = frag_eff(d);
+				wave_copy(dst + at, a.umem + eff, d.len, lane);
+				at += d.len;
+				end = eff + d.len;
+			}
+			/* udp_csum's over-read byte, then zeros to the 16-byte end */
+			for (uint64_t o = at + lane; o < bounce_size(at); o += kFragWave)
+				dst[o] = (o == at && end < a.usize) ? a.umem[end] : 0;
+		}
+	}
+}
+
+__global__ __launch_bounds__(kFragBlock) void frag_scatter_kernel(FragArgs a)
+{
+	const uint64_t step = (uint64_t)gridDim.x * kFragBlock;
+	for (uint64_t k = (uint64_t)blockIdx.x * kFragBlock + threadIdx.x; k < a.m;
+	     k += step) {
+		const uint2 mp = a.bmap[k];
+		const uint8_t v = a.bverdict[k];
+		for (uint32_t f = 0; f < mp.y; f++) {
+			a.verdict[mp.x + f] = v;
+			if (f)
+				zero_outputs(a, mp.x + f);
+		}
+		if (a.res)
+			*reinterpret_cast<uint4 *>(a.res + mp.x) =
+				*reinterpret_cast<const uint4 *>(a.bres + k);
+		for (uint32_t b = 0; b < a.tb; b++)
+			a.tup[(uint64_t)mp.x * a.tb + b] = a.btup[k * a.tb + b];
+		if (v != XDPGPU_TX)
+			continue;
+		/* the echo reply's bytes back into the fragments */
+		const uint4 bd = *reinterpret_cast<const uint4 *>(a.bdesc + k);
+		const uint8_t *src = a.bounce + (((uint64_t)bd.y << 32) | bd.x);
+		const uint64_t want = bd.z < 64u ? bd.z : 64u;
+		uint64_t at = 0;
+		for (uint32_t f = 0; f < mp.y && at < want; f++) {
+			const xdpgpu_desc d = a.desc[mp.x + f];
+			const uint64_t eff = frag_eff(d);
+			for (uint32_t o = 0; o < d.len && at < want; o++, at++)
+				a.umem[eff + o] = src[at];
+		}
+	}
+}
+
+uint32_t frag_blocks(uint64_t items)
+{
+	uint64_t b = (items + kFragBlock - 1) / kFragBlock;
+	if (b > kFragMaxBlocks)
+		b = kFragMaxBlocks;
+	return b ? (uint32_t)b : 1u;
+}
+
+} // namespace
+
+hipError_t launch_frag_count(const FragArgs &a, hipStream_t stream)
+{
+	hipLaunchKernelGGL(frag_count_kernel, dim3(frag_blocks(a.n)), dim3(kFragBlock),
+			   0, stream, a);
+	return hipGetLastError();
+}
+
+hipError_t launch_frag_gather(const FragArgs &a, hipStream_t stream)
+{
+	hipLaunchKernelGGL(frag_gather_kernel, dim3(frag_blocks(a.n)), dim3(kFragBlock),
+			   0, stream, a);
+	return hipGetLastError();
+}
+
+hipError_t launch_frag_scatter(const FragArgs &a, hipStream_t stream)
+{
+	hipLaunchKernelGGL(frag_scatter_kernel, dim3(frag_blocks(a.m)), dim3(kFragBlock),
+			   0, stream, a);
+	return hipGetLastError();
+}
+
+} // namespace xdpgpu

@@ -1291,8 +1291,18 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 	}
 	for (; t < ntiles; t += nwaves) {
 		const uint64_t i = t * kWave + lane;
-		const bool active = i < a.n;
 		const uint4 dv = dcur;
+		/* multi-buffer mode: the descriptors of packets of several
+		 * fragments are the fragment kernels' (frags.hip) */
+		bool skip = false;
+		if (a.frags) {
+			const uint32_t contd = dv.w & XDPGPU_PKT_CONTD;
+			uint32_t prev = (uint32_t)__shfl_up((int)contd, 1, kWave);
+			if (lane == 0)
+				prev = t ? a.desc[t * kWave - 1].options & XDPGPU_PKT_CONTD : 0u;
+			skip = (contd | prev) != 0;
+		}
+		const bool active = (i < a.n) & !skip;
 
 		/* 1. this lane's window out of LDS (4 conflict-free b128 reads),
 		 * then the next tile's DMA and descriptors */

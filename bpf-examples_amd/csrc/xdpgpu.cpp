@@ -43,6 +43,17 @@ struct Slot {
 	uint4 *d_ylist = nullptr;     /* exception payload sums (generic -> bulk) */
 	uint64_t xcap = 0;
 	uint32_t *d_xcount = nullptr;
+	/* multi-buffer packets (XDPGPU_CFG_FRAGS) */
+	unsigned long long *d_fc = nullptr;   /* fragment kernels' counters */
+	unsigned long long *h_fc = nullptr;   /* pinned host copy           */
+	uint8_t *d_bounce = nullptr;          /* bounce UMEM                */
+	uint64_t bounce_cap = 0;
+	xdpgpu_desc *d_bdesc = nullptr;       /* per packet                 */
+	uint2 *d_bmap = nullptr;
+	uint8_t *d_bverdict = nullptr;
+	xdpgpu_result *d_bres = nullptr;
+	uint8_t *d_btup = nullptr;
+	uint64_t pk_cap = 0;
 	bool busy = false;
 	/* pending host copies for xdpgpu_wait() */
 	uint32_t n = 0;
@@ -134,6 +145,15 @@ static void free_slot(Slot &s)
 		(void)hipFree(s.d_xcount);
 	if (s.d_ylist)
 		(void)hipFree(s.d_ylist);
+	if (s.h_fc)
+		(void)hipHostFree(s.h_fc);
+	(void)hipFree(s.d_fc);
+	(void)hipFree(s.d_bounce);
+	(void)hipFree(s.d_bdesc);
+	(void)hipFree(s.d_bmap);
+	(void)hipFree(s.d_bverdict);
+	(void)hipFree(s.d_bres);
+	(void)hipFree(s.d_btup);
 	if (s.done)
 		(void)hipEventDestroy(s.done);
 	if (s.stream)
@@ -318,6 +338,51 @@ static int ensure_xlist(xdpgpu_ctx *ctx, Slot &s, uint32_t n)
 	return 0;
 }
 
+/* Fragment scratch of a slot (XDPGPU_CFG_FRAGS): the counters, and the
+ * bounce UMEM and per-packet arrays for m packets of `bytes` bounce bytes.
+ * Called with the slot's stream idle. */
+static int ensure_frag_bufs(xdpgpu_ctx *ctx, Slot &s, uint64_t m, uint64_t bytes)
+{
+	if (!s.d_fc && (hipMalloc(&s.d_fc, 4 * sizeof(unsigned long long)) != hipSuccess ||
+			hipHostMalloc((void **)&s.h_fc, 4 * sizeof(unsigned long long), 0) !=
+				hipSuccess))
+		return set_err(ctx, -ENOMEM, "fragment counters");
+	if (bytes && bytes + 64 > s.bounce_cap) {
+		(void)hipFree(s.d_bounce);
+		s.d_bounce = nullptr;
+		s.bounce_cap = 0;
+		const uint64_t cap = std::max<uint64_t>(bytes + 64, 1ull << 20);
+		if (hipMalloc(&s.d_bounce, cap) != hipSuccess)
+			return set_err(ctx, -ENOMEM, "bounce UMEM of %llu bytes",
+				       (unsigned long long)cap);
+		s.bounce_cap = cap;
+	}
+	if (m > s.pk_cap) {
+		(void)hipFree(s.d_bdesc);
+		(void)hipFree(s.d_bmap);
+		(void)hipFree(s.d_bverdict);
+		(void)hipFree(s.d_bres);
+		(void)hipFree(s.d_btup);
+		s.d_bdesc = nullptr;
+		s.d_bmap = nullptr;
+		s.d_bverdict = nullptr;
+		s.d_bres = nullptr;
+		s.d_btup = nullptr;
+		s.pk_cap = 0;
+		const uint64_t cap = std::max<uint64_t>(m, 4096);
+		const uint32_t tb = tuple_bytes(ctx->cfg.tuple_fmt);
+		if (hipMalloc(&s.d_bdesc, cap * sizeof(xdpgpu_desc)) != hipSuccess ||
+		    hipMalloc(&s.d_bmap, cap * sizeof(uint2)) != hipSuccess ||
+		    hipMalloc(&s.d_bverdict, cap) != hipSuccess ||
+		    hipMalloc(&s.d_bres, cap * sizeof(xdpgpu_result)) != hipSuccess ||
+		    (tb && hipMalloc(&s.d_btup, cap * tb) != hipSuccess))
+			return set_err(ctx, -ENOMEM, "fragment arrays for %llu packets",
+				       (unsigned long long)cap);
+		s.pk_cap = cap;
+	}
+	return 0;
+}
+
 static int enqueue_rx(xdpgpu_ctx *ctx, Slot &s, uint8_t *d_umem, uint64_t usize,
 		      const xdpgpu_desc *d_desc, uint32_t n, uint8_t *d_verdict,
 		      xdpgpu_result *d_res, uint8_t *d_tup, hipStream_t stream)
@@ -346,11 +411,68 @@ static int enqueue_rx(xdpgpu_ctx *ctx, Slot &s, uint8_t *d_umem, uint64_t usize,
 	a.ycount = s.d_xcount + kMaxRxBlocks * 4 * 2;
 	a.ydefer = !((ctx->cfg.tune >> 8) & 1);
 	a.force_generic = (ctx->cfg.tune >> 9) & 1;
+	a.frags = (ctx->cfg.flags & XDPGPU_CFG_FRAGS) ? 1u : 0u;
+
+	/* multi-buffer packets: counted (and the broken ones finished) before
+	 * the RX kernels, which skip them; one host round trip for the bounce
+	 * sizes */
+	FragArgs f;
+	memset(&f, 0, sizeof(f));
+	uint64_t m = 0, bbytes = 0;
+	if (a.frags) {
+		rc = ensure_frag_bufs(ctx, s, 0, 0);
+		if (rc)
+			return rc;
+		f.umem = d_umem;
+		f.usize = usize;
+		f.desc = d_desc;
+		f.n = n;
+		f.verdict = d_verdict;
+		f.res = d_res;
+		f.tup = d_tup;
+		f.tb = d_tup ? tuple_bytes(ctx->cfg.tuple_fmt) : 0;
+		f.stats = a.stats;
+		f.fc = s.d_fc;
+		HIP_TRY(ctx, hipMemsetAsync(s.d_fc, 0, 4 * sizeof(unsigned long long), stream));
+		HIP_TRY(ctx, launch_frag_count(f, stream));
+		HIP_TRY(ctx, hipMemcpyAsync(s.h_fc, s.d_fc, 2 * sizeof(unsigned long long),
+					    hipMemcpyDeviceToHost, stream));
+		HIP_TRY(ctx, hipStreamSynchronize(stream));
+		m = s.h_fc[0];
+		bbytes = s.h_fc[1];
+		rc = ensure_frag_bufs(ctx, s, m, bbytes);
+		if (rc)
+			return rc;
+	}
 	hipEvent_t *ev = nullptr;
 	if (ctx->tev && ctx->tn < XDPGPU_TIMING_MAX)
 		ev = ctx->tev + 4 * ctx->tn++;
 	HIP_TRY(ctx, launch_rx(a, ctx->cfg.window, ctx->max_blocks, stream,
 			       ctx->cfg.tune, ev));
+	if (!m)
+		return 0;
+	/* one frame per packet: gathered into the bounce UMEM, the RX kernels
+	 * over the bounce batch, the outputs back to the packets' descriptors */
+	f.bounce = s.d_bounce;
+	f.bdesc = s.d_bdesc;
+	f.bmap = s.d_bmap;
+	f.bverdict = s.d_bverdict;
+	f.bres = s.d_bres;
+	f.btup = s.d_btup;
+	f.m = (uint32_t)m;
+	HIP_TRY(ctx, launch_frag_gather(f, stream));
+	RxArgs b = a;
+	b.umem = s.d_bounce;
+	b.usize = bbytes;
+	b.desc = s.d_bdesc;
+	b.n = (uint32_t)m;
+	b.verdict = s.d_bverdict;
+	b.res = d_res ? s.d_bres : nullptr;
+	b.tup = d_tup ? s.d_btup : nullptr;
+	b.frags = 0;
+	HIP_TRY(ctx, launch_rx(b, ctx->cfg.window, ctx->max_blocks, stream,
+			       ctx->cfg.tune, nullptr));
+	HIP_TRY(ctx, launch_frag_scatter(f, stream));
 	return 0;
 }
 

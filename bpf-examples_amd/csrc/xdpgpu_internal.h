@@ -52,6 +52,8 @@ struct RxArgs {
 				    * region of both lists                  */
 	uint32_t nregions;         /* set by the launcher: fast-kernel waves */
 	uint32_t force_generic;    /* 1: defer every frame (diagnostic)     */
+	uint32_t frags;            /* XDPGPU_CFG_FRAGS: skip the descriptors
+				    * of packets of several (frags.hip)     */
 };
 
 /* ev (nullable): four events recorded before the fast kernel and after
@@ -61,6 +63,33 @@ hipError_t launch_rx(const RxArgs &a, uint32_t window, uint32_t max_blocks,
 uint32_t rx_grid_blocks(uint32_t n, uint32_t max_blocks);
 uint32_t rx_xregion(uint32_t n, uint32_t blocks);
 hipError_t launch_ceiling(const RxArgs &a, uint32_t blocks, hipStream_t stream);
+
+/* Multi-buffer packets (XDPGPU_CFG_FRAGS, frags.hip): count the packets of
+ * several descriptors (and finish the broken ones), gather them into a
+ * bounce UMEM as one frame each, scatter the bounce batch's outputs back. */
+struct FragArgs {
+	uint8_t *umem;
+	uint64_t usize;
+	const xdpgpu_desc *desc;
+	uint32_t n;
+	uint8_t *verdict;
+	xdpgpu_result *res;        /* nullable */
+	uint8_t *tup;              /* nullable */
+	uint32_t tb;               /* tuple bytes, 0 without tuples         */
+	unsigned long long *stats; /* block 0's counter slot, or null       */
+	unsigned long long *fc;    /* [0] packets, [1] bounce bytes (count);
+				    * [2], [3] the gather's cursors         */
+	uint8_t *bounce;           /* gather, scatter */
+	xdpgpu_desc *bdesc;        /* one per packet  */
+	uint2 *bmap;               /* first descriptor, descriptors         */
+	uint8_t *bverdict;
+	xdpgpu_result *bres;
+	uint8_t *btup;
+	uint32_t m;                /* scatter: packets */
+};
+hipError_t launch_frag_count(const FragArgs &a, hipStream_t stream);
+hipError_t launch_frag_gather(const FragArgs &a, hipStream_t stream);
+hipError_t launch_frag_scatter(const FragArgs &a, hipStream_t stream);
 
 /* nat64 static tables (v6_state_map and v4_reversemap, nat64_kern.c:17-46):
  * 4-way buckets of one 128-byte line, so a lookup touches one line; the

@@ -41,6 +41,8 @@ CFG_VERIFY_CSUM = 0x1
 CFG_ICMP6_ECHO = 0x2
 CFG_TIMING = 0x8
 CFG_STATS = 0x4
+CFG_FRAGS = 0x10      # multi-buffer packets (include/xdpgpu.h)
+PKT_CONTD = 0x1       # xdp_desc.options: the packet continues
 CFG_DEFAULT = CFG_VERIFY_CSUM | CFG_STATS
 
 TUPLE_NONE, TUPLE_V4, TUPLE_NET = 0, 1, 2

@@ -113,6 +113,19 @@ struct xdpgpu_network_tuple {
 #define XDPGPU_CFG_ICMP6_ECHO  0x2 /* process_packet echo responder (af_xdp_user.c:968-1040)  */
 #define XDPGPU_CFG_STATS       0x4 /* keep per-verdict counters (xdpgpu_stats)                */
 #define XDPGPU_CFG_TIMING      0x8 /* record HIP events around each RX kernel (diagnostic)     */
+/* Multi-buffer packets (xdpsock --frags, xdpsock.c:67,1349; the XDP_USE_SG
+ * socket): a packet is a run of descriptors whose options carry
+ * XDPGPU_PKT_CONTD on all but the last (headers/linux/if_xdp.h:122).  The
+ * packet is processed as one frame: the concatenation of its fragments,
+ * with udp_csum's over-read byte the byte after the last fragment.  Every
+ * descriptor of the packet gets the packet's verdict; the first carries its
+ * result record and tuple, the others all-zero ones; an ICMPv6 echo reply
+ * is written back into the fragments.  A packet the batch ends inside of,
+ * or with a fragment outside the UMEM, is ABORTED.  The counters count
+ * packets (and their bytes).  Without this flag options are ignored and
+ * every descriptor is a frame, as process_packet does. */
+#define XDPGPU_CFG_FRAGS       0x10
+#define XDPGPU_PKT_CONTD       0x1 /* xdp_desc.options: the packet continues  */
 #define XDPGPU_CFG_DEFAULT     (XDPGPU_CFG_VERIFY_CSUM | XDPGPU_CFG_STATS)
 
 struct xdpgpu_cfg {

@@ -700,6 +700,63 @@ static void frame_pipeline(uint8_t *umem, uint64_t usize,
 	o->verdict = XDPGPU_REDIRECT;
 }
 
+/* Multi-buffer packets (XDPGPU_CFG_FRAGS, include/xdpgpu.h): descriptors
+ * [i, j] with XDPGPU_PKT_CONTD on all but d[j] (IS_EOP_DESC, xdpsock.c:67;
+ * j == n when the batch ends inside the packet).  The fragments are
+ * concatenated, with the byte after the last one as udp_csum's over-read
+ * byte, and run through frame_pipeline as one frame; an echo rewrite is
+ * copied back into the fragments.  *bytes: the packet's byte count. */
+static void packet_pipeline(uint8_t *umem, uint64_t usize,
+			    const struct xdpgpu_desc *d, uint32_t i, uint32_t j,
+			    uint32_t n, uint32_t flags, uint32_t initval,
+			    struct frame_out *o, uint64_t *bytes)
+{
+	const uint32_t last = j < n ? j : n - 1;
+	uint64_t total = 0, at, end = 0;
+	int ok = j < n;
+	uint32_t k;
+	uint8_t *buf;
+
+	for (k = i; k <= last; k++) {
+		const uint64_t eff = (d[k].addr & ((1ull << 48) - 1)) + (d[k].addr >> 48);
+
+		total += d[k].len;
+		if ((uint64_t)d[k].len > usize || eff > usize - d[k].len)
+			ok = 0;
+		end = eff + d[k].len;
+	}
+	*bytes = total;
+	memset(o, 0, sizeof(*o));
+	o->verdict = XDPGPU_ABORTED;
+	if (!ok || total > 0xffffffffull)
+		return;
+	buf = malloc(total + 1);
+	if (!buf)
+		return;
+	for (at = 0, k = i; k <= last; k++) {
+		const uint64_t eff = (d[k].addr & ((1ull << 48) - 1)) + (d[k].addr >> 48);
+
+		memcpy(buf + at, umem + eff, d[k].len);
+		at += d[k].len;
+	}
+	buf[total] = end < usize ? umem[end] : 0;
+	{
+		const struct xdpgpu_desc pd = { 0, (uint32_t)total, 0 };
+
+		frame_pipeline(buf, total + 1, &pd, flags, initval, o);
+	}
+	if (o->verdict == XDPGPU_TX) {
+		for (at = 0, k = i; k <= last; k++) {
+			const uint64_t eff = (d[k].addr & ((1ull << 48) - 1)) +
+					     (d[k].addr >> 48);
+
+			memcpy(umem + eff, buf + at, d[k].len);
+			at += d[k].len;
+		}
+	}
+	free(buf);
+}
+
 static void emit_tuple(const struct frame_out *o, uint32_t fmt, void *tuples,
 		       uint32_t i)
 {
@@ -732,14 +789,29 @@ int oracle_process(uint8_t *umem, uint64_t umem_size,
 		   uint8_t *verdict, struct xdpgpu_result *res, void *tuples,
 		   struct xdpgpu_stats *stats)
 {
+	struct frame_out zero;
 	uint32_t i;
 
 	if (!umem || !descs || !verdict)
 		return -22;
-	for (i = 0; i < n; i++) {
+	memset(&zero, 0, sizeof(zero));
+	for (i = 0; i < n;) {
 		struct frame_out o;
+		uint64_t bytes;
+		uint32_t j = i, last, k;
 
-		frame_pipeline(umem, umem_size, &descs[i], cfg_flags, initval, &o);
+		/* a packet of several descriptors (XDPGPU_CFG_FRAGS) */
+		if (cfg_flags & XDPGPU_CFG_FRAGS)
+			while (j < n && (descs[j].options & XDPGPU_PKT_CONTD))
+				j++;
+		if (j == i) {
+			frame_pipeline(umem, umem_size, &descs[i], cfg_flags, initval, &o);
+			bytes = descs[i].len;
+		} else {
+			packet_pipeline(umem, umem_size, descs, i, j, n, cfg_flags,
+					initval, &o, &bytes);
+		}
+		last = j < n ? j : n - 1;
 		if (o.verdict == XDPGPU_ABORTED || o.verdict == XDPGPU_PASS) {
 			/* not delivered to the application: zero records */
 			uint8_t v = o.verdict;
@@ -747,19 +819,24 @@ int oracle_process(uint8_t *umem, uint64_t umem_size,
 			memset(&o, 0, sizeof(o));
 			o.verdict = v;
 		}
-		verdict[i] = o.verdict;
-		if (res)
-			res[i] = o.r;
-		emit_tuple(&o, tuple_fmt, tuples, i);
+		/* every descriptor of a packet: its verdict; the first: its
+		 * record and tuple, the others all-zero ones */
+		for (k = i; k <= last; k++) {
+			verdict[k] = o.verdict;
+			if (res)
+				res[k] = k == i ? o.r : zero.r;
+			emit_tuple(k == i ? &o : &zero, tuple_fmt, tuples, k);
+		}
 		if (stats) {
 			stats->frames++;
-			stats->bytes += descs[i].len;
+			stats->bytes += bytes;
 			stats->verdict[o.verdict]++;
 			stats->l3_bad += o.l3_bad;
 			stats->l4_bad += o.l4_bad;
 			stats->l4_absent += o.l4_absent;
 			stats->frag += o.frag;
 		}
+		i = last + 1;
 	}
 	return 0;
 }

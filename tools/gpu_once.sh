@@ -1,10 +1,10 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_nat64.py tests/test_apps.py -m gpu -q -x --timeout 200 --timeout-method thread > gpurun_out/pytest_nat64.log 2>&1; rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|^FAILED|Error" gpurun_out/pytest_nat64.log | head -12
+timeout -k 10 300 python -u -m pytest tests/test_frags.py -m gpu -q -x --timeout 200 --timeout-method thread > gpurun_out/pytest_frags.log 2>&1; rc=$?; echo "frags pytest rc=$rc"; grep -E "passed|failed|^FAILED|Error|error" gpurun_out/pytest_frags.log | head -12
 [ $rc -eq 0 ] || exit $rc
-for lib in build/ab_HEAD/libxdpgpu.so bpf-examples_amd/csrc/libxdpgpu.so; do
-for args in "--direction 0" "--direction 1" "--direction 1 --headroom 32"; do
-  XDPGPU_LIB=$lib timeout -k 10 300 python3 tools/nat64_probe.py $args > gpurun_out/n64.log 2>&1 || exit 3; echo "$lib $args: $(grep -v amdgpu.ids gpurun_out/n64.log | cut -c1-80)"
-done
+timeout -k 10 600 python -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread > gpurun_out/pytest.log 2>&1; rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|^FAILED" gpurun_out/pytest.log | head -8
+[ $rc -eq 0 ] || exit $rc
+for lib in build/ab_HEAD/libxdpgpu.so bpf-examples_amd/csrc/libxdpgpu.so build/ab_HEAD/libxdpgpu.so bpf-examples_amd/csrc/libxdpgpu.so; do
+  XDPGPU_LIB=$lib timeout -k 10 300 python3 tools/tune_rx.py --variants 64:0 --rounds 5 > gpurun_out/t64.log 2>&1 || exit 3; echo "$lib $(grep -v amdgpu.ids gpurun_out/t64.log | cut -c1-60)"
 done
