@@ -255,7 +255,7 @@ int main(int argc, char **argv)
 	int rc;
 	if (pcap) {
 		/* af_xdp_user's UMEM: FRAME_SIZE chunks, af_xdp_user.c:56 */
-		rc = rx_source_pcap(&src, pcap, 4096, 0, false, 0);
+		rc = rx_source_pcap(&src, pcap, 4096, 0, false, false, 0);
 		if (rc) {
 			fprintf(stderr, "ERR: %s: %s\n", pcap, strerror(-rc));
 			return EXIT_FAIL;

@@ -86,6 +86,7 @@ int rx_source_pool(struct rx_source *src, const struct xdpgpu_pool_spec *spec,
 	}
 	src->umem_size = size;
 	src->n = n;
+	src->packets = n;
 	src->headroom = spec->headroom;
 	int rc = xdpgpu_pool_generate(spec, src->umem, size, src->descs, n, NULL);
 	if (rc)
@@ -102,7 +103,7 @@ static uint32_t rd32(const uint8_t *p, bool swap)
 }
 
 int rx_source_pcap(struct rx_source *src, const char *path, uint32_t chunk_size,
-		   uint32_t headroom, bool unaligned, uint32_t max_frames)
+		   uint32_t headroom, bool unaligned, bool frags, uint32_t max_frames)
 {
 	memset(src, 0, sizeof(*src));
 	FILE *f = fopen(path, "rb");
@@ -134,8 +135,9 @@ int rx_source_pcap(struct rx_source *src, const char *path, uint32_t chunk_size,
 		return -EINVAL;
 	}
 
-	/* pass 1: sizes */
-	uint64_t n = 0, size = 0;
+	/* pass 1: sizes (a record split over nch chunks with frags) */
+	const uint32_t room = unaligned ? 0 : chunk_size - headroom;
+	uint64_t n = 0, size = 0, packets = 0;
 	long body = ftell(f);
 	uint8_t rh[16];
 	while (fread(rh, 1, 16, f) == 16) {
@@ -146,16 +148,14 @@ int rx_source_pcap(struct rx_source *src, const char *path, uint32_t chunk_size,
 		}
 		if (max_frames && n >= max_frames)
 			break;
-		if (!unaligned && incl > chunk_size - headroom) {
+		if ((!unaligned && incl > room && !frags) || incl > 65535) {
 			src->skipped++;
 			continue;
 		}
-		if (incl > 65535) {
-			src->skipped++;
-			continue;
-		}
-		size += unaligned ? ((headroom + incl + 63) & ~63ull) : chunk_size;
-		n++;
+		const uint64_t nch = unaligned ? 1 : incl > room ? (incl + room - 1) / room : 1;
+		size += unaligned ? ((headroom + incl + 63) & ~63ull) : nch * chunk_size;
+		n += nch;
+		packets++;
 	}
 	if (!n || n > 0xffffffffull) {
 		fclose(f);
@@ -171,6 +171,7 @@ int rx_source_pcap(struct rx_source *src, const char *path, uint32_t chunk_size,
 	}
 	src->umem_size = size;
 	src->n = (uint32_t)n;
+	src->packets = (uint32_t)packets;
 	src->skipped = skipped;
 	src->chunk_size = unaligned ? 0 : chunk_size;
 	src->headroom = headroom;
@@ -182,20 +183,26 @@ int rx_source_pcap(struct rx_source *src, const char *path, uint32_t chunk_size,
 	uint32_t k = 0;
 	while (k < n && fread(rh, 1, 16, f) == 16) {
 		uint32_t incl = rd32(rh + 8, swap);
-		if ((!unaligned && incl > chunk_size - headroom) || incl > 65535) {
+		if ((!unaligned && incl > room && !frags) || incl > 65535) {
 			fseek(f, incl, SEEK_CUR);
 			continue;
 		}
-		if (fread(src->umem + off + headroom, 1, incl, f) != incl) {
-			fclose(f);
-			rx_source_free(src);
-			return -EPROTO;
-		}
-		src->descs[k].addr = off + headroom;
-		src->descs[k].len = incl;
-		src->descs[k].options = 0;
-		off += unaligned ? ((headroom + incl + 63) & ~63ull) : chunk_size;
-		k++;
+		/* the record's bytes over one chunk, or several (fragments) */
+		uint32_t left = incl;
+		do {
+			const uint32_t piece = unaligned || left <= room ? left : room;
+			if (k >= n || fread(src->umem + off + headroom, 1, piece, f) != piece) {
+				fclose(f);
+				rx_source_free(src);
+				return -EPROTO;
+			}
+			left -= piece;
+			src->descs[k].addr = off + headroom;
+			src->descs[k].len = piece;
+			src->descs[k].options = left ? XDPGPU_PKT_CONTD : 0;
+			off += unaligned ? ((headroom + piece + 63) & ~63ull) : chunk_size;
+			k++;
+		} while (left);
 	}
 	fclose(f);
 	return 0;
@@ -248,6 +255,8 @@ void rx_source_describe(const struct rx_source *src, const char *what)
 	       what, src->n, (unsigned long long)bytes, src->n ? lo : 0, hi,
 	       (unsigned long long)src->umem_size, src->chunk_size, src->headroom,
 	       src->umem_flags & XDPGPU_UMEM_UNALIGNED_CHUNK_FLAG ? ", unaligned" : "");
+	if (src->packets != src->n)
+		printf(", %u packets", src->packets);
 	if (src->skipped)
 		printf(", %llu records skipped (larger than a chunk)",
 		       (unsigned long long)src->skipped);
@@ -259,7 +268,7 @@ void rx_source_describe(const struct rx_source *src, const char *what)
 
 struct rx_stats_state {
 	uint64_t t_prev;
-	uint64_t rx_prev, tx_prev, rxb_prev, txb_prev;
+	uint64_t rx_prev, tx_prev, rxb_prev, txb_prev, rxf_prev, txf_prev;
 };
 
 static void print_stats(const struct rx_opts *o, const struct rx_totals *t,
@@ -272,11 +281,26 @@ static void print_stats(const struct rx_opts *o, const struct rx_totals *t,
 		/* dump_stats, xdpsock.c:478-582 */
 		const char *fmt = "%-18s %'-14.0f %'-14lu\n";
 		printf("\n sock0@%s\n", label);
-		printf("%-18s %-14s %-14s %-14.2f\n", "", "pps", "pkts", dt);
-		printf(fmt, "rx", (double)(t->rx_pkts - st->rx_prev) / period,
-		       (unsigned long)t->rx_pkts);
-		printf(fmt, "tx", (double)(t->tx_pkts - st->tx_prev) / period,
-		       (unsigned long)t->tx_pkts);
+		if (o->frags) {
+			/* the --frags table, xdpsock.c:500-514 */
+			const char *ffmt = "%-18s %'-14.0f %'-14lu %'-14.0f %'-14lu\n";
+			printf("%-18s %-14s %-14s %-14s %-14s %-14.2f\n", "", "pps", "pkts",
+			       "fps", "frags", dt);
+			printf(ffmt, "rx", (double)(t->rx_pkts - st->rx_prev) / period,
+			       (unsigned long)t->rx_pkts,
+			       (double)(t->rx_frags - st->rxf_prev) / period,
+			       (unsigned long)t->rx_frags);
+			printf(ffmt, "tx", (double)(t->tx_pkts - st->tx_prev) / period,
+			       (unsigned long)t->tx_pkts,
+			       (double)(t->tx_frags - st->txf_prev) / period,
+			       (unsigned long)t->tx_frags);
+		} else {
+			printf("%-18s %-14s %-14s %-14.2f\n", "", "pps", "pkts", dt);
+			printf(fmt, "rx", (double)(t->rx_pkts - st->rx_prev) / period,
+			       (unsigned long)t->rx_pkts);
+			printf(fmt, "tx", (double)(t->tx_pkts - st->tx_prev) / period,
+			       (unsigned long)t->tx_pkts);
+		}
 		if (o->cfg_flags & XDPGPU_CFG_STATS) {
 			/* extra: the GPU verdict histogram (enum xdp_action) */
 			printf(fmt, "gpu aborted", 0.0, (unsigned long)t->verdict[XDPGPU_ABORTED]);
@@ -306,6 +330,8 @@ static void print_stats(const struct rx_opts *o, const struct rx_totals *t,
 	st->tx_prev = t->tx_pkts;
 	st->rxb_prev = t->rx_bytes;
 	st->txb_prev = t->tx_bytes;
+	st->rxf_prev = t->rx_frags;
+	st->txf_prev = t->tx_frags;
 }
 
 /* ------------------------------------------------------------------ */
@@ -329,21 +355,26 @@ static void swap_macs(uint8_t *p)
 	memcpy(p + 6, t, 6);
 }
 
+/* Apply a batch's verdicts as the reference bodies do (rx_drop, l2fwd:
+ * xdpsock.c:1462-1506, 1718-1784; process_packet's TX, af_xdp_user.c:
+ * 1023-1036).  With fragments (IS_EOP_DESC, xdpsock.c:67) packets count on
+ * their last descriptor and the MAC swap touches a packet's first. */
 static void apply(const struct rx_source *src, const struct rx_opts *o,
 		  const struct rx_slot *s, struct rx_totals *t, uint8_t *first_pass)
 {
 	for (uint32_t i = 0; i < s->n; i++) {
 		const uint8_t v = s->v[i];
 		const uint32_t len = s->d[i].len;
-		t->rx_pkts++;
+		const bool eop = !o->frags || !(s->d[i].options & XDPGPU_PKT_CONTD);
+		const bool first = t->open_frags++ == 0;
+		t->rx_frags++;
 		t->rx_bytes += len;
-		if (v < XDPGPU_NUM_VERDICTS)
-			t->verdict[v]++;
 		if (first_pass && s->first + i < src->n)
 			first_pass[s->first + i] = v;
 		bool tx = false;
 		if (o->mode == RX_MODE_L2FWD && v == XDPGPU_REDIRECT) {
-			swap_macs(src->umem + desc_off(&s->d[i]));
+			if (first)
+				swap_macs(src->umem + desc_off(&s->d[i]));
 			tx = true;
 		} else if (v == XDPGPU_TX) {
 			/* process_packet returned true: the reply goes out
@@ -351,8 +382,16 @@ static void apply(const struct rx_source *src, const struct rx_opts *o,
 			tx = o->mode != RX_MODE_DROP;
 		}
 		if (tx) {
-			t->tx_pkts++;
+			t->tx_frags++;
 			t->tx_bytes += len;
+		}
+		if (eop) {
+			t->rx_pkts++;
+			if (v < XDPGPU_NUM_VERDICTS)
+				t->verdict[v]++;
+			if (tx)
+				t->tx_pkts++;
+			t->open_frags = 0;
 		}
 	}
 }
@@ -429,6 +468,16 @@ int rx_run(const struct rx_source *src, const struct rx_opts *o,
 			s->first = pos;
 			for (uint32_t i = 0; i < s->n; i++)
 				s->d[i] = src->descs[(pos + i) % src->n];
+			/* fragments: release whole packets only (l2fwd's
+			 * frags_done, xdpsock.c:1764-1775); the rest is peeked
+			 * again with the next batch */
+			if (o->frags && (s->d[s->n - 1].options & XDPGPU_PKT_CONTD)) {
+				uint32_t e = s->n - 1;
+				while (e && (s->d[e - 1].options & XDPGPU_PKT_CONTD))
+					e--;
+				if (e)
+					s->n = e;
+			}
 			rc = xdpgpu_submit(ctx, k & 1, s->d, s->n, s->v, NULL, NULL);
 			if (rc)
 				break;
@@ -479,12 +528,14 @@ int rx_run(const struct rx_source *src, const struct rx_opts *o,
 	if (!rc && o->json) {
 		const double mpps = out->seconds > 0 ? out->rx_pkts / out->seconds / 1e6 : 0;
 		printf("{\"prog\": \"%s\", \"frames\": %llu, \"seconds\": %.6f, \"mpps\": %.3f, "
-		       "\"rx_pkts\": %llu, \"rx_bytes\": %llu, \"tx_pkts\": %llu, "
+		       "\"rx_pkts\": %llu, \"rx_frags\": %llu, \"rx_bytes\": %llu, "
+		       "\"tx_pkts\": %llu, "
 		       "\"tx_bytes\": %llu, \"batch\": %u, \"batches\": %llu, "
 		       "\"verdict\": {\"ABORTED\": %llu, \"DROP\": %llu, \"PASS\": %llu, "
 		       "\"TX\": %llu, \"REDIRECT\": %llu}}\n",
 		       o->prog, (unsigned long long)out->rx_pkts, out->seconds, mpps,
-		       (unsigned long long)out->rx_pkts, (unsigned long long)out->rx_bytes,
+		       (unsigned long long)out->rx_pkts, (unsigned long long)out->rx_frags,
+		       (unsigned long long)out->rx_bytes,
 		       (unsigned long long)out->tx_pkts, (unsigned long long)out->tx_bytes,
 		       o->batch, (unsigned long long)out->batches,
 		       (unsigned long long)out->verdict[0], (unsigned long long)out->verdict[1],

@@ -30,6 +30,8 @@ struct rx_source {
 	uint32_t headroom;
 	uint32_t umem_flags;     /* XDPGPU_UMEM_UNALIGNED_CHUNK_FLAG       */
 	uint64_t skipped;        /* pcap records that did not fit a chunk */
+	uint32_t packets;        /* packets: n, or fewer when split into
+				  * fragments (XDPGPU_PKT_CONTD)           */
 };
 
 /* Synthetic pool (xdpgpu_pool_generate) of n frames.  0 or -errno. */
@@ -39,10 +41,13 @@ int rx_source_pool(struct rx_source *src, const struct xdpgpu_pool_spec *spec,
 /* Frames of a classic pcap file (LINKTYPE_ETHERNET; either byte order,
  * micro- or nanosecond timestamps), at most max_frames (0: all).  Aligned
  * mode: one chunk of chunk_size bytes per frame, the frame at headroom
- * (xdpsock's UMEM geometry, xdpsock.c:2062); unaligned: packed at 64-byte
- * rounded strides.  0 or -errno (-EPROTO: not a usable pcap). */
+ * (xdpsock's UMEM geometry, xdpsock.c:2062); a record longer than a chunk
+ * is skipped, or with frags split over consecutive chunks as a multi-buffer
+ * packet (XDPGPU_PKT_CONTD on all but the last, xdpsock --frags).
+ * Unaligned: packed at 64-byte rounded strides.  0 or -errno (-EPROTO: not
+ * a usable pcap). */
 int rx_source_pcap(struct rx_source *src, const char *path, uint32_t chunk_size,
-		   uint32_t headroom, bool unaligned, uint32_t max_frames);
+		   uint32_t headroom, bool unaligned, bool frags, uint32_t max_frames);
 
 void rx_source_free(struct rx_source *src);
 
@@ -76,6 +81,9 @@ struct rx_opts {
 	enum rx_stats_fmt stats_fmt;
 	bool quiet;
 	bool json;               /* final JSON summary line on stdout         */
+	bool frags;              /* multi-buffer packets (XDPGPU_CFG_FRAGS):
+				  * batches end on a packet's last fragment,
+				  * packets and fragments counted apart    */
 	const char *verdict_out; /* per-frame verdicts of the first pass      */
 	const char *tx_pcap;     /* frames sent on TX in the first pass       */
 	const char *prog;        /* program name for messages                 */
@@ -84,6 +92,8 @@ struct rx_opts {
 
 struct rx_totals {
 	uint64_t rx_pkts, rx_bytes, tx_pkts, tx_bytes;
+	uint64_t rx_frags, tx_frags;  /* descriptors (xdpsock ring_stats)   */
+	uint32_t open_frags;          /* fragments of the packet in progress */
 	uint64_t verdict[XDPGPU_NUM_VERDICTS];
 	uint64_t batches;
 	double seconds;

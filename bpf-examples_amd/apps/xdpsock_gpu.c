@@ -9,8 +9,10 @@
  * interval, -Q, -x, -f frame size and -u unaligned chunks (UMEM geometry),
  * and the generator's -s/-P/-V/-J/-K/-G/-H (gen_eth_hdr_data,
  * xdpsock.c:893-971) for pool mode.  Socket and scheduling options (-i, -q,
- * -p, -S, -N, -z, -c, -m, -M, -B, -R, -F, -w, -W, -U, -I, -O, -T, -y, -a)
- * are parsed as xdpsock parses them and only label the statistics: frames
+ * -p, -S, -N, -z, -c, -m, -M, -B, -R, -w, -W, -U, -I, -O, -T, -y, -a)
+ * are parsed as xdpsock parses them and only label the statistics.  -F
+ * (--frags) splits pcap records longer than a chunk into multi-buffer
+ * packets (XDPGPU_CFG_FRAGS) and counts packets and fragments.  Frames
  * come from a UMEM this program fills, either a synthetic pool (--pool N)
  * or a pcap file (--pcap FILE).  Live AF_XDP sockets are not part of this
  * build.
@@ -120,7 +122,9 @@ static void usage(const char *prog)
 		"  -H, --tx-smac=<MAC>  Pool source MAC\n"
 		"  -x, --extra-stats	GPU verdict counters in the statistics\n"
 		"  -Q, --quiet          Do not display any stats\n"
-		"  -p -S -N -z -c -m -M -B -R -F -w -W -U -I -O -T -y -a: accepted, no effect\n"
+		"  -F, --frags          Multi-buffer packets: pcap records longer than a chunk span\n"
+		"                       several chunks (XDP_PKT_CONTD); packets and frags counted\n"
+		"  -p -S -N -z -c -m -M -B -R -w -W -U -I -O -T -y -a: accepted, no effect\n"
 		"  Options (this build):\n"
 		"      --gpu=n          HIP device (default 0)\n"
 		"      --pool=n         Synthetic UMEM pool of n frames\n"
@@ -224,8 +228,13 @@ int main(int argc, char **argv)
 		case 'Q': o.quiet = true; break;
 		case 'p': case 'N': case 'w': case 'O': case 'c': case 'z': case 'm':
 		case 'M': case 'T': case 'y': case 'W': case 'U': case 'a': case 'I':
-		case 'B': case 'R': case 'F':
+		case 'B': case 'R':
 			break;    /* socket / scheduling options: no socket here */
+		case 'F':
+			/* opt_frags (xdpsock.c:1349): multi-buffer packets */
+			o.frags = true;
+			o.cfg_flags |= XDPGPU_CFG_FRAGS;
+			break;
 		case OPT_GPU: o.device = atoi(optarg); break;
 		case OPT_POOL: pool_n = (uint32_t)strtoul(optarg, NULL, 0); break;
 		case OPT_POOL_KIND:
@@ -273,7 +282,7 @@ int main(int argc, char **argv)
 	struct rx_source src;
 	int rc;
 	if (pcap) {
-		rc = rx_source_pcap(&src, pcap, frame_size, 0, unaligned, 0);
+		rc = rx_source_pcap(&src, pcap, frame_size, 0, unaligned, o.frags, 0);
 		if (rc) {
 			fprintf(stderr, "%s: %s: %s\n", prog, pcap, strerror(-rc));
 			return 1;

@@ -12,7 +12,8 @@
  *    outside the UMEM) are finished as ABORTED;
  *  - frag_gather: each complete packet, and the byte after its last
  *    fragment (udp_csum's over-read byte), is copied to a bounce UMEM at a
- *    16-byte aligned offset, one wave per packet with coalesced copies, and
+ *    16-byte aligned offset, one wave per packet with coalesced 16-byte
+ *    copies where the fragments allow them, and
  *    gets a bounce descriptor; the RX kernels then run over the bounce
  *    batch, one frame per packet;
  *  - frag_scatter: the packet's verdict goes to each of its descriptors,
@@ -93,12 +94,36 @@ __device__ void zero_outputs(const FragArgs &a, uint32_t k)
 		a.tup[(uint64_t)k * a.tb + b] = 0;
 }
 
-/* Wave-cooperative copy of n bytes: dwords when source and destination
- * share their alignment mod 4 (256 bytes per step), bytes otherwise. */
+/* Wave-cooperative copy of n bytes: 16-byte vectors, four per lane and
+ * step (4 KiB per wave-step), when source and destination share their
+ * alignment mod 16 (chunk-aligned fragments); dwords when they share it mod
+ * 4; bytes otherwise. */
 __device__ void wave_copy(uint8_t *dst, const uint8_t *src, uint64_t n, int lane)
 {
 	uint64_t o = 0;
-	if (!(((uintptr_t)dst ^ (uintptr_t)src) & 3)) {
+	const uintptr_t mis = (uintptr_t)dst ^ (uintptr_t)src;
+	if (!(mis & 15)) {
+		const uint64_t head = (16 - ((uintptr_t)dst & 15)) & 15;
+		o = head < n ? head : n;
+		if ((uint64_t)lane < o)
+			dst[lane] = src[lane];
+		const uint64_t vecs = (n - o) / 16;
+		uint4 *dv = reinterpret_cast<uint4 *>(dst + o);
+		const uint4 *sv = reinterpret_cast<const uint4 *>(src + o);
+		uint64_t w = lane;
+		for (; w + 3 * kFragWave < vecs; w += 4 * kFragWave) {
+			uint4 t[4];
+#pragma unroll
+			for (int u = 0; u < 4; u++)
+				t[u] = sv[w + u * kFragWave];
+#pragma unroll
+			for (int u = 0; u < 4; u++)
+				dv[w + u * kFragWave] = t[u];
+		}
+		for (; w < vecs; w += kFragWave)
+			dv[w] = sv[w];
+		o += 16 * vecs;
+	} else if (!(mis & 3)) {
 		const uint64_t head = (4 - ((uintptr_t)dst & 3)) & 3;
 		o = head < n ? head : n;
 		if ((uint64_t)lane < o)
@@ -114,20 +139,52 @@ __device__ void wave_copy(uint8_t *dst, const uint8_t *src, uint64_t n, int lane
 		dst[b] = src[b];
 }
 
+/* wave sum and exclusive wave prefix sum of a u64 */
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v)
+{
+#pragma unroll
+	for (int m = kFragWave / 2; m >= 1; m >>= 1) {
+		const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, kFragWave);
+		const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, kFragWave);
+		v += ((uint64_t)hi << 32) | lo;
+	}
+	return v;
+}
+
+__device__ __forceinline__ uint64_t wave_excl_u64(uint64_t v, int lane)
+{
+	uint64_t x = v;
+#pragma unroll
+	for (int d = 1; d < kFragWave; d <<= 1) {
+		const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)x, d, kFragWave);
+		const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)(x >> 32), d, kFragWave);
+		if (lane >= d)
+			x += ((uint64_t)hi << 32) | lo;
+	}
+	return x - v;
+}
+
+/* Grid-stride over the descriptors with wave-uniform trip counts; per
+ * wave one count and one byte total go to the counters (not one atomic per
+ * packet on two words). */
 __global__ __launch_bounds__(kFragBlock) void frag_count_kernel(FragArgs a)
 {
+	const int lane = threadIdx.x & (kFragWave - 1);
 	const uint64_t step = (uint64_t)gridDim.x * kFragBlock;
-	for (uint64_t i = (uint64_t)blockIdx.x * kFragBlock + threadIdx.x; i < a.n;
-	     i += step) {
-		if (!packet_head(a, (uint32_t)i))
-			continue;
-		uint32_t last;
-		uint64_t total;
-		if (packet_walk(a, (uint32_t)i, last, total)) {
-			atomicAdd(&a.fc[0], 1ull);
-			atomicAdd(&a.fc[1], (unsigned long long)bounce_size(total));
-			continue;
+	for (uint64_t b = (uint64_t)blockIdx.x * kFragBlock; b < a.n; b += step) {
+		const uint64_t i = b + threadIdx.x;
+		uint32_t last = 0;
+		uint64_t total = 0;
+		const bool head = i < a.n && packet_head(a, (uint32_t)i);
+		const bool ok = head && packet_walk(a, (uint32_t)i, last, total);
+		const uint64_t okm = __ballot(ok);
+		const uint64_t bytes = wave_sum_u64(ok ? bounce_size(total) : 0);
+		if (okm && lane == 0) {
+			atomicAdd(&a.fc[0], (unsigned long long)__popcll(okm));
+			atomicAdd(&a.fc[1], (unsigned long long)bytes);
 		}
+		if (!head || ok)
+			continue;
 		for (uint32_t k = (uint32_t)i; k <= last; k++) {
 			a.verdict[k] = XDPGPU_ABORTED;
 			zero_outputs(a, k);
@@ -148,18 +205,33 @@ __global__ __launch_bounds__(kFragBlock) void frag_gather_kernel(FragArgs a)
 	for (uint64_t base = w0 * kFragWave; base < a.n; base += nw * kFragWave) {
 		const uint64_t i = base + lane;
 		uint32_t last = 0;
-		uint64_t total = 0, off = 0;
+		uint64_t total = 0;
 		const bool mine = i < a.n && packet_head(a, (uint32_t)i) &&
 				  packet_walk(a, (uint32_t)i, last, total);
+		/* the wave's packets: consecutive packet slots and bounce bytes,
+		 * claimed with one atomic each */
+		const uint64_t mm = __ballot(mine);
+		if (!mm)
+			continue;
+		const uint64_t sz = mine ? bounce_size(total) : 0;
+		const uint64_t pre = wave_excl_u64(sz, lane);
+		const uint64_t wsum = rl64(pre + sz, kFragWave - 1);
+		uint64_t kb = 0, ob = 0;
+		if (lane == 0) {
+			kb = atomicAdd(&a.fc[2], (unsigned long long)__popcll(mm));
+			ob = atomicAdd(&a.fc[3], (unsigned long long)wsum);
+		}
+		kb = rl64(kb, 0);
+		const uint64_t off = rl64(ob, 0) + pre;
 		if (mine) {
-			const uint32_t k = (uint32_t)atomicAdd(&a.fc[2], 1ull);
-			off = atomicAdd(&a.fc[3], (unsigned long long)bounce_size(total));
+			const uint32_t k = (uint32_t)kb + __builtin_amdgcn_mbcnt_hi(
+				(uint32_t)(mm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0));
 			*reinterpret_cast<uint4 *>(a.bdesc + k) =
 				make_uint4((uint32_t)off, (uint32_t)(off >> 32), (uint32_t)total, 0u);
 			a.bmap[k] = make_uint2((uint32_t)i, last - (uint32_t)i + 1);
 		}
 		/* the wave copies its packets one after the other */
-		for (uint64_t m = __ballot(mine); m; m &= m - 1) {
+		for (uint64_t m = mm; m; m &= m - 1) {
 			const int src = __builtin_ctzll(m);
 			const uint32_t first = rl32((uint32_t)i, src), lst = rl32(last, src);
 			uint8_t *dst = a.bounce + rl64(off, src);

@@ -71,6 +71,43 @@ def chunked(frames, chunk=4096):
     return umem, descs
 
 
+def jumbo_frames(seed, n=120):
+    """IPv4/IPv6 UDP/TCP frames of 60..8000 bytes (1 in 10 with a bad L4
+    checksum): the records of a --frags pcap."""
+    import frames as F
+    rng = np.random.default_rng(seed)
+    out = []
+    for k in range(n):
+        pay = rng.integers(0, 256, int(rng.integers(10, 7900)), dtype=np.uint8).tobytes()
+        if k % 3 == 2:
+            fr = F.v6_frame(17, F.udp(1000 + k, 53, pay))
+        elif k % 3 == 1:
+            fr = F.v4_frame(6, F.tcp(1000 + k, 80, pay))
+        else:
+            fr = F.v4_frame(17, F.udp(1000 + k, 53, pay))
+        if k % 10 == 9:
+            b = bytearray(fr)
+            b[-1] ^= 0x5A
+            fr = bytes(b)
+        out.append(fr)
+    return out
+
+
+def chunked_frags(frames, chunk):
+    """The UMEM xdpsock-gpu --frags builds from a pcap: each record over as
+    many chunks as it needs, XDP_PKT_CONTD on all but the last."""
+    nd = []
+    for fr in frames:
+        for o in range(0, len(fr), chunk):
+            nd.append((len(nd) * chunk, fr[o:o + chunk], o + chunk < len(fr)))
+    umem = np.zeros(len(nd) * chunk + 64, np.uint8)
+    descs = np.zeros(len(nd), xdpgpu.DESC_DTYPE)
+    for k, (off, piece, more) in enumerate(nd):
+        umem[off:off + len(piece)] = np.frombuffer(piece, np.uint8)
+        descs[k] = (off, len(piece), xdpgpu.PKT_CONTD if more else 0)
+    return umem, descs
+
+
 # ------------------------------------------------------------------ CPU tests
 def test_option_errors():
     assert run(XDPSOCK).returncode == 2                         # no source
@@ -123,6 +160,22 @@ def test_pcap_source(tmp_path, golden, big_endian, nsec):
     r = run(XDPSOCK, "--pcap", p, "-u", "--dry-run")
     packed = sum((len(f) + 63) & ~63 for f in frames)
     assert f"UMEM {packed} bytes, chunk 0" in r.stdout and "unaligned" in r.stdout
+
+
+def test_pcap_frags_source(tmp_path):
+    """-F: records longer than a chunk span several chunks."""
+    frames = jumbo_frames(1)
+    p = str(tmp_path / "j.pcap")
+    write_pcap(p, frames)
+    _, descs = chunked_frags(frames, 2048)
+    r = run(XDPSOCK, "--pcap", p, "-f", "2048", "-F", "--dry-run")
+    assert r.returncode == 0, r.stderr
+    total = sum(len(f) for f in frames)
+    assert f"{len(descs)} frames, {total} bytes" in r.stdout
+    assert f"{len(frames)} packets" in r.stdout and "skipped" not in r.stdout
+    r = run(XDPSOCK, "--pcap", p, "-f", "2048", "--dry-run")
+    big = sum(1 for f in frames if len(f) > 2048)
+    assert f"{big} records skipped" in r.stdout
 
 
 def test_pcap_rejects(tmp_path):
@@ -246,6 +299,41 @@ def test_af_xdp_user_pool_stats():
                                           ppm_echo6=200000)
     ov, _, _, _ = oracle.process(umem, descs, 0x6, 0, 0)
     assert js["tx_pkts"] == int((ov == xdpgpu.TX).sum()) > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,batch", [("-r", 64), ("-l", 7)])
+def test_xdpsock_frags_pcap(tmp_path, mode, batch):
+    """--frags: every descriptor's verdict is its packet's (the oracle over
+    the same chunk layout), packets and fragments are counted apart, l2fwd
+    swaps the MACs of a packet's first fragment only, and batches release
+    whole packets (-b 7 cuts many packets)."""
+    frames = jumbo_frames(2)
+    p, out, vf = str(tmp_path / "j.pcap"), str(tmp_path / "o.pcap"), str(tmp_path / "v.bin")
+    write_pcap(p, frames)
+    r = run(XDPSOCK, mode, "-F", "--pcap", p, "-f", "2048", "-b", str(batch), "--verdicts", vf,
+            "--tx-pcap", out, "--json", "-x", "-Q")
+    assert r.returncode == 0, r.stderr
+    umem, descs = chunked_frags(frames, 2048)
+    ov, _, _, ost = oracle.process(umem, descs, 0x5 | xdpgpu.CFG_FRAGS, 0, 0)
+    np.testing.assert_array_equal(np.fromfile(vf, np.uint8), ov)
+    js = json.loads(r.stdout.strip().splitlines()[-1])
+    assert js["rx_pkts"] == len(frames) and js["rx_frags"] == len(descs)
+    assert [js["verdict"][k] for k in ("ABORTED", "DROP", "PASS", "TX", "REDIRECT")] == \
+        ost["verdict"]
+    assert ost["verdict"][xdpgpu.DROP] > 0 and ost["verdict"][xdpgpu.REDIRECT] > 0
+    if mode == "-l":
+        first = np.ones(len(descs), bool)
+        first[1:] = (descs["options"][:-1] & xdpgpu.PKT_CONTD) == 0
+        want = []
+        for k, d in enumerate(descs):
+            if ov[k] != xdpgpu.REDIRECT:
+                continue
+            b = umem[int(d["addr"]):int(d["addr"]) + int(d["len"])].tobytes()
+            want.append(b[6:12] + b[0:6] + b[12:] if first[k] else b)
+        assert read_pcap(out) == want
+        assert js["tx_pkts"] == int(((ov == xdpgpu.REDIRECT) &
+                                     ((descs["options"] & xdpgpu.PKT_CONTD) == 0)).sum())
 
 
 def read_pcap(path):
