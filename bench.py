@@ -211,6 +211,42 @@ def nat64_run(dev, stream, n, steps, local):
     return out
 
 
+def frags_run(dev, stream, n, steps, local, size=9000, chunk=4096):
+    """Multi-buffer packets (XDPGPU_CFG_FRAGS): n jumbo frames, each cut in
+    place into fragments of at most `chunk` bytes (XDP_PKT_CONTD on all but
+    the last).  Times the whole launch (count, RX kernels over the gathered
+    packets, scatter) and checks every fragment's verdict against the
+    generator's verdict for its frame."""
+    u, d, ex = xdpgpu.pool_generate(n, xdpgpu.POOL_UDP4, size, 0x5EED0022)
+    lens = d["len"].astype(np.int64)
+    nf = (lens + chunk - 1) // chunk
+    frame_of = np.repeat(np.arange(n), nf)
+    k = np.arange(len(frame_of)) - np.repeat(np.cumsum(nf) - nf, nf)
+    fd = np.zeros(len(frame_of), xdpgpu.DESC_DTYPE)
+    fd["addr"] = d["addr"][frame_of] + k * chunk
+    fd["len"] = np.minimum(lens[frame_of] - k * chunk, chunk)
+    fd["options"] = np.where(k < nf[frame_of] - 1, xdpgpu.PKT_CONTD, 0)
+    m = len(fd)
+    g_umem = to_dev(u, dev)
+    g_desc = to_dev(fd, dev, 0)
+    g_v = torch.empty(m, dtype=torch.uint8, device=dev)
+    g_res = torch.empty(m * 16, dtype=torch.uint8, device=dev)
+    g_tup = torch.empty(m * 16, dtype=torch.uint8, device=dev)
+    with xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT | xdpgpu.CFG_FRAGS, 0, xdpgpu.TUPLE_V4,
+                       64) as g:
+        w = time_device(g, g_umem, u.nbytes, g_desc, m, g_v, g_res, g_tup, stream, steps, 2, 1)
+    ok = bool(np.array_equal(g_v.cpu().numpy(), ex[frame_of]))
+    t = w / steps
+    out = {"workload": f"{n} x {size}B IPv4/UDP packets in {chunk}B fragments "
+                       f"({m} descriptors), XDPGPU_CFG_FRAGS",
+           "packets": n, "descriptors": m, "mpps": round(n / t / 1e6, 1),
+           "ms_per_launch": round(t * 1e3, 4),
+           "packet_gbps": round(float(lens.sum()) / t / 1e9, 1), "verdicts_ok": ok}
+    del g_umem, g_desc, g_v, g_res, g_tup
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -221,8 +257,8 @@ def main():
     ap.add_argument("--window", type=int, default=64)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
-    ap.add_argument("--legs", default="1500,imix,nat64",
-                    help="secondary workloads: comma list of 1500, imix, nat64")
+    ap.add_argument("--legs", default="1500,imix,nat64,frags",
+                    help="secondary workloads: comma list of 1500, imix, nat64, frags")
     ap.add_argument("--imix-frames", type=int, default=16 << 20)
     ap.add_argument("--nat64-frames", type=int, default=16 << 20)
     ap.add_argument("--e2e", action="store_true", help="also time the host path")
@@ -296,6 +332,8 @@ def main():
         if "nat64" in legs:
             secondary["config4_nat64"] = nat64_run(dev, stream, args.nat64_frames, steps2,
                                                    local)
+        if "frags" in legs:
+            secondary["multibuffer_9000B"] = frags_run(dev, stream, 1 << 16, steps2, local)
 
     e2e = None
     if args.e2e and rank == 0 and world == 1:

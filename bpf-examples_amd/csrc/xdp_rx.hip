@@ -1186,7 +1186,7 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
  * payload sum here and go to the bulk list; every other frame is deferred
  * to the exception kernel.
  */
-template <int MINW>
+template <int MINW, bool FRAGS>
 __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 {
 	constexpr int XQ = 2 * kWave;      /* deferral queues per wave */
@@ -1292,10 +1292,11 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 	for (; t < ntiles; t += nwaves) {
 		const uint64_t i = t * kWave + lane;
 		const uint4 dv = dcur;
-		/* multi-buffer mode: the descriptors of packets of several
+		/* multi-buffer mode (a variant of its own, so that the plain
+		 * kernel is untouched): the descriptors of packets of several
 		 * fragments are the fragment kernels' (frags.hip) */
 		bool skip = false;
-		if (a.frags) {
+		if constexpr (FRAGS) {
 			const uint32_t contd = dv.w & XDPGPU_PKT_CONTD;
 			uint32_t prev = (uint32_t)__shfl_up((int)contd, 1, kWave);
 			if (lane == 0)
@@ -1653,7 +1654,7 @@ static hipError_t launch_sized(RxArgs a, uint32_t max_blocks,
 			       hipStream_t stream, uint32_t bulk_variant,
 			       hipEvent_t *ev)
 {
-	uint32_t cap = resident_blocks<xdp_rx_kernel<MINW>>();
+	uint32_t cap = resident_blocks<xdp_rx_kernel<MINW, false>>();
 	if (cap < max_blocks)
 		max_blocks = cap;
 	const uint32_t blocks = rx_grid_blocks(a.n, max_blocks);
@@ -1661,8 +1662,12 @@ static hipError_t launch_sized(RxArgs a, uint32_t max_blocks,
 	a.nregions = blocks * kWavesPerBlock;
 	if (ev)
 		(void)hipEventRecord(ev[0], stream);
-	hipLaunchKernelGGL((xdp_rx_kernel<MINW>), dim3(blocks),
-			   dim3(kBlock), 0, stream, a);
+	if (a.frags)
+		hipLaunchKernelGGL((xdp_rx_kernel<MINW, true>), dim3(blocks),
+				   dim3(kBlock), 0, stream, a);
+	else
+		hipLaunchKernelGGL((xdp_rx_kernel<MINW, false>), dim3(blocks),
+				   dim3(kBlock), 0, stream, a);
 	hipError_t e = hipGetLastError();
 	if (e != hipSuccess)
 		return e;
