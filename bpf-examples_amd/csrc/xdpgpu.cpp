@@ -843,4 +843,18 @@ int xdpgpu_ip_fast_csum_dev(xdpgpu_ctx *ctx, const void *d_hdrs,
 	return 0;
 }
 
+int xdpgpu_hints_dev(xdpgpu_ctx *ctx, const void *d_umem, uint64_t umem_size,
+		     const xdpgpu_desc *d_descs, uint32_t n, uint32_t rx_time_btf_id,
+		     uint32_t mark_btf_id, xdpgpu_hints *d_out, void *stream)
+{
+	if (!ctx || (n && (!d_umem || !d_descs || !d_out)))
+		return -EINVAL;
+	if (n == 0)
+		return 0;
+	hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
+	HIP_TRY(ctx, launch_hints((const uint8_t *)d_umem, umem_size, d_descs, n,
+				  rx_time_btf_id, mark_btf_id, d_out, st));
+	return 0;
+}
+
 } // extern "C"

@@ -143,6 +143,9 @@ hipError_t launch_nat64(const Nat64Args &a, uint32_t max_blocks,
 			hipStream_t stream);
 uint32_t nat64_slot_hash(uint32_t a, uint32_t b, uint32_t c, uint32_t d);
 
+hipError_t launch_hints(const uint8_t *umem, uint64_t usize,
+			const xdpgpu_desc *desc, uint32_t n, uint32_t rx_time_id,
+			uint32_t mark_id, xdpgpu_hints *out, hipStream_t stream);
 hipError_t launch_jhash(const uint8_t *keys, uint32_t key_len,
 			uint32_t stride, uint32_t n, uint32_t initval,
 			uint32_t *out, hipStream_t stream);

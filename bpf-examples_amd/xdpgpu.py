@@ -144,8 +144,11 @@ EXPORTS = (
     "xdpgpu_nat64_setup", "xdpgpu_nat64_dev", "xdpgpu_nat64_pool_config",
     "xdpgpu_device_count", "xdpgpu_last_error",
     "xdpgpu_abi_version", "xdpgpu_pool_size", "xdpgpu_pool_generate",
-    "xdpgpu_pool_spec_default",
+    "xdpgpu_pool_spec_default", "xdpgpu_hints_dev",
 )
+
+# struct xdpgpu_hints (XDP hints in front of a frame)
+HINTS_DTYPE = np.dtype([("rx_ktime", "<u8"), ("value", "<u4"), ("btf_id", "<u4")])
 
 
 def load_library(path: str = LIB_PATH) -> C.CDLL:
@@ -170,6 +173,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.xdpgpu_stats_reset.argtypes = [vp]
     lib.xdpgpu_jhash_dev.argtypes = [vp, vp, u32, u32, u32, u32, vp, vp]
     lib.xdpgpu_ip_fast_csum_dev.argtypes = [vp, vp, u32, u32, vp, vp]
+    lib.xdpgpu_hints_dev.argtypes = [vp, vp, u64, vp, u32, u32, u32, vp, vp]
     lib.xdpgpu_sync.argtypes = [vp, vp]
     lib.xdpgpu_ceiling_dev.argtypes = [vp, vp, u64, vp, u32, vp, vp, vp, vp]
     lib.xdpgpu_kernel_times.argtypes = [vp, C.POINTER(KTimes)]
@@ -330,6 +334,13 @@ class XdpGpu:
         self._check(self.lib.xdpgpu_ip_fast_csum_dev(
             self.h, _ptr(hdrs), stride, n, _ptr(out), _stream_handle(stream)),
             "xdpgpu_ip_fast_csum_dev")
+
+    def hints_dev(self, umem, umem_size: int, descs, n: int, rx_time_btf_id: int,
+                  mark_btf_id: int, out, stream=None) -> None:
+        """XDP hints in front of each frame into out (HINTS_DTYPE[n])."""
+        self._check(self.lib.xdpgpu_hints_dev(
+            self.h, _ptr(umem), umem_size, _ptr(descs), n, rx_time_btf_id,
+            mark_btf_id, _ptr(out), _stream_handle(stream)), "xdpgpu_hints_dev")
 
     def sync(self, stream=None) -> None:
         self._check(self.lib.xdpgpu_sync(self.h, _stream_handle(stream)),

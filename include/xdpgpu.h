@@ -215,6 +215,26 @@ int xdpgpu_ip_fast_csum_dev(struct xdpgpu_ctx *ctx, const void *d_hdrs,
 			    uint32_t hdr_stride, uint32_t n, uint16_t *d_out,
 			    void *stream);
 
+/* XDP hints (AF_XDP-interaction/af_xdp_kern.c:42-105): the metadata an XDP
+ * program writes in front of a frame (bpf_xdp_adjust_meta), the struct's
+ * BTF id in its last 4 bytes, read per frame as print_meta_info_via_btf
+ * does (af_xdp_user.c:813-829, xsk_umem__btf_id lib_xsk_extend.c:16-27):
+ * btf_id = the u32 before the frame; rx_time_btf_id selects struct
+ * xdp_hints_rx_time {u64 rx_ktime; u32 xdp_rx_cpu; u32 btf_id} (packed, 16
+ * bytes), mark_btf_id struct xdp_hints_mark {u32 mark; u32 btf_id}.  Ids
+ * of 0 never match.  A frame with fewer bytes in front of it than its
+ * struct, or outside the UMEM, reads as no hints (all zero). */
+struct xdpgpu_hints {
+	uint64_t rx_ktime;   /* xdp_hints_rx_time.rx_ktime, else 0        */
+	uint32_t value;      /* xdp_rx_cpu (rx_time) or mark (mark), else 0 */
+	uint32_t btf_id;     /* the id in front of the frame (0: none)     */
+};
+
+int xdpgpu_hints_dev(struct xdpgpu_ctx *ctx, const void *d_umem,
+		     uint64_t umem_size, const struct xdpgpu_desc *d_descs,
+		     uint32_t n, uint32_t rx_time_btf_id, uint32_t mark_btf_id,
+		     struct xdpgpu_hints *d_out, void *stream);
+
 /* Diagnostic: the RX kernel's memory traffic (descriptor, 64-byte header
  * window, 16 B result + 16 B tuple + verdict stores) with no parse, to
  * measure the achievable bandwidth ceiling of that access pattern.  Outputs

@@ -44,6 +44,10 @@ int oracle_process(uint8_t *umem, uint64_t umem_size,
 
 /* nat64 (nat64_oracle.c): same inputs and outputs as xdpgpu_nat64_dev;
  * umem is translated in place. */
+/* XDP hints in front of each frame (xdpgpu_hints_dev semantics) */
+void oracle_hints(const uint8_t *umem, uint64_t umem_size,
+		  const struct xdpgpu_desc *descs, uint32_t n, uint32_t rx_time_id,
+		  uint32_t mark_id, struct xdpgpu_hints *out);
 int oracle_nat64(uint8_t *umem, uint64_t umem_size,
 		 const struct xdpgpu_desc *descs, uint32_t n,
 		 const struct xdpgpu_nat64_cfg *cfg,

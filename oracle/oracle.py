@@ -89,6 +89,7 @@ def lib() -> C.CDLL:
         o.oracle_bench.restype = C.c_double
         o.oracle_nat64.argtypes = [vp, u64, vp, u32, C.POINTER(Nat64Cfg), vp, u32,
                                    vp, vp]
+        o.oracle_hints.argtypes = [vp, u64, vp, u32, u32, u32, vp]
         o.oracle_v4addr_to_v6.argtypes = [vp, vp, vp, C.c_int]
         o.oracle_v6addr_to_v4.argtypes = [vp, C.c_int, vp, vp]
         del u8p
@@ -192,6 +193,16 @@ def nat64(umem: np.ndarray, descs: np.ndarray, cfg: "Nat64Cfg", smap: np.ndarray
                    smap.ctypes.data if len(smap) else None, len(smap),
                    action.ctypes.data, out.ctypes.data)
     return action, out
+
+
+def hints(umem: np.ndarray, descs: np.ndarray, rx_time_id: int, mark_id: int):
+    """XDP hints in front of each frame (xdpgpu_hints_dev semantics)."""
+    import xdpgpu
+    descs = np.ascontiguousarray(descs, DESC_DTYPE)
+    out = np.zeros(len(descs), xdpgpu.HINTS_DTYPE)
+    lib().oracle_hints(umem.ctypes.data, umem.nbytes, descs.ctypes.data, len(descs),
+                       rx_time_id, mark_id, out.ctypes.data)
+    return out
 
 
 def v4addr_to_v6(a4: bytes, pref: bytes, plen: int):

@@ -841,6 +841,35 @@ int oracle_process(uint8_t *umem, uint64_t umem_size,
 	return 0;
 }
 
+/* XDP hints (af_xdp_user.c:813-829): the u32 before the frame is the BTF id
+ * (xsk_umem__btf_id, lib_xsk_extend.c:16-27); a known id selects the struct
+ * that ends at the frame (af_xdp_kern.c:42-51), read at its negative
+ * offsets (xsk_btf__read, lib_xsk_extend.c:123-141). */
+void oracle_hints(const uint8_t *umem, uint64_t umem_size,
+		  const struct xdpgpu_desc *descs, uint32_t n, uint32_t rx_time_id,
+		  uint32_t mark_id, struct xdpgpu_hints *out)
+{
+	uint32_t i;
+
+	for (i = 0; i < n; i++) {
+		const uint64_t eff = (descs[i].addr & ((1ull << 48) - 1)) +
+				     (descs[i].addr >> 48);
+		const uint8_t *p = umem + eff;
+
+		memset(&out[i], 0, sizeof(out[i]));
+		if (eff < 4 || eff > umem_size)
+			continue;
+		out[i].btf_id = ld_le32(p - 4);
+		if (out[i].btf_id && out[i].btf_id == rx_time_id && eff >= 16) {
+			out[i].rx_ktime = (uint64_t)ld_le32(p - 16) |
+					  ((uint64_t)ld_le32(p - 12) << 32);
+			out[i].value = ld_le32(p - 8);
+		} else if (out[i].btf_id && out[i].btf_id == mark_id && eff >= 8) {
+			out[i].value = ld_le32(p - 8);
+		}
+	}
+}
+
 /* ------------------------------------------------------------------ */
 /* CPU baseline harness                                                */
 
