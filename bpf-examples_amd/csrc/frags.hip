@@ -7,8 +7,9 @@
  * place: its bytes are spread over UMEM chunks.  The RX fast kernel skips
  * its descriptors, and these kernels handle it as one frame:
  *  - frag_count: the packets' first descriptors (lane per descriptor) walk
- *    their fragments; complete packets are counted with the bounce bytes
- *    they need, the others (the batch ends inside them, or a fragment lies
+ *    their fragments; complete packets are counted per block with the
+ *    bounce bytes they need (frag_scan turns the block totals into
+ *    prefixes), the others (the batch ends inside them, or a fragment lies
  *    outside the UMEM) are finished as ABORTED;
  *  - frag_gather: each complete packet, and the byte after its last
  *    fragment (udp_csum's over-read byte), is copied to a bounce UMEM at a
@@ -34,6 +35,7 @@ namespace {
 constexpr int kFragWave = 64;
 constexpr int kFragBlock = 256;
 constexpr uint64_t kFragMaxBlocks = 4096;
+constexpr int kFragScan = 1024;          /* count / gather grid at most */
 
 __device__ __forceinline__ uint64_t frag_eff(const xdpgpu_desc &d)
 {
@@ -164,27 +166,32 @@ __device__ __forceinline__ uint64_t wave_excl_u64(uint64_t v, int lane)
 	return x - v;
 }
 
-/* Grid-stride over the descriptors with wave-uniform trip counts; per
- * wave one count and one byte total go to the counters (not one atomic per
- * packet on two words). */
+/* Count and gather walk the descriptors in the same order: frag_grid(n)
+ * blocks, block-strided 256 descriptors at a time.  Count leaves each
+ * block's packets and bounce bytes in blk[]; one block turns them into
+ * exclusive prefixes; gather places a block's packets from its prefix on,
+ * in descriptor order.  No atomics on shared words (a returning device
+ * atomic on one word serialises at ~80 per microsecond), and the bounce
+ * layout is deterministic. */
 __global__ __launch_bounds__(kFragBlock) void frag_count_kernel(FragArgs a)
 {
-	const int lane = threadIdx.x & (kFragWave - 1);
+	__shared__ unsigned long long part[2][kFragBlock / kFragWave];
+	const int lane = threadIdx.x & (kFragWave - 1), wid = threadIdx.x / kFragWave;
 	const uint64_t step = (uint64_t)gridDim.x * kFragBlock;
+	uint64_t cnt = 0, bytes = 0;    /* this lane's complete packets */
 	for (uint64_t b = (uint64_t)blockIdx.x * kFragBlock; b < a.n; b += step) {
 		const uint64_t i = b + threadIdx.x;
 		uint32_t last = 0;
 		uint64_t total = 0;
 		const bool head = i < a.n && packet_head(a, (uint32_t)i);
 		const bool ok = head && packet_walk(a, (uint32_t)i, last, total);
-		const uint64_t okm = __ballot(ok);
-		const uint64_t bytes = wave_sum_u64(ok ? bounce_size(total) : 0);
-		if (okm && lane == 0) {
-			atomicAdd(&a.fc[0], (unsigned long long)__popcll(okm));
-			atomicAdd(&a.fc[1], (unsigned long long)bytes);
+		if (ok) {
+			cnt++;
+			bytes += bounce_size(total);
 		}
 		if (!head || ok)
 			continue;
+		/* broken packet: ABORTED here, one frame in the counters */
 		for (uint32_t k = (uint32_t)i; k <= last; k++) {
 			a.verdict[k] = XDPGPU_ABORTED;
 			zero_outputs(a, k);
@@ -195,36 +202,88 @@ __global__ __launch_bounds__(kFragBlock) void frag_count_kernel(FragArgs a)
 			atomicAdd(&a.stats[CNT_VERDICT0 + XDPGPU_ABORTED], 1ull);
 		}
 	}
+	cnt = wave_sum_u64(cnt);
+	bytes = wave_sum_u64(bytes);
+	if (lane == 0) {
+		part[0][wid] = cnt;
+		part[1][wid] = bytes;
+	}
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		unsigned long long c = 0, y = 0;
+		for (int w = 0; w < kFragBlock / kFragWave; w++) {
+			c += part[0][w];
+			y += part[1][w];
+		}
+		a.blk[2 * blockIdx.x] = c;
+		a.blk[2 * blockIdx.x + 1] = y;
+	}
+}
+
+/* one block: exclusive prefixes of the g block totals; the grand totals
+ * to fc[0] (packets) and fc[1] (bounce bytes) */
+__global__ __launch_bounds__(kFragScan) void frag_scan_kernel(FragArgs a, uint32_t g)
+{
+	__shared__ unsigned long long sc[2][kFragScan];
+	const uint32_t t = threadIdx.x;
+	const unsigned long long c = t < g ? a.blk[2 * t] : 0, y = t < g ? a.blk[2 * t + 1] : 0;
+	sc[0][t] = c;
+	sc[1][t] = y;
+	__syncthreads();
+	for (uint32_t d = 1; d < kFragScan; d <<= 1) {
+		const unsigned long long c2 = t >= d ? sc[0][t - d] : 0;
+		const unsigned long long y2 = t >= d ? sc[1][t - d] : 0;
+		__syncthreads();
+		sc[0][t] += c2;
+		sc[1][t] += y2;
+		__syncthreads();
+	}
+	if (t < g) {
+		a.blk[2 * t] = sc[0][t] - c;
+		a.blk[2 * t + 1] = sc[1][t] - y;
+	}
+	if (t == kFragScan - 1) {
+		a.fc[0] = sc[0][t];
+		a.fc[1] = sc[1][t];
+	}
 }
 
 __global__ __launch_bounds__(kFragBlock) void frag_gather_kernel(FragArgs a)
 {
-	const int lane = threadIdx.x & (kFragWave - 1);
-	const uint64_t w0 = ((uint64_t)blockIdx.x * kFragBlock + threadIdx.x) / kFragWave;
-	const uint64_t nw = (uint64_t)gridDim.x * (kFragBlock / kFragWave);
-	for (uint64_t base = w0 * kFragWave; base < a.n; base += nw * kFragWave) {
-		const uint64_t i = base + lane;
+	__shared__ unsigned long long wpart[2][kFragBlock / kFragWave];
+	const int lane = threadIdx.x & (kFragWave - 1), wid = threadIdx.x / kFragWave;
+	const uint64_t step = (uint64_t)gridDim.x * kFragBlock;
+	/* where this block's next packet goes */
+	uint64_t kbase = a.blk[2 * blockIdx.x], obase = a.blk[2 * blockIdx.x + 1];
+	for (uint64_t b = (uint64_t)blockIdx.x * kFragBlock; b < a.n; b += step) {
+		const uint64_t i = b + threadIdx.x;
 		uint32_t last = 0;
 		uint64_t total = 0;
 		const bool mine = i < a.n && packet_head(a, (uint32_t)i) &&
 				  packet_walk(a, (uint32_t)i, last, total);
-		/* the wave's packets: consecutive packet slots and bounce bytes,
-		 * claimed with one atomic each */
 		const uint64_t mm = __ballot(mine);
-		if (!mm)
-			continue;
 		const uint64_t sz = mine ? bounce_size(total) : 0;
 		const uint64_t pre = wave_excl_u64(sz, lane);
-		const uint64_t wsum = rl64(pre + sz, kFragWave - 1);
-		uint64_t kb = 0, ob = 0;
-		if (lane == 0) {
-			kb = atomicAdd(&a.fc[2], (unsigned long long)__popcll(mm));
-			ob = atomicAdd(&a.fc[3], (unsigned long long)wsum);
+		if (lane == kFragWave - 1) {
+			wpart[0][wid] = (unsigned long long)__popcll(mm);
+			wpart[1][wid] = pre + sz;
 		}
-		kb = rl64(kb, 0);
-		const uint64_t off = rl64(ob, 0) + pre;
+		__syncthreads();
+		uint64_t kw = kbase, ow = obase, kt = 0, ot = 0;
+		for (int w = 0; w < kFragBlock / kFragWave; w++) {
+			if (w < wid) {
+				kw += wpart[0][w];
+				ow += wpart[1][w];
+			}
+			kt += wpart[0][w];
+			ot += wpart[1][w];
+		}
+		__syncthreads();
+		kbase += kt;
+		obase += ot;
+		const uint64_t off = ow + pre;
 		if (mine) {
-			const uint32_t k = (uint32_t)kb + __builtin_amdgcn_mbcnt_hi(
+			const uint32_t k = (uint32_t)kw + __builtin_amdgcn_mbcnt_hi(
 				(uint32_t)(mm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0));
 			*reinterpret_cast<uint4 *>(a.bdesc + k) =
 				make_uint4((uint32_t)off, (uint32_t)(off >> 32), (uint32_t)total, 0u);
@@ -283,11 +342,11 @@ __global__ __launch_bounds__(kFragBlock) void frag_scatter_kernel(FragArgs a)
 	}
 }
 
-uint32_t frag_blocks(uint64_t items)
+uint32_t frag_blocks(uint64_t items, uint64_t cap)
 {
 	uint64_t b = (items + kFragBlock - 1) / kFragBlock;
-	if (b > kFragMaxBlocks)
-		b = kFragMaxBlocks;
+	if (b > cap)
+		b = cap;
 	return b ? (uint32_t)b : 1u;
 }
 
@@ -295,22 +354,23 @@ uint32_t frag_blocks(uint64_t items)
 
 hipError_t launch_frag_count(const FragArgs &a, hipStream_t stream)
 {
-	hipLaunchKernelGGL(frag_count_kernel, dim3(frag_blocks(a.n)), dim3(kFragBlock),
-			   0, stream, a);
+	const uint32_t g = frag_blocks(a.n, kFragScan);
+	hipLaunchKernelGGL(frag_count_kernel, dim3(g), dim3(kFragBlock), 0, stream, a);
+	hipLaunchKernelGGL(frag_scan_kernel, dim3(1), dim3(kFragScan), 0, stream, a, g);
 	return hipGetLastError();
 }
 
 hipError_t launch_frag_gather(const FragArgs &a, hipStream_t stream)
 {
-	hipLaunchKernelGGL(frag_gather_kernel, dim3(frag_blocks(a.n)), dim3(kFragBlock),
-			   0, stream, a);
+	hipLaunchKernelGGL(frag_gather_kernel, dim3(frag_blocks(a.n, kFragScan)),
+			   dim3(kFragBlock), 0, stream, a);
 	return hipGetLastError();
 }
 
 hipError_t launch_frag_scatter(const FragArgs &a, hipStream_t stream)
 {
-	hipLaunchKernelGGL(frag_scatter_kernel, dim3(frag_blocks(a.m)), dim3(kFragBlock),
-			   0, stream, a);
+	hipLaunchKernelGGL(frag_scatter_kernel, dim3(frag_blocks(a.m, kFragMaxBlocks)),
+			   dim3(kFragBlock), 0, stream, a);
 	return hipGetLastError();
 }
 

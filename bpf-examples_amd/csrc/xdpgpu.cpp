@@ -44,7 +44,8 @@ struct Slot {
 	uint64_t xcap = 0;
 	uint32_t *d_xcount = nullptr;
 	/* multi-buffer packets (XDPGPU_CFG_FRAGS) */
-	unsigned long long *d_fc = nullptr;   /* fragment kernels' counters */
+	unsigned long long *d_fc = nullptr;   /* fragment kernels' counters:
+					       * 2 totals, then 2 per block */
 	unsigned long long *h_fc = nullptr;   /* pinned host copy           */
 	uint8_t *d_bounce = nullptr;          /* bounce UMEM                */
 	uint64_t bounce_cap = 0;
@@ -343,7 +344,8 @@ static int ensure_xlist(xdpgpu_ctx *ctx, Slot &s, uint32_t n)
  * Called with the slot's stream idle. */
 static int ensure_frag_bufs(xdpgpu_ctx *ctx, Slot &s, uint64_t m, uint64_t bytes)
 {
-	if (!s.d_fc && (hipMalloc(&s.d_fc, 4 * sizeof(unsigned long long)) != hipSuccess ||
+	if (!s.d_fc && (hipMalloc(&s.d_fc, (2 + 2 * 1024) * sizeof(unsigned long long)) !=
+				hipSuccess ||
 			hipHostMalloc((void **)&s.h_fc, 4 * sizeof(unsigned long long), 0) !=
 				hipSuccess))
 		return set_err(ctx, -ENOMEM, "fragment counters");
@@ -433,7 +435,7 @@ static int enqueue_rx(xdpgpu_ctx *ctx, Slot &s, uint8_t *d_umem, uint64_t usize,
 		f.tb = d_tup ? tuple_bytes(ctx->cfg.tuple_fmt) : 0;
 		f.stats = a.stats;
 		f.fc = s.d_fc;
-		HIP_TRY(ctx, hipMemsetAsync(s.d_fc, 0, 4 * sizeof(unsigned long long), stream));
+		f.blk = s.d_fc + 2;
 		HIP_TRY(ctx, launch_frag_count(f, stream));
 		HIP_TRY(ctx, hipMemcpyAsync(s.h_fc, s.d_fc, 2 * sizeof(unsigned long long),
 					    hipMemcpyDeviceToHost, stream));

@@ -77,8 +77,9 @@ struct FragArgs {
 	uint8_t *tup;              /* nullable */
 	uint32_t tb;               /* tuple bytes, 0 without tuples         */
 	unsigned long long *stats; /* block 0's counter slot, or null       */
-	unsigned long long *fc;    /* [0] packets, [1] bounce bytes (count);
-				    * [2], [3] the gather's cursors         */
+	unsigned long long *fc;    /* [0] packets, [1] bounce bytes         */
+	unsigned long long *blk;   /* per count/gather block: packets and
+				    * bounce bytes, then their prefixes     */
 	uint8_t *bounce;           /* gather, scatter */
 	xdpgpu_desc *bdesc;        /* one per packet  */
 	uint2 *bmap;               /* first descriptor, descriptors         */
