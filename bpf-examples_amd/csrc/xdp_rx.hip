@@ -1519,8 +1519,11 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_bulk_kernel(RxArgs a)
 
 /* Exception kernel: the generic pipeline on the frames the fast kernel
  * deferred, one wave per fast-kernel wave region, 64 frames per batch. */
+/* held to 96 VGPRs (5 waves/SIMD, a few spilled registers): the kernel is
+ * latency-bound, and on IMIX it ran 0.30-0.31 ms against 0.34-0.36 ms at
+ * the compiler's 3 waves (same process, tools/tune_rx.py) */
 template <int WIN>
-__global__ __launch_bounds__(kBlock) void xdp_rx_generic_kernel(RxArgs a)
+__global__ __launch_bounds__(kBlock, 5) void xdp_rx_generic_kernel(RxArgs a)
 {
 	constexpr int SDW = WIN / 4 + 1;
 	__shared__ uint32_t lds[kWavesPerBlock * kWave * SDW + 8];
