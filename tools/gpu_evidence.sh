@@ -31,6 +31,8 @@ prof config2 python3 bench.py --no-cpu --no-secondary --steps 20
 prof 1500 python3 tools/tune_rx.py --variants 64:0 --rounds 3 --frames 2097152 --size 1500
 prof imix python3 tools/tune_rx.py --variants 64:0 --rounds 3 --kind 1 --seed 0x5EED0003
 prof nat64 python3 tools/nat64_probe.py --reps 5
+prof nat64_egress python3 tools/nat64_probe.py --reps 5 --direction 1
+prof frags python3 tools/frags_probe.py --reps 5
 step pmc 900 env DEST=$OUT/pmc_summary.json bash tools/pmc_profile.sh
 step e2e 600 python3 bench.py --no-cpu --no-secondary --steps 10 --e2e
 step cli 300 bpf-examples_amd/apps/xdpsock-gpu --pool 16777216 --pool-kind udp4 -b 1048576 -C 67108864 --json -Q
