@@ -13,10 +13,10 @@
  *    outside the UMEM) are finished as ABORTED;
  *  - frag_gather: each complete packet, and the byte after its last
  *    fragment (udp_csum's over-read byte), is copied to a bounce UMEM at a
- *    16-byte aligned offset, one wave per packet with coalesced 16-byte
- *    copies where the fragments allow them, and
- *    gets a bounce descriptor; the RX kernels then run over the bounce
- *    batch, one frame per packet;
+ *    16-byte aligned offset (its block's prefix on, in descriptor order),
+ *    one wave per packet with coalesced 16-byte copies where the fragments
+ *    allow them, and gets a bounce descriptor; the RX kernels then run over
+ *    the bounce batch, one frame per packet;
  *  - frag_scatter: the packet's verdict goes to each of its descriptors,
  *    its record and tuple to the first (all-zero ones to the others), and
  *    an ICMPv6 echo reply's first 64 bytes back into the fragments (the
