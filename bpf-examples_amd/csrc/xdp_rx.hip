@@ -1015,10 +1015,13 @@ __device__ __forceinline__ uint4 ld_nt16(const void *p)
  * udp_csum's over-read byte; zero past the UMEM) into the window sum the
  * fast kernel left in the result record.
  *
- * Per batch of 64 listed frames the wave works as four quarter-waves: a
- * quarter streams one frame at a time, 16 lanes x 16 B x U per step, and on finishing a frame takes the next unassigned one of the batch
- * (dynamic, so long and short frames balance).  Per-lane partial sums go to
- * LDS; lane f then adds frame f's 16 partials and completes its record.
+ * Per batch of 64 listed frames the wave works as four quarter-waves
+ * (G = 16; a diagnostic G = 8 variant uses eight 8-lane groups): a group
+ * streams one frame at a time, G lanes x 16 B x U per step, and on
+ * finishing a frame takes the next unassigned one of the batch (dynamic,
+ * so long and short frames balance).  Per-lane partial sums go to LDS, 16
+ * per frame (G = 8 zero-fills the other 8); lane f then adds frame f's 16
+ * partials and completes its record.
  * Frames are 16-byte aligned (a fast-shape condition), so absolute and
  * frame-relative 16-bit words coincide.
  */
@@ -1029,7 +1032,7 @@ __device__ __forceinline__ uint4 ld_nt16(const void *p)
  * result record).  GEN true: exception-kernel entries (xdpgpu ylist: index,
  * partial sum | check word, range start | check offset, range end | flags;
  * any alignment).  meta: 64 uint4, part4: 256 uint4 of this wave's LDS. */
-template <int U, bool NT, bool GEN>
+template <int U, bool NT, bool GEN, int G>
 __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 					   uint4 *part4, int lane,
 					   const void *list, uint32_t nb,
@@ -1037,7 +1040,8 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 					   uint64_t &my_bytes)
 {
 	uint32_t *part = reinterpret_cast<uint32_t *>(part4);
-	const uint32_t sub = lane & 15;
+	static_assert(G == 16 || G == 8, "group of 16 or 8 lanes per frame");
+	const uint32_t sub = lane & (G - 1);
 	const bool act = (uint32_t)lane < nb;
 	uint4 ye = make_uint4(0, 0, 0, 0);
 	uint64_t i;
@@ -1064,9 +1068,9 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 				(uint32_t)(lo - lo_al));
 	__builtin_amdgcn_wave_barrier();
 
-	/* quarter-wave streaming with dynamic frame assignment */
-	uint32_t k = lane >> 4;            /* this quarter's frame */
-	uint32_t nxt = 4;                  /* next unassigned (uniform) */
+	/* G-lane group streaming with dynamic frame assignment */
+	uint32_t k = lane / G;             /* this group's frame */
+	uint32_t nxt = kWave / G;          /* next unassigned (uniform) */
 	bool live = k < nb;
 	uint4 m = meta[live ? k : 0];
 	uint64_t flo = ((uint64_t)m.y << 32) | m.x;
@@ -1075,7 +1079,7 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 		uint4 v[U];
 #pragma unroll
 		for (int u = 0; u < U; u++) {
-			const uint32_t ou = o + 256 * u + 16 * sub;
+			const uint32_t ou = o + 16 * G * u + 16 * sub;
 			v[u] = make_uint4(0, 0, 0, 0);
 			if (live && ou < fnb)
 				v[u] = NT ? ld_nt16(a.umem + flo + ou)
@@ -1083,7 +1087,7 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 		}
 #pragma unroll
 		for (int u = 0; u < U; u++) {
-			const uint32_t ou = o + 256 * u + 16 * sub;
+			const uint32_t ou = o + 16 * G * u + 16 * sub;
 			if ((ou + 16 > fnb || ou < fsk) && ou < fnb) {
 				const uint4 mk = chunk_keep(ou, fsk, fnb);
 				v[u].x &= mk.x;
@@ -1094,14 +1098,16 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 			acc += halves(v[u].x) + halves(v[u].y) + halves(v[u].z) +
 			       halves(v[u].w);
 		}
-		o += 256 * U;
+		o += 16 * G * U;
 		const bool done = live && o >= fnb;
 		const uint64_t dq = __ballot(done && sub == 0);
 		if (dq) {
 			if (done) {
 				part[16 * k + sub] = acc;
+				if constexpr (G == 8)
+					part[16 * k + 8 + sub] = 0;
 				acc = 0;
-				k = nxt + (uint32_t)__popcll(dq & ((1ull << (lane & ~15)) - 1));
+				k = nxt + (uint32_t)__popcll(dq & ((1ull << (lane & ~(G - 1))) - 1));
 				live = k < nb;
 				m = meta[live ? k : 0];
 				flo = ((uint64_t)m.y << 32) | m.x;
@@ -1481,7 +1487,7 @@ struct RegionWalk {
 };
 
 /* Bulk kernel: the bulk pass as a kernel of its own (cfg.tune bit 8). */
-template <int MINW, int U, bool NT>
+template <int MINW, int U, bool NT, int G = 16>
 __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_bulk_kernel(RxArgs a)
 {
 	__shared__ uint4 meta_all[kWavesPerBlock * kWave];
@@ -1504,13 +1510,13 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_bulk_kernel(RxArgs a)
 		const uint32_t count = a.bcount[r];
 		const uint32_t *bl = a.blist + (uint64_t)r * a.xregion;
 		for (uint32_t b = w.bfirst; b < count; b += w.bstep)
-			bulk_batch<U, NT, false>(a, meta, part4, lane, bl + b,
+			bulk_batch<U, NT, false, G>(a, meta, part4, lane, bl + b,
 						 count - b < (uint32_t)kWave ? count - b : kWave,
 						 cnt, my_bytes);
 		const uint32_t ycount = a.ycount[r];
 		const uint4 *yl = a.ylist + (uint64_t)r * a.xregion;
 		for (uint32_t b = w.bfirst; b < ycount; b += w.bstep)
-			bulk_batch<U, NT, true>(a, meta, part4, lane, yl + b,
+			bulk_batch<U, NT, true, G>(a, meta, part4, lane, yl + b,
 						ycount - b < (uint32_t)kWave ? ycount - b : kWave,
 						cnt, my_bytes);
 	}
@@ -1686,7 +1692,7 @@ static hipError_t launch_sized(RxArgs a, uint32_t max_blocks,
 		(void)hipEventRecord(ev[2], stream);
 	switch (bulk_variant) {
 	case 1:
-		e = launch_resident<xdp_rx_bulk_kernel<8, 2, false>>(a, icap, stream);
+		e = launch_resident<xdp_rx_bulk_kernel<8, 4, true, 8>>(a, icap, stream);
 		break;
 	case 2:
 		e = launch_resident<xdp_rx_bulk_kernel<8, 2, true>>(a, icap, stream);
@@ -1716,7 +1722,7 @@ hipError_t launch_rx(const RxArgs &a, uint32_t window, uint32_t max_blocks,
 {
 	const uint32_t waves = tune & 0xff;
 	/* bits 10-11: bulk-kernel loads per lane and step (0: 4 non-temporal,
-	 * 1: 2, 2: 2 non-temporal, 3: 4) */
+	 * 1: 4 non-temporal in 8-lane groups, 2: 2 non-temporal, 3: 4) */
 	const uint32_t bu = (tune >> 10) & 3;
 	if (window == 128)
 		return launch_sized<128, 1>(a, max_blocks, stream, bu, ev);
