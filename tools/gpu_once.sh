@@ -1,9 +1,11 @@
 set -e
 mkdir -p gpurun_out
-export TMPDIR=/tmp
-for i in 1 2 3; do
-  echo "== new $i"; timeout -k 10 120 python -u tools/frags_probe.py --reps 5
-  echo "== old $i"; XDPGPU_LIB=build/ab_HEAD/libxdpgpu.so timeout -k 10 120 python -u tools/frags_probe.py --reps 5
-done > gpurun_out/frag_ab.log 2>&1
-timeout -k 10 300 python -u -m pytest tests/test_frags.py -x -q --timeout 200 --timeout-method thread -m gpu > gpurun_out/frag_par.log 2>&1
-timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_fragnew -o run -- python3 tools/frags_probe.py --reps 5 > gpurun_out/prof_fragnew.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_max_frames.py tests/test_frags.py -x -q --timeout 200 --timeout-method thread -m gpu > gpurun_out/mix_par.log 2>&1
+for i in 1 2; do
+  for lib in new old; do
+    if [ $lib = old ]; then export XDPGPU_LIB=build/ab_HEAD/libxdpgpu.so; else unset XDPGPU_LIB; fi
+    echo "== $lib imix"; timeout -k 10 120 python -u tools/tune_rx.py --frames 16777216 --kind 1 --seed 0x5EED0003 --variants 64:0 --rounds 5
+    echo "== $lib 1500"; timeout -k 10 120 python -u tools/tune_rx.py --frames 2097152 --size 1500 --variants 64:0 --rounds 5
+    echo "== $lib 64"; timeout -k 10 120 python -u tools/tune_rx.py --variants 64:0 --rounds 5
+  done
+done > gpurun_out/mix_ab.log 2>&1
