@@ -282,15 +282,22 @@ __global__ __launch_bounds__(kFragBlock) void frag_gather_kernel(FragArgs a)
 		kbase += kt;
 		obase += ot;
 		const uint64_t off = ow + pre;
+		/* a packet past the bounce capacity (only descriptors that
+		 * repeat UMEM bytes can get there: the capacity is the UMEM
+		 * size plus the per-packet padding) gets an empty bounce
+		 * descriptor, which the RX kernels finish as ABORTED */
+		const bool fits = off + sz <= a.bounce_cap;
 		if (mine) {
 			const uint32_t k = (uint32_t)kw + __builtin_amdgcn_mbcnt_hi(
 				(uint32_t)(mm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0));
 			*reinterpret_cast<uint4 *>(a.bdesc + k) =
-				make_uint4((uint32_t)off, (uint32_t)(off >> 32), (uint32_t)total, 0u);
+				fits ? make_uint4((uint32_t)off, (uint32_t)(off >> 32),
+						  (uint32_t)total, 0u)
+				     : make_uint4(0u, 0u, 0u, 0u);
 			a.bmap[k] = make_uint2((uint32_t)i, last - (uint32_t)i + 1);
 		}
 		/* the wave copies its packets one after the other */
-		for (uint64_t m = mm; m; m &= m - 1) {
+		for (uint64_t m = __ballot(mine && fits); m; m &= m - 1) {
 			const int src = __builtin_ctzll(m);
 			const uint32_t first = rl32((uint32_t)i, src), lst = rl32(last, src);
 			uint8_t *dst = a.bounce + rl64(off, src);
@@ -312,7 +319,8 @@ __global__ __launch_bounds__(kFragBlock) void frag_gather_kernel(FragArgs a)
 __global__ __launch_bounds__(kFragBlock) void frag_scatter_kernel(FragArgs a)
 {
 	const uint64_t step = (uint64_t)gridDim.x * kFragBlock;
-	for (uint64_t k = (uint64_t)blockIdx.x * kFragBlock + threadIdx.x; k < a.m;
+	const uint64_t m = a.fc[0];        /* packets gathered (device count) */
+	for (uint64_t k = (uint64_t)blockIdx.x * kFragBlock + threadIdx.x; k < m;
 	     k += step) {
 		const uint2 mp = a.bmap[k];
 		const uint8_t v = a.bverdict[k];

@@ -1,0 +1,98 @@
+// SPDX-License-Identifier: GPL-2.0
+/*
+ * hostpath.hip - the host path's write-back of ICMPv6 echo replies.
+ *
+ * xdpgpu_submit runs the RX kernels on the slot's device mirror of the
+ * host UMEM.  The echo responder (process_packet, af_xdp_user.c:968-1040)
+ * rewrites a TX frame in place: MACs, IPv6 addresses, type and checksum,
+ * all in its bytes 0-57.  Only those frames may be written back: the rest
+ * of the UMEM belongs to the application and the kernel (fill ring frames
+ * the NIC may be filling), SURVEY §8b.  So for every descriptor of the
+ * batch whose verdict is TX this kernel copies bytes [0, min(len, 64)) of
+ * its frame, and nothing else:
+ *  - straight into the host UMEM through its mapped pinned pointer (the
+ *    writes cross PCIe as posted writes; they are visible to the host once
+ *    the slot's completion event has fired), or
+ *  - as compact 80-byte records (EchoRec) that xdpgpu_wait scatters, when
+ *    the UMEM is not mapped.
+ * Multi-buffer packets: each fragment of a TX packet has verdict TX, and
+ * packet byte p < 64 lies at offset <= p of its fragment, so the fragments'
+ * first 64 bytes cover the rewrite.
+ */
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "xdpgpu_internal.h"
+
+namespace xdpgpu {
+
+namespace {
+
+constexpr int kEchoWave = 64;
+constexpr int kEchoBlock = 256;
+
+__device__ __forceinline__ uint32_t rl32(uint32_t v, int l)
+{
+	return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+
+/* One lane per descriptor; the wave copies its TX frames one after the
+ * other, lane j byte j. */
+__global__ __launch_bounds__(kEchoBlock) void echo_writeback_kernel(EchoArgs a)
+{
+	const int lane = threadIdx.x & (kEchoWave - 1);
+	const uint64_t i = (uint64_t)blockIdx.x * kEchoBlock + threadIdx.x;
+	bool tx = false;
+	uint64_t eff = 0;
+	uint32_t w = 0;
+	if (i < a.n && a.verdict[i] == XDPGPU_TX) {
+		const xdpgpu_desc d = a.desc[i];
+		eff = (d.addr & ((1ull << 48) - 1)) + (d.addr >> 48);
+		/* a TX verdict implies a frame inside the UMEM; checked anyway */
+		tx = (uint64_t)d.len <= a.usize && eff <= a.usize - d.len;
+		w = d.len < kEchoBytes ? d.len : kEchoBytes;
+	}
+	const uint64_t m = __ballot(tx);
+	if (!m)
+		return;
+	uint32_t base = 0;
+	if (!a.host) {
+		if (lane == 0)
+			base = atomicAdd(a.nrec, (uint32_t)__popcll(m));
+		base = __builtin_amdgcn_readfirstlane(base);
+	}
+	uint32_t r = 0;
+	for (uint64_t k = m; k; k &= k - 1, r++) {
+		const int src = __builtin_ctzll(k);
+		const uint64_t se = ((uint64_t)rl32((uint32_t)(eff >> 32), src) << 32) |
+				    rl32((uint32_t)eff, src);
+		const uint32_t sw = rl32(w, src);
+		const uint8_t b = (uint32_t)lane < sw ? a.mirror[se + lane] : 0;
+		if (a.host) {
+			if ((uint32_t)lane < sw)
+				a.host[se + lane] = b;
+		} else {
+			EchoRec *rec = a.rec + base + r;
+			rec->b[lane] = b;
+			if (lane == 0) {
+				rec->eff = se;
+				rec->len = sw;
+				rec->rsvd = 0;
+			}
+		}
+	}
+}
+
+} // namespace
+
+hipError_t launch_echo_writeback(const EchoArgs &a, hipStream_t stream)
+{
+	if (!a.n)
+		return hipSuccess;
+	const uint32_t blocks = (uint32_t)(((uint64_t)a.n + kEchoBlock - 1) / kEchoBlock);
+	hipLaunchKernelGGL(echo_writeback_kernel, dim3(blocks), dim3(kEchoBlock), 0,
+			   stream, a);
+	return hipGetLastError();
+}
+
+} // namespace xdpgpu

@@ -1180,19 +1180,7 @@ __global__ __launch_bounds__(kBlockN) void xdp_nat64_fast_kernel(Nat64Args a)
 template <auto KERN>
 static uint32_t resident_n()
 {
-	static uint32_t cached = 0;
-	if (!cached) {
-		int per_cu = 0, dev = 0;
-		hipDeviceProp_t prop;
-		if (hipGetDevice(&dev) != hipSuccess ||
-		    hipGetDeviceProperties(&prop, dev) != hipSuccess ||
-		    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, KERN, kBlockN, 0) !=
-			    hipSuccess ||
-		    per_cu <= 0)
-			return 1024;
-		cached = (uint32_t)per_cu * (uint32_t)prop.multiProcessorCount;
-	}
-	return cached;
+	return resident_blocks_dev<KERN, kBlockN>(1024);
 }
 
 uint32_t nat64_grid(uint32_t n, uint32_t max_blocks)

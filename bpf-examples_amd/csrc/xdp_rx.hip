@@ -1213,7 +1213,11 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 		blk_cnt[threadIdx.x] = 0;
 	__syncthreads();
 
-	const uint64_t ntiles = ((uint64_t)a.n + kWave - 1) / kWave;
+	/* frames: a.n, or the device count it bounds (the bounce batch of
+	 * multi-buffer packets, frags.hip) */
+	const uint32_t nfr = a.ndev ? (uint32_t)min((unsigned long long)a.n, *a.ndev)
+				    : a.n;
+	const uint64_t ntiles = ((uint64_t)nfr + kWave - 1) / kWave;
 	const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
 	const uint64_t wgid = (uint64_t)blockIdx.x * kWavesPerBlock + wid;
 	uint32_t *xl = a.xlist + wgid * a.xregion;
@@ -1261,7 +1265,7 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 	 * prefetch is an unconditional load (lanes past the end are inactive) */
 	auto ld_desc = [&](uint64_t tt) -> uint4 {
 		uint64_t i = tt * kWave + lane;
-		i = i < a.n ? i : a.n - 1;
+		i = i < nfr ? i : nfr - 1;
 		return *reinterpret_cast<const uint4 *>(a.desc + i);
 	};
 	/* DMA the 64-byte windows of a tile into buf: frames that are not
@@ -1309,7 +1313,7 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 				prev = t ? a.desc[t * kWave - 1].options & XDPGPU_PKT_CONTD : 0u;
 			skip = (contd | prev) != 0;
 		}
-		const bool active = (i < a.n) & !skip;
+		const bool active = (i < nfr) & !skip;
 
 		/* 1. this lane's window out of LDS (4 conflict-free b128 reads),
 		 * then the next tile's DMA and descriptors */
@@ -1626,21 +1630,7 @@ uint32_t rx_grid_blocks(uint32_t n, uint32_t max_blocks)
 template <auto KERN>
 static uint32_t resident_blocks()
 {
-	static uint32_t cached = 0;
-	if (!cached) {
-		int per_cu = 0, dev = 0;
-		hipDeviceProp_t prop;
-		if (hipGetDevice(&dev) != hipSuccess ||
-		    hipGetDeviceProperties(&prop, dev) != hipSuccess ||
-		    hipOccupancyMaxActiveBlocksPerMultiprocessor(
-			    &per_cu, KERN, kBlock, 0) != hipSuccess ||
-		    per_cu <= 0)
-			return kMaxRxBlocks;
-		cached = (uint32_t)per_cu * (uint32_t)prop.multiProcessorCount;
-		if (cached > kMaxRxBlocks)
-			cached = kMaxRxBlocks;
-	}
-	return cached;
+	return resident_blocks_dev<KERN, kBlock>(kMaxRxBlocks);
 }
 
 /* Launch the fast kernel on a grid of resident blocks (no partial second

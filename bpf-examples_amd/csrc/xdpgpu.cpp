@@ -55,6 +55,22 @@ struct Slot {
 	xdpgpu_result *d_bres = nullptr;
 	uint8_t *d_btup = nullptr;
 	uint64_t pk_cap = 0;
+	/* host path: this slot's device mirror of the registered UMEM (one
+	 * per slot, so two batches in flight never share mirror bytes) */
+	uint8_t *d_mirror = nullptr;
+	uint64_t mirror_cap = 0;
+	/* echo write-back as compact records (UMEM not mapped) */
+	EchoRec *d_erec = nullptr;
+	EchoRec *h_erec = nullptr;
+	uint32_t *d_ecnt = nullptr;
+	uint32_t *h_ecnt = nullptr;          /* pinned */
+	uint64_t erec_cap = 0;
+	bool echo_pending = false;
+	/* ordering of the slot's scratch (deferral lists, counts, counters,
+	 * fragment buffers) between launches on different streams: the event
+	 * recorded after the last launch that used it, on scr_last */
+	hipEvent_t scr_ev = nullptr;
+	hipStream_t scr_last = nullptr;
 	bool busy = false;
 	/* pending host copies for xdpgpu_wait() */
 	uint32_t n = 0;
@@ -70,7 +86,6 @@ struct xdpgpu_ctx {
 	uint8_t *h_umem = nullptr;
 	uint64_t umem_size = 0;
 	bool pinned = false;
-	uint8_t *d_umem = nullptr;       /* device mirror                  */
 	uint8_t *d_umem_mapped = nullptr; /* device view of pinned host UMEM */
 	/* XDPGPU_CFG_TIMING: 4 events per recorded launch */
 	hipEvent_t *tev = nullptr;
@@ -155,6 +170,14 @@ static void free_slot(Slot &s)
 	(void)hipFree(s.d_bverdict);
 	(void)hipFree(s.d_bres);
 	(void)hipFree(s.d_btup);
+	(void)hipFree(s.d_mirror);
+	(void)hipFree(s.d_erec);
+	(void)hipFree(s.d_ecnt);
+	if (s.h_ecnt)
+		(void)hipHostFree(s.h_ecnt);
+	free(s.h_erec);
+	if (s.scr_ev)
+		(void)hipEventDestroy(s.scr_ev);
 	if (s.done)
 		(void)hipEventDestroy(s.done);
 	if (s.stream)
@@ -176,8 +199,6 @@ void xdpgpu_fini(xdpgpu_ctx *ctx)
 				(void)hipEventDestroy(ctx->tev[i]);
 		delete[] ctx->tev;
 	}
-	if (ctx->d_umem)
-		(void)hipFree(ctx->d_umem);
 	if (ctx->d_v6map)
 		(void)hipFree(ctx->d_v6map);
 	if (ctx->d_v4map)
@@ -226,6 +247,7 @@ int xdpgpu_init(const xdpgpu_cfg *cfg, xdpgpu_ctx **out)
 			size_t stat_bytes = (size_t)kMaxRxBlocks * CNT_SLOT * 8;
 			if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||
 			    hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess ||
+			    hipEventCreateWithFlags(&s.scr_ev, hipEventDisableTiming) != hipSuccess ||
 			    hipMalloc(&s.d_stats, stat_bytes) != hipSuccess ||
 			    hipMemset(s.d_stats, 0, stat_bytes) != hipSuccess)
 				rc = set_err(ctx, -ENOMEM, "slot %u allocation failed", i);
@@ -253,6 +275,40 @@ int xdpgpu_init(const xdpgpu_cfg *cfg, xdpgpu_ctx **out)
 	return 0;
 }
 
+/* Drop the registered UMEM: the slots' mirrors and the host pinning. */
+static void release_umem(xdpgpu_ctx *ctx)
+{
+	(void)hipDeviceSynchronize();
+	for (uint32_t i = 0; i < kSlots; i++) {
+		Slot &s = ctx->slot[i];
+		(void)hipFree(s.d_mirror);
+		s.d_mirror = nullptr;
+		s.mirror_cap = 0;
+	}
+	if (ctx->pinned)
+		(void)hipHostUnregister(ctx->h_umem);
+	ctx->pinned = false;
+	ctx->h_umem = nullptr;
+	ctx->umem_size = 0;
+	ctx->d_umem_mapped = nullptr;
+}
+
+/* A slot's device mirror of the registered UMEM (+64: 16-byte loads of a
+ * frame's last chunk stay inside it). */
+static int ensure_mirror(xdpgpu_ctx *ctx, Slot &s)
+{
+	if (s.d_mirror && s.mirror_cap >= ctx->umem_size + 64)
+		return 0;
+	(void)hipFree(s.d_mirror);
+	s.d_mirror = nullptr;
+	s.mirror_cap = 0;
+	if (hipMalloc(&s.d_mirror, ctx->umem_size + 64) != hipSuccess)
+		return set_err(ctx, -ENOMEM, "device UMEM mirror of %llu bytes",
+			       (unsigned long long)ctx->umem_size);
+	s.mirror_cap = ctx->umem_size + 64;
+	return 0;
+}
+
 int xdpgpu_register_umem(xdpgpu_ctx *ctx, void *base, uint64_t size,
 			 uint32_t chunk_size, uint32_t headroom, uint32_t flags)
 {
@@ -265,18 +321,12 @@ int xdpgpu_register_umem(xdpgpu_ctx *ctx, void *base, uint64_t size,
 	if (headroom && chunk_size && headroom >= chunk_size)
 		return -EINVAL;
 	HIP_TRY(ctx, hipSetDevice(ctx->cfg.device));
-	if (ctx->d_umem) {
-		HIP_TRY(ctx, hipDeviceSynchronize());
-		(void)hipFree(ctx->d_umem);
-		ctx->d_umem = nullptr;
-	}
-	if (ctx->pinned) {
-		(void)hipHostUnregister(ctx->h_umem);
-		ctx->pinned = false;
-	}
+	for (uint32_t i = 0; i < kSlots; i++)
+		if (ctx->slot[i].busy)
+			return set_err(ctx, -EBUSY, "slot %u in flight", i);
+	release_umem(ctx);
 	ctx->h_umem = (uint8_t *)base;
 	ctx->umem_size = size;
-	ctx->d_umem_mapped = nullptr;
 	/* pin (and map) the caller's UMEM; pageable memory still works,
 	 * only slower */
 	if (hipHostRegister(base, size, hipHostRegisterMapped) == hipSuccess) {
@@ -287,15 +337,21 @@ int xdpgpu_register_umem(xdpgpu_ctx *ctx, void *base, uint64_t size,
 	} else {
 		(void)hipGetLastError();
 	}
-	/* +64: 16-byte loads of a frame's last chunk stay inside the mirror */
-	if (hipMalloc(&ctx->d_umem, size + 64) != hipSuccess)
-		return set_err(ctx, -ENOMEM, "device UMEM mirror of %llu bytes",
-			       (unsigned long long)size);
+	/* slot 0's mirror now, so that a size the device cannot hold fails
+	 * here; slot 1's on its first batch */
+	const int rc = ensure_mirror(ctx, ctx->slot[0]);
+	if (rc) {
+		release_umem(ctx);
+		return rc;
+	}
 	return 0;
 }
 
 static int ensure_slot_buffers(xdpgpu_ctx *ctx, Slot &s, uint32_t n)
 {
+	int rc = ensure_mirror(ctx, s);
+	if (rc)
+		return rc;
 	if (s.d_desc)
 		return 0;
 	uint32_t cap = ctx->cfg.max_batch;
@@ -349,7 +405,7 @@ static int ensure_frag_bufs(xdpgpu_ctx *ctx, Slot &s, uint64_t m, uint64_t bytes
 			hipHostMalloc((void **)&s.h_fc, 4 * sizeof(unsigned long long), 0) !=
 				hipSuccess))
 		return set_err(ctx, -ENOMEM, "fragment counters");
-	if (bytes && bytes + 64 > s.bounce_cap) {
+	if (bytes + 64 > s.bounce_cap) {
 		(void)hipFree(s.d_bounce);
 		s.d_bounce = nullptr;
 		s.bounce_cap = 0;
@@ -385,6 +441,24 @@ static int ensure_frag_bufs(xdpgpu_ctx *ctx, Slot &s, uint64_t m, uint64_t bytes
 	return 0;
 }
 
+/* A launch on `stream` that uses slot s's scratch waits for the previous
+ * launch that used it when that one went to another stream (a caller's
+ * stream for xdpgpu_process_dev / xdpgpu_nat64_dev, the slot's own for
+ * xdpgpu_submit); scratch_leave marks the new owner. */
+static int scratch_enter(xdpgpu_ctx *ctx, Slot &s, hipStream_t stream)
+{
+	if (s.scr_last && s.scr_last != stream)
+		HIP_TRY(ctx, hipStreamWaitEvent(stream, s.scr_ev, 0));
+	return 0;
+}
+
+static int scratch_leave(xdpgpu_ctx *ctx, Slot &s, hipStream_t stream)
+{
+	HIP_TRY(ctx, hipEventRecord(s.scr_ev, stream));
+	s.scr_last = stream;
+	return 0;
+}
+
 static int enqueue_rx(xdpgpu_ctx *ctx, Slot &s, uint8_t *d_umem, uint64_t usize,
 		      const xdpgpu_desc *d_desc, uint32_t n, uint8_t *d_verdict,
 		      xdpgpu_result *d_res, uint8_t *d_tup, hipStream_t stream)
@@ -415,16 +489,30 @@ static int enqueue_rx(xdpgpu_ctx *ctx, Slot &s, uint8_t *d_umem, uint64_t usize,
 	a.force_generic = (ctx->cfg.tune >> 9) & 1;
 	a.frags = (ctx->cfg.flags & XDPGPU_CFG_FRAGS) ? 1u : 0u;
 
-	/* multi-buffer packets: counted (and the broken ones finished) before
-	 * the RX kernels, which skip them; one host round trip for the bounce
-	 * sizes */
+	/* Multi-buffer packets.  No host round trip: the bounce arrays are
+	 * sized from bounds known here (a packet has at least two
+	 * descriptors; its bounce bytes are its own bytes plus at most 16 of
+	 * padding, and the fragments of distinct packets are distinct UMEM
+	 * bytes), and the kernels after the count read the packet count from
+	 * the device. */
 	FragArgs f;
 	memset(&f, 0, sizeof(f));
-	uint64_t m = 0, bbytes = 0;
+	const uint64_t mcap = a.frags ? (uint64_t)n / 2 + 1 : 0;
 	if (a.frags) {
-		rc = ensure_frag_bufs(ctx, s, 0, 0);
-		if (rc)
-			return rc;
+		const uint64_t bytes = usize + 16 * mcap;
+		if (!s.d_fc || bytes + 64 > s.bounce_cap || mcap > s.pk_cap) {
+			/* (re)allocation: the slot's earlier launches first */
+			if (s.scr_last)
+				HIP_TRY(ctx, hipEventSynchronize(s.scr_ev));
+			rc = ensure_frag_bufs(ctx, s, mcap, bytes);
+			if (rc)
+				return rc;
+		}
+	}
+	rc = scratch_enter(ctx, s, stream);
+	if (rc)
+		return rc;
+	if (a.frags) {
 		f.umem = d_umem;
 		f.usize = usize;
 		f.desc = d_desc;
@@ -436,46 +524,41 @@ static int enqueue_rx(xdpgpu_ctx *ctx, Slot &s, uint8_t *d_umem, uint64_t usize,
 		f.stats = a.stats;
 		f.fc = s.d_fc;
 		f.blk = s.d_fc + 2;
+		f.bounce = s.d_bounce;
+		f.bounce_cap = s.bounce_cap - 64;
+		f.bdesc = s.d_bdesc;
+		f.bmap = s.d_bmap;
+		f.bverdict = s.d_bverdict;
+		f.bres = s.d_bres;
+		f.btup = s.d_btup;
+		f.m = (uint32_t)mcap;
 		HIP_TRY(ctx, launch_frag_count(f, stream));
-		HIP_TRY(ctx, hipMemcpyAsync(s.h_fc, s.d_fc, 2 * sizeof(unsigned long long),
-					    hipMemcpyDeviceToHost, stream));
-		HIP_TRY(ctx, hipStreamSynchronize(stream));
-		m = s.h_fc[0];
-		bbytes = s.h_fc[1];
-		rc = ensure_frag_bufs(ctx, s, m, bbytes);
-		if (rc)
-			return rc;
 	}
 	hipEvent_t *ev = nullptr;
 	if (ctx->tev && ctx->tn < XDPGPU_TIMING_MAX)
 		ev = ctx->tev + 4 * ctx->tn++;
 	HIP_TRY(ctx, launch_rx(a, ctx->cfg.window, ctx->max_blocks, stream,
 			       ctx->cfg.tune, ev));
-	if (!m)
-		return 0;
-	/* one frame per packet: gathered into the bounce UMEM, the RX kernels
-	 * over the bounce batch, the outputs back to the packets' descriptors */
-	f.bounce = s.d_bounce;
-	f.bdesc = s.d_bdesc;
-	f.bmap = s.d_bmap;
-	f.bverdict = s.d_bverdict;
-	f.bres = s.d_bres;
-	f.btup = s.d_btup;
-	f.m = (uint32_t)m;
-	HIP_TRY(ctx, launch_frag_gather(f, stream));
-	RxArgs b = a;
-	b.umem = s.d_bounce;
-	b.usize = bbytes;
-	b.desc = s.d_bdesc;
-	b.n = (uint32_t)m;
-	b.verdict = s.d_bverdict;
-	b.res = d_res ? s.d_bres : nullptr;
-	b.tup = d_tup ? s.d_btup : nullptr;
-	b.frags = 0;
-	HIP_TRY(ctx, launch_rx(b, ctx->cfg.window, ctx->max_blocks, stream,
-			       ctx->cfg.tune, nullptr));
-	HIP_TRY(ctx, launch_frag_scatter(f, stream));
-	return 0;
+	if (a.frags) {
+		/* one frame per packet: gathered into the bounce UMEM, the RX
+		 * kernels over the bounce batch, the outputs back to the
+		 * packets' descriptors */
+		HIP_TRY(ctx, launch_frag_gather(f, stream));
+		RxArgs b = a;
+		b.umem = s.d_bounce;
+		b.usize = f.bounce_cap;
+		b.desc = s.d_bdesc;
+		b.n = (uint32_t)mcap;
+		b.ndev = s.d_fc;
+		b.verdict = s.d_bverdict;
+		b.res = d_res ? s.d_bres : nullptr;
+		b.tup = d_tup ? s.d_btup : nullptr;
+		b.frags = 0;
+		HIP_TRY(ctx, launch_rx(b, ctx->cfg.window, ctx->max_blocks, stream,
+				       ctx->cfg.tune, nullptr));
+		HIP_TRY(ctx, launch_frag_scatter(f, stream));
+	}
+	return scratch_leave(ctx, s, stream);
 }
 
 int xdpgpu_kernel_times(xdpgpu_ctx *ctx, xdpgpu_ktimes *out)
@@ -646,8 +729,15 @@ int xdpgpu_nat64_dev(xdpgpu_ctx *ctx, void *d_umem, uint64_t umem_size,
 		memcpy(a.pref_w, ctx->ncfg.v6_prefix, 12);
 	}
 	hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
+	if (!a.fast) {
+		HIP_TRY(ctx, launch_nat64(a, ctx->max_blocks, st));
+		return 0;
+	}
+	int rc = scratch_enter(ctx, ctx->slot[0], st);
+	if (rc)
+		return rc;
 	HIP_TRY(ctx, launch_nat64(a, ctx->max_blocks, st));
-	return 0;
+	return scratch_leave(ctx, ctx->slot[0], st);
 }
 
 int xdpgpu_ceiling_dev(xdpgpu_ctx *ctx, const void *d_umem, uint64_t umem_size,
@@ -672,6 +762,54 @@ int xdpgpu_ceiling_dev(xdpgpu_ctx *ctx, const void *d_umem, uint64_t umem_size,
 	return 0;
 }
 
+/* The UMEM bytes a batch reads, as runs of nearby frames (gaps up to
+ * kRunGap bytes are copied along): one run for a batch of consecutive
+ * frames, two for a batch that wraps round a cyclic fill ring.  More than
+ * kMaxRuns runs: the batch is scattered over the UMEM, and runs is left
+ * empty.  [lo, hi) is the span of all of them; used the bytes the
+ * descriptors name.  +1 byte per frame: udp_csum's odd over-read. */
+struct Run {
+	uint64_t lo, hi;
+};
+constexpr uint64_t kRunGap = 4096;
+constexpr size_t kMaxRuns = 64;
+
+static void batch_runs(const xdpgpu_ctx *ctx, const xdpgpu_desc *descs,
+		       uint32_t n, std::vector<Run> &runs, uint64_t &lo,
+		       uint64_t &hi, uint64_t &used)
+{
+	runs.clear();
+	lo = UINT64_MAX;
+	hi = 0;
+	used = 0;
+	bool scattered = false;
+	for (uint32_t i = 0; i < n; i++) {
+		const uint64_t eff = (descs[i].addr & ((1ull << 48) - 1)) +
+				     (descs[i].addr >> 48);
+		if (eff >= ctx->umem_size)
+			continue;
+		uint64_t end = eff + descs[i].len + 1;
+		if (end > ctx->umem_size)
+			end = ctx->umem_size;
+		lo = std::min(lo, eff);
+		hi = std::max(hi, end);
+		used += descs[i].len;
+		if (scattered)
+			continue;
+		if (!runs.empty() && eff >= runs.back().lo &&
+		    eff <= runs.back().hi + kRunGap) {
+			runs.back().hi = std::max(runs.back().hi, end);
+			continue;
+		}
+		if (runs.size() == kMaxRuns) {
+			scattered = true;
+			runs.clear();
+			continue;
+		}
+		runs.push_back({eff, end});
+	}
+}
+
 int xdpgpu_submit(xdpgpu_ctx *ctx, uint32_t slot, const xdpgpu_desc *descs,
 		  uint32_t n, uint8_t *verdict, xdpgpu_result *res,
 		  void *tuples)
@@ -690,36 +828,42 @@ int xdpgpu_submit(xdpgpu_ctx *ctx, uint32_t slot, const xdpgpu_desc *descs,
 	if (rc)
 		return rc;
 	s.n = n;
+	s.echo_pending = false;
 	if (n == 0)
 		return 0;
 
-	/* UMEM span this batch touches (+1 byte: udp_csum's odd over-read) */
-	uint64_t lo = UINT64_MAX, hi = 0, used = 0;
-	for (uint32_t i = 0; i < n; i++) {
-		uint64_t eff = (descs[i].addr & ((1ull << 48) - 1)) +
-			       (descs[i].addr >> 48);
-		if (eff >= ctx->umem_size)
-			continue;
-		uint64_t end = eff + descs[i].len + 1;
-		if (end > ctx->umem_size)
-			end = ctx->umem_size;
-		lo = std::min(lo, eff);
-		hi = std::max(hi, end);
-		used += descs[i].len;
-	}
-	uint8_t *kumem = ctx->d_umem;
+	/* the frames go to this slot's own mirror: a batch in flight on the
+	 * other slot never sees them, whatever the two batches' addresses */
+	std::vector<Run> runs;
+	uint64_t lo, hi, used;
+	batch_runs(ctx, descs, n, runs, lo, hi, used);
+	const bool echo = ctx->cfg.flags & XDPGPU_CFG_ICMP6_ECHO;
+	const bool mapped_ok = ctx->d_umem_mapped && !(ctx->umem_size & 15) &&
+			       !((ctx->cfg.tune >> 14) & 1);
+	uint8_t *kumem = s.d_mirror;
 	bool zero_copy = false;
 	if (hi > lo) {
-		uint64_t span = hi - lo;
-		/* sparse batch over pinned memory: read the frames in place */
-		if (ctx->d_umem_mapped && !(ctx->umem_size & 15) &&
-		    span > 4 * used + (1u << 20)) {
+		uint64_t copy = 0;
+		for (const Run &r : runs)
+			copy += r.hi - r.lo;
+		if (runs.empty())
+			copy = hi - lo;
+		/* sparse batch over pinned memory: the kernels read the frames
+		 * in place (and an echo rewrite lands in the host UMEM) */
+		if (mapped_ok && copy > 4 * used + (1u << 20)) {
 			kumem = ctx->d_umem_mapped;
 			zero_copy = true;
-		} else {
-			HIP_TRY(ctx, hipMemcpyAsync(ctx->d_umem + lo, ctx->h_umem + lo,
-						    span, hipMemcpyHostToDevice,
+		} else if (runs.empty()) {
+			HIP_TRY(ctx, hipMemcpyAsync(s.d_mirror + lo, ctx->h_umem + lo,
+						    hi - lo, hipMemcpyHostToDevice,
 						    s.stream));
+		} else {
+			for (const Run &r : runs)
+				HIP_TRY(ctx, hipMemcpyAsync(s.d_mirror + r.lo,
+							    ctx->h_umem + r.lo,
+							    r.hi - r.lo,
+							    hipMemcpyHostToDevice,
+							    s.stream));
 		}
 	}
 	HIP_TRY(ctx, hipMemcpyAsync(s.d_desc, descs, (size_t)n * sizeof(*descs),
@@ -729,6 +873,47 @@ int xdpgpu_submit(xdpgpu_ctx *ctx, uint32_t slot, const xdpgpu_desc *descs,
 			res ? s.d_res : nullptr, d_tup, s.stream);
 	if (rc)
 		return rc;
+	/* echo replies were written in the mirror: only the TX frames' first
+	 * bytes go back to the host UMEM (SURVEY §8b ownership) */
+	if (echo && !zero_copy) {
+		EchoArgs e;
+		memset(&e, 0, sizeof(e));
+		e.mirror = s.d_mirror;
+		e.usize = ctx->umem_size;
+		e.desc = s.d_desc;
+		e.verdict = s.d_verdict;
+		e.n = n;
+		if (ctx->d_umem_mapped && !((ctx->cfg.tune >> 14) & 1)) {
+			e.host = ctx->d_umem_mapped;
+		} else {
+			if (s.erec_cap < n) {
+				HIP_TRY(ctx, hipStreamSynchronize(s.stream));
+				(void)hipFree(s.d_erec);
+				free(s.h_erec);
+				s.d_erec = nullptr;
+				s.h_erec = nullptr;
+				s.erec_cap = 0;
+				const uint64_t cap = std::max<uint64_t>(n, 4096);
+				s.h_erec = (EchoRec *)malloc(cap * sizeof(EchoRec));
+				if (!s.h_erec ||
+				    hipMalloc(&s.d_erec, cap * sizeof(EchoRec)) != hipSuccess)
+					return set_err(ctx, -ENOMEM, "echo records");
+				s.erec_cap = cap;
+			}
+			if (!s.d_ecnt &&
+			    (hipMalloc(&s.d_ecnt, sizeof(uint32_t)) != hipSuccess ||
+			     hipHostMalloc((void **)&s.h_ecnt, sizeof(uint32_t), 0) != hipSuccess))
+				return set_err(ctx, -ENOMEM, "echo record count");
+			HIP_TRY(ctx, hipMemsetAsync(s.d_ecnt, 0, sizeof(uint32_t), s.stream));
+			e.rec = s.d_erec;
+			e.nrec = s.d_ecnt;
+			s.echo_pending = true;
+		}
+		HIP_TRY(ctx, launch_echo_writeback(e, s.stream));
+		if (s.echo_pending)
+			HIP_TRY(ctx, hipMemcpyAsync(s.h_ecnt, s.d_ecnt, sizeof(uint32_t),
+						    hipMemcpyDeviceToHost, s.stream));
+	}
 	HIP_TRY(ctx, hipMemcpyAsync(verdict, s.d_verdict, n,
 				    hipMemcpyDeviceToHost, s.stream));
 	if (res)
@@ -738,10 +923,6 @@ int xdpgpu_submit(xdpgpu_ctx *ctx, uint32_t slot, const xdpgpu_desc *descs,
 		HIP_TRY(ctx, hipMemcpyAsync(tuples, d_tup,
 					    (size_t)n * tuple_bytes(ctx->cfg.tuple_fmt),
 					    hipMemcpyDeviceToHost, s.stream));
-	/* echo rewrites happened in the mirror: bring the span back */
-	if ((ctx->cfg.flags & XDPGPU_CFG_ICMP6_ECHO) && !zero_copy && hi > lo)
-		HIP_TRY(ctx, hipMemcpyAsync(ctx->h_umem + lo, ctx->d_umem + lo,
-					    hi - lo, hipMemcpyDeviceToHost, s.stream));
 	HIP_TRY(ctx, hipEventRecord(s.done, s.stream));
 	s.busy = true;
 	return 0;
@@ -756,7 +937,34 @@ int xdpgpu_wait(xdpgpu_ctx *ctx, uint32_t slot)
 		return 0;
 	s.busy = false;
 	HIP_TRY(ctx, hipEventSynchronize(s.done));
+	if (s.echo_pending) {
+		/* compact echo records: scatter each TX frame's first bytes */
+		s.echo_pending = false;
+		const uint32_t m = *s.h_ecnt;
+		if (m) {
+			HIP_TRY(ctx, hipMemcpyAsync(s.h_erec, s.d_erec, (size_t)m * sizeof(EchoRec),
+						    hipMemcpyDeviceToHost, s.stream));
+			HIP_TRY(ctx, hipStreamSynchronize(s.stream));
+			for (uint32_t k = 0; k < m; k++)
+				memcpy(ctx->h_umem + s.h_erec[k].eff, s.h_erec[k].b,
+				       s.h_erec[k].len);
+		}
+	}
 	return 0;
+}
+
+void *xdpgpu_host_alloc(uint64_t size)
+{
+	void *p = nullptr;
+	if (!size || hipHostMalloc(&p, size, hipHostMallocPortable) != hipSuccess)
+		return nullptr;
+	return p;
+}
+
+void xdpgpu_host_free(void *p)
+{
+	if (p)
+		(void)hipHostFree(p);
 }
 
 int xdpgpu_process(xdpgpu_ctx *ctx, const xdpgpu_desc *descs, uint32_t n,

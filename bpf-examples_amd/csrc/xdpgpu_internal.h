@@ -6,9 +6,44 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <atomic>
+
 #include "xdpgpu.h"
 
 namespace xdpgpu {
+
+/* Blocks of THREADS threads of a kernel resident at once on the current
+ * device (occupancy x CUs, at most cap), cached per device ordinal.
+ * Contexts on different devices, or threads racing on the first call, each
+ * compute the same value; the relaxed atomic makes the race benign. */
+template <auto KERN, int THREADS>
+static uint32_t resident_blocks_dev(uint32_t cap)
+{
+	constexpr int kMaxDev = 64;
+	static std::atomic<uint32_t> cached[kMaxDev];
+	int dev = 0;
+	if (hipGetDevice(&dev) != hipSuccess || dev < 0)
+		return cap;
+	if (dev < kMaxDev) {
+		const uint32_t c = cached[dev].load(std::memory_order_relaxed);
+		if (c)
+			return c;
+	}
+	int per_cu = 0;
+	hipDeviceProp_t prop;
+	if (hipGetDeviceProperties(&prop, dev) != hipSuccess ||
+	    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, KERN, THREADS, 0) !=
+		    hipSuccess ||
+	    per_cu <= 0)
+		return cap;
+	uint32_t c = (uint32_t)per_cu * (uint32_t)prop.multiProcessorCount;
+	if (c > cap)
+		c = cap;
+	if (dev < kMaxDev)
+		cached[dev].store(c, std::memory_order_relaxed);
+	return c;
+}
 
 /* Per-block counter slot layout (u64 each); slots summed by xdpgpu_stats. */
 enum {
@@ -54,6 +89,9 @@ struct RxArgs {
 	uint32_t force_generic;    /* 1: defer every frame (diagnostic)     */
 	uint32_t frags;            /* XDPGPU_CFG_FRAGS: skip the descriptors
 				    * of packets of several (frags.hip)     */
+	const unsigned long long *ndev; /* nullable: the frame count lives on
+				    * the device (the bounce batch of
+				    * frags.hip); n is then its upper bound */
 };
 
 /* ev (nullable): four events recorded before the fast kernel and after
@@ -81,16 +119,44 @@ struct FragArgs {
 	unsigned long long *blk;   /* per count/gather block: packets and
 				    * bounce bytes, then their prefixes     */
 	uint8_t *bounce;           /* gather, scatter */
+	uint64_t bounce_cap;       /* bytes; a packet past it is ABORTED    */
 	xdpgpu_desc *bdesc;        /* one per packet  */
 	uint2 *bmap;               /* first descriptor, descriptors         */
 	uint8_t *bverdict;
 	xdpgpu_result *bres;
 	uint8_t *btup;
-	uint32_t m;                /* scatter: packets */
+	uint32_t m;                /* upper bound of the packets (fc[0])    */
 };
 hipError_t launch_frag_count(const FragArgs &a, hipStream_t stream);
 hipError_t launch_frag_gather(const FragArgs &a, hipStream_t stream);
 hipError_t launch_frag_scatter(const FragArgs &a, hipStream_t stream);
+
+/* Host path write-back of ICMPv6 echo replies (xdpgpu_submit): for every
+ * descriptor of the batch with verdict TX, bytes [0, min(len, 64)) of its
+ * frame (the rewrite of process_packet, af_xdp_user.c:990-1037, touches
+ * bytes 0-57) go from the slot's device mirror to the host UMEM: straight
+ * through the mapped pinned UMEM (host non-null), or as compact records
+ * the host scatters after xdpgpu_wait.  Nothing else of the UMEM is
+ * written. */
+constexpr uint32_t kEchoBytes = 64;
+struct EchoRec {
+	uint64_t eff;              /* frame's UMEM offset                   */
+	uint32_t len;              /* bytes of b[] that are the frame's     */
+	uint32_t rsvd;
+	uint8_t b[kEchoBytes];
+};
+static_assert(sizeof(EchoRec) == 80, "echo record layout");
+struct EchoArgs {
+	const uint8_t *mirror;
+	uint8_t *host;             /* mapped host UMEM or null              */
+	uint64_t usize;
+	const xdpgpu_desc *desc;
+	const uint8_t *verdict;
+	uint32_t n;
+	EchoRec *rec;              /* host null: one record per TX frame    */
+	uint32_t *nrec;
+};
+hipError_t launch_echo_writeback(const EchoArgs &a, hipStream_t stream);
 
 /* nat64 static tables (v6_state_map and v4_reversemap, nat64_kern.c:17-46):
  * 4-way buckets of one 128-byte line, so a lookup touches one line; the

@@ -144,7 +144,8 @@ EXPORTS = (
     "xdpgpu_nat64_setup", "xdpgpu_nat64_dev", "xdpgpu_nat64_pool_config",
     "xdpgpu_device_count", "xdpgpu_last_error",
     "xdpgpu_abi_version", "xdpgpu_pool_size", "xdpgpu_pool_generate",
-    "xdpgpu_pool_spec_default", "xdpgpu_hints_dev",
+    "xdpgpu_pool_spec_default", "xdpgpu_hints_dev", "xdpgpu_host_alloc",
+    "xdpgpu_host_free",
 )
 
 # struct xdpgpu_hints (XDP hints in front of a frame)
@@ -189,6 +190,10 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.xdpgpu_pool_generate.argtypes = [C.POINTER(PoolSpec), vp, u64, vp, u32, vp]
     lib.xdpgpu_pool_spec_default.argtypes = [C.POINTER(PoolSpec), u32, u32, u64]
     lib.xdpgpu_pool_spec_default.restype = None
+    lib.xdpgpu_host_alloc.argtypes = [u64]
+    lib.xdpgpu_host_alloc.restype = vp
+    lib.xdpgpu_host_free.argtypes = [vp]
+    lib.xdpgpu_host_free.restype = None
     _lib = lib
     return lib
 
@@ -211,6 +216,34 @@ def _stream_handle(stream) -> Optional[int]:
     if isinstance(stream, int):
         return stream
     return stream.cuda_stream  # torch.cuda.Stream
+
+
+class HostBuffer:
+    """Page-locked host memory from xdpgpu_host_alloc, viewed as a numpy
+    array (the RX loop's descriptor and output arrays)."""
+
+    def __init__(self, n: int, dtype):
+        self.lib = load_library()
+        dt = np.dtype(dtype)
+        nbytes = max(n * dt.itemsize, 1)
+        p = self.lib.xdpgpu_host_alloc(nbytes)
+        if not p:
+            raise XdpGpuError(f"xdpgpu_host_alloc({nbytes}) failed")
+        self.p = p
+        buf = (C.c_uint8 * nbytes).from_address(p)
+        self.array = np.frombuffer(buf, np.uint8)[: n * dt.itemsize].view(dt)
+
+    def close(self) -> None:
+        if getattr(self, "p", None):
+            self.array = None
+            self.lib.xdpgpu_host_free(self.p)
+            self.p = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def device_count() -> int:

@@ -139,7 +139,9 @@ struct xdpgpu_cfg {
 	uint32_t tune;          /* kernel variant (diagnostic): bits 0-7 waves per
 				 * SIMD, bit 8 exception kernel keeps its
 				 * payload sums, bit 9 exception path only,
-				 * bits 10-11 bulk-kernel variant;
+				 * bits 10-11 bulk-kernel variant, bit 14
+				 * host path without the mapped UMEM (span
+				 * copies, compact echo records);
 				 * 0 = default */
 	uint32_t rsvd;
 };
@@ -168,7 +170,8 @@ void xdpgpu_fini(struct xdpgpu_ctx *ctx);
 
 /* Register the host UMEM (replaces xsk_umem__create's buffer argument,
  * af_xdp_user.c:433 / xdpsock.c:1013).  The memory stays owned by the caller;
- * it is pinned (hipHostRegister) and mirrored on the device. */
+ * it is pinned and mapped (hipHostRegister) and each in-flight slot keeps a
+ * device mirror of it.  -EBUSY while a slot is in flight. */
 int xdpgpu_register_umem(struct xdpgpu_ctx *ctx, void *base, uint64_t size,
 			 uint32_t chunk_size, uint32_t headroom, uint32_t flags);
 
@@ -177,24 +180,41 @@ int xdpgpu_register_umem(struct xdpgpu_ctx *ctx, void *base, uint64_t size,
  * and of the kernel-side verdict xdp_sock_prog() (af_xdp_kern.c:150-191).
  * Host buffers: descs[n] in, verdict[n] out (required), res[n] and
  * tuples[n] (format cfg.tuple_fmt) out, both nullable.  Synchronous.
- * With XDPGPU_CFG_ICMP6_ECHO, TX frames are rewritten in the host UMEM. */
+ * The UMEM is only read, except that with XDPGPU_CFG_ICMP6_ECHO the TX
+ * frames' first min(len, 64) bytes are rewritten in place (the reply of
+ * process_packet, af_xdp_user.c:990-1037); no other UMEM byte is written.
+ * Buffers from xdpgpu_host_alloc (pinned) are copied asynchronously;
+ * pageable ones are staged by the HIP runtime. */
 int xdpgpu_process(struct xdpgpu_ctx *ctx, const struct xdpgpu_desc *descs,
 		   uint32_t n, uint8_t *verdict, struct xdpgpu_result *res,
 		   void *tuples);
 
 /* Asynchronous form of xdpgpu_process on one of two in-flight slots
  * (double buffering of the RX batches).  Output buffers must stay valid
- * until xdpgpu_wait(ctx, slot) returns. */
+ * until xdpgpu_wait(ctx, slot) returns, and the batch's frames must not be
+ * handed back to the kernel (fill or TX ring) before it returns.  The two
+ * slots are independent: their batches may name the same UMEM frames
+ * (each slot reads its own device mirror), and each writes back only its
+ * own TX frames. */
 int xdpgpu_submit(struct xdpgpu_ctx *ctx, uint32_t slot,
 		  const struct xdpgpu_desc *descs, uint32_t n, uint8_t *verdict,
 		  struct xdpgpu_result *res, void *tuples);
 int xdpgpu_wait(struct xdpgpu_ctx *ctx, uint32_t slot);
 
+/* Page-locked host memory for descriptor and output arrays (the RX loop's
+ * per-batch buffers): xdpgpu_submit copies them without staging.  NULL on
+ * failure. */
+void *xdpgpu_host_alloc(uint64_t size);
+void xdpgpu_host_free(void *p);
+
 /* Device-resident form: every pointer is device memory (d_umem is written
  * only for ICMPv6 echo rewrites).  stream is a hipStream_t (NULL: the
- * context's stream).  Returns after the launch is enqueued.  d_umem must
- * be readable up to round_up(umem_size, 16) (the kernel loads 16-byte
- * aligned chunks and masks what lies past umem_size). */
+ * context's stream).  Returns after the launch is enqueued, also with
+ * XDPGPU_CFG_FRAGS (no host round trip).  d_umem must be readable up to
+ * round_up(umem_size, 16) (the kernel loads 16-byte aligned chunks and
+ * masks what lies past umem_size).  Launches of one context on different
+ * streams are ordered by the context (they share its scratch); launches
+ * on one stream run back to back. */
 int xdpgpu_process_dev(struct xdpgpu_ctx *ctx, void *d_umem,
 		       uint64_t umem_size, const struct xdpgpu_desc *d_descs,
 		       uint32_t n, uint8_t *d_verdict,

@@ -1,0 +1,219 @@
+# SPDX-License-Identifier: GPL-2.0
+"""The host path (xdpgpu_submit / xdpgpu_wait) as an RX loop drives it:
+two batches in flight, descriptors of a recycled fill ring (interleaved,
+shuffled, reused addresses, a batch that wraps round the ring), ICMPv6 echo
+replies written back.  SURVEY §8b ownership: the library writes only the TX
+frames' own bytes, so after every batch the whole host UMEM must equal the
+oracle run over the same batches in submission order, byte for byte.
+
+The batches two slots hold at once name disjoint frames (an AF_XDP
+application cannot hand a frame back to the kernel before its batch is
+done: af_xdp_user.c:1087-1106), but their UMEM spans overlap and later
+batches receive frames earlier batches rewrote."""
+import numpy as np
+import pytest
+
+import oracle
+import xdpgpu
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+ECHO = 0x7       # verify + echo + stats
+
+
+def ring_batches(nframes: int, nbatch: int, B: int, seed: int):
+    """Frame indices per batch: random frames not in the previous batch
+    (recycled, interleaved), one batch that wraps round the end of the
+    frame array, and one in strictly cyclic order."""
+    rng = np.random.default_rng(seed)
+    out = []
+    prev = np.zeros(0, np.int64)
+    for k in range(nbatch):
+        if k == nbatch // 3:
+            b = (np.arange(B) + nframes - B // 2) % nframes     # wraps
+        elif k == nbatch // 2:
+            b = (np.arange(B) * 7 + 3) % nframes                # strided
+        else:
+            free = np.setdiff1d(np.arange(nframes), prev)
+            b = rng.choice(free, B, replace=False)
+        if np.intersect1d(b, prev).size:
+            free = np.setdiff1d(np.arange(nframes), prev)
+            b = rng.choice(free, B, replace=False)
+        out.append(b)
+        prev = b
+    return out
+
+
+def run_ring(umem, descs, batches, flags, tune, fmt=xdpgpu.TUPLE_NET, pinned=True):
+    """Submit the batches alternately on the two slots, waiting for a slot
+    only when it is needed again; returns outputs per batch and stats."""
+    n_max = max(len(b) for b in batches)
+    tb = xdpgpu.TUPLE_BYTES[fmt]
+    outs = []
+    with xdpgpu.XdpGpu(0, flags, 0x9E3779B9, fmt, max_batch=n_max, tune=tune) as ctx:
+        ctx.register_umem(umem)
+        bufs = []
+        for slot in range(2):
+            if pinned:
+                d = xdpgpu.HostBuffer(n_max, xdpgpu.DESC_DTYPE)
+                v = xdpgpu.HostBuffer(n_max, np.uint8)
+                r = xdpgpu.HostBuffer(n_max, xdpgpu.RESULT_DTYPE)
+                t = xdpgpu.HostBuffer(n_max * tb, np.uint8)
+                bufs.append((d, v, r, t))
+            else:
+                bufs.append(tuple(type("B", (), {"array": a})() for a in (
+                    np.zeros(n_max, xdpgpu.DESC_DTYPE), np.zeros(n_max, np.uint8),
+                    np.zeros(n_max, xdpgpu.RESULT_DTYPE), np.zeros(n_max * tb, np.uint8))))
+        pending = [None, None]
+
+        def collect(slot):
+            k, m = pending[slot]
+            ctx.wait(slot)
+            d, v, r, t = bufs[slot]
+            outs[k] = (v.array[:m].copy(), r.array[:m].copy(), t.array[: m * tb].copy())
+            pending[slot] = None
+
+        for k, b in enumerate(batches):
+            slot = k & 1
+            if pending[slot] is not None:
+                collect(slot)
+            outs.append(None)
+            d, v, r, t = bufs[slot]
+            m = len(b)
+            d.array[:m] = descs[b]
+            ctx.submit(slot, d.array[:m], v.array[:m], r.array[:m], t.array[: m * tb])
+            pending[slot] = (k, m)
+        for slot in range(2):
+            if pending[slot] is not None:
+                collect(slot)
+        st = ctx.stats()
+        for bb in bufs:
+            for x in bb:
+                if hasattr(x, "close"):
+                    x.close()
+    return outs, st
+
+
+def oracle_ring(umem, descs, batches, flags, fmt=xdpgpu.TUPLE_NET):
+    outs = []
+    tot = None
+    for b in batches:
+        v, res, tup, st = oracle.process(umem, np.ascontiguousarray(descs[b]), flags,
+                                         0x9E3779B9, fmt)
+        outs.append((v, res.view(np.uint8).reshape(-1), tup))
+        if tot is None:
+            tot = st
+        else:
+            for key in ("frames", "bytes", "l3_bad", "l4_bad", "l4_absent", "frag"):
+                tot[key] += st[key]
+            tot["verdict"] = [a + c for a, c in zip(tot["verdict"], st["verdict"])]
+    return outs, tot
+
+
+@pytest.mark.parametrize("tune", [0, 1 << 14], ids=["mapped", "span_copy"])
+@pytest.mark.parametrize("pinned", [True, False], ids=["pinned", "pageable"])
+def test_ring_echo_two_slots(tune, pinned):
+    nframes = 16384
+    umem, descs, _ = xdpgpu.pool_generate(nframes, xdpgpu.POOL_UDP4, 128, 31,
+                                          ppm_echo6=300000)
+    batches = ring_batches(nframes, 24, 2048, 5)
+    host = umem.copy()
+    got, st = run_ring(host, descs, batches, ECHO, tune, pinned=pinned)
+    ou = umem.copy()
+    want, ost = oracle_ring(ou, descs, batches, ECHO)
+    ntx = 0
+    for k, (g, w) in enumerate(zip(got, want)):
+        np.testing.assert_array_equal(g[0], w[0], err_msg=f"batch {k} verdicts")
+        np.testing.assert_array_equal(g[1].view(np.uint8).reshape(-1), w[1],
+                                      err_msg=f"batch {k} results")
+        np.testing.assert_array_equal(g[2], w[2], err_msg=f"batch {k} tuples")
+        ntx += int((w[0] == xdpgpu.TX).sum())
+    assert ntx > 1000, "the pool must exercise the echo responder"
+    # replies that came round again are REDIRECTed (type 129 is no request)
+    assert np.array_equal(host, ou), "host UMEM differs from the oracle's"
+    assert st["frames"] == ost["frames"]
+    assert [st["verdict"][x] for x in xdpgpu.VERDICT_NAMES] == ost["verdict"]
+
+
+def test_tx_only_write_back():
+    """Bytes of frames outside the batch, and of non-TX frames, are never
+    written: the host changes them while the batch is in flight (as a NIC
+    refilling fill-ring frames would) and the changes survive."""
+    nframes = 4096
+    umem, descs, _ = xdpgpu.pool_generate(nframes, xdpgpu.POOL_UDP4, 128, 32,
+                                          ppm_echo6=500000)
+    host = umem.copy()
+    batch = np.arange(0, nframes, 2)                 # every other frame
+    with xdpgpu.XdpGpu(0, ECHO, 0, xdpgpu.TUPLE_V4, max_batch=len(batch)) as ctx:
+        ctx.register_umem(host)
+        d = np.ascontiguousarray(descs[batch])
+        v = np.zeros(len(batch), np.uint8)
+        ctx.submit(0, d, v)
+        # the odd frames are not in the batch: scribble on them now
+        for f in range(1, nframes, 2):
+            a = int(descs["addr"][f])
+            host[a:a + 64] = 0xA5
+        ctx.wait(0)
+    ou = umem.copy()
+    ov, _, _, _ = oracle.process(ou, d, ECHO, 0, 1)
+    np.testing.assert_array_equal(v, ov)
+    for f in range(1, nframes, 2):
+        a = int(descs["addr"][f])
+        ou[a:a + 64] = 0xA5
+    assert np.array_equal(host, ou)
+
+
+def test_frags_ring_host_path():
+    """Multi-buffer packets on the host path, two slots in flight, echo on:
+    every fragment's bytes only as the oracle writes them."""
+    import test_frags as TF
+    umem, descs = TF.pool("echo6")
+    u2, d2, _ = TF.split_pool(umem, descs, 3)
+    # packets = runs of descriptors; batches of whole packets
+    heads = np.nonzero(np.r_[True, (d2["options"][:-1] & xdpgpu.PKT_CONTD) == 0])[0]
+    bounds = np.r_[heads, len(d2)]
+    per = 64
+    batches = []
+    for p0 in range(0, len(heads), per):
+        batches.append(np.arange(bounds[p0], bounds[min(p0 + per, len(heads))]))
+    host = u2.copy()
+    got, st = run_ring(host, d2, batches, ECHO | xdpgpu.CFG_FRAGS, 0,
+                       fmt=xdpgpu.TUPLE_V4)
+    ou = u2.copy()
+    want, ost = oracle_ring(ou, d2, batches, ECHO | xdpgpu.CFG_FRAGS, fmt=xdpgpu.TUPLE_V4)
+    for k, (g, w) in enumerate(zip(got, want)):
+        np.testing.assert_array_equal(g[0], w[0], err_msg=f"batch {k} verdicts")
+    assert np.array_equal(host, ou)
+    assert st["frames"] == ost["frames"]
+
+
+def test_process_dev_two_streams():
+    """Launches of one context on two streams share its scratch (deferral
+    lists, counts): the context orders them, and each batch's outputs
+    equal the oracle's.  IMIX defers many frames, so an unordered pair of
+    launches would mix the lists."""
+    from test_gpu_parity import to_dev
+    pools = [xdpgpu.pool_generate(200000, xdpgpu.POOL_IMIX, 64, s) for s in (41, 42)]
+    want = [oracle.process(u.copy(), d, 0x5, 0, 2)[:3] for u, d, _ in pools]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    with xdpgpu.XdpGpu(0, 0x5, 0, xdpgpu.TUPLE_NET) as ctx:
+        bufs = []
+        for u, d, _ in pools:
+            n = len(d)
+            bufs.append((to_dev(u), u.nbytes, to_dev(d, 16), n,
+                         torch.empty(n, dtype=torch.uint8, device="cuda:0"),
+                         torch.empty(n * 16, dtype=torch.uint8, device="cuda:0"),
+                         torch.empty(n * 44, dtype=torch.uint8, device="cuda:0")))
+        torch.cuda.synchronize()
+        for rep in range(6):
+            k = rep & 1
+            du, us, dd, n, dv, dr, dt = bufs[k]
+            ctx.process_dev(du, us, dd, n, dv, dr, dt, stream=streams[k])
+        torch.cuda.synchronize()
+        for k in range(2):
+            du, us, dd, n, dv, dr, dt = bufs[k]
+            wv, wres, wtup = want[k]
+            np.testing.assert_array_equal(dv.cpu().numpy(), wv)
+            np.testing.assert_array_equal(dr.cpu().numpy(), wres.view(np.uint8).reshape(-1))
+            np.testing.assert_array_equal(dt.cpu().numpy(), wtup)
