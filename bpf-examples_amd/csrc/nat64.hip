@@ -1088,6 +1088,7 @@ __global__ __launch_bounds__(kBlockN) void xdp_nat64_fast_kernel(Nat64Args a)
 		const bool active = i < a.n;
 		const uint4 dv = dcur;
 		uint32_t F[16];
+		lds_dma_landed();
 		{
 			const int sw = (lane >> 2) & 3;
 #pragma unroll
@@ -1099,7 +1100,7 @@ __global__ __launch_bounds__(kBlockN) void xdp_nat64_fast_kernel(Nat64Args a)
 				F[4 * c + 3] = v.w;
 			}
 		}
-		__builtin_amdgcn_s_waitcnt(0xc07f);   /* lgkmcnt(0) */
+		lds_reads_done();
 		__builtin_amdgcn_wave_barrier();
 		dcur = dnext;
 		issue(dcur, t + nwaves < ntiles);

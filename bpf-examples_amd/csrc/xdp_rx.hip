@@ -37,6 +37,25 @@ constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = kWave * kWavesPerBlock;
 
+/* Diagnostic builds (-DXDPGPU_DBG, tools/dbg_build.sh): the accesses of the
+ * double-buffered kernel and its tail are bounds-checked; a violation is
+ * counted (g_dbg[2 code]) with its value (g_dbg[2 code + 1]) and the access
+ * is skipped.  Read by xdpgpu_debug_read. */
+#ifdef XDPGPU_DBG
+__device__ unsigned long long g_dbg[64];
+__device__ __forceinline__ bool dbg_bad(bool bad, uint32_t code, uint64_t val)
+{
+	if (bad) {
+		atomicAdd(&g_dbg[2 * code], 1ull);
+		atomicExch(&g_dbg[2 * code + 1], (unsigned long long)val);
+	}
+	return bad;
+}
+#define DBG_BAD(c, code, v) dbg_bad((c), (code), (uint64_t)(v))
+#else
+#define DBG_BAD(c, code, v) false
+#endif
+
 /* ------------------------------------------------------------------ */
 /* one's-complement helpers                                            */
 
@@ -1051,6 +1070,8 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 	} else {
 		i = reinterpret_cast<const uint32_t *>(list)[act ? lane : 0];
 	}
+	if (DBG_BAD(i >= a.n, GEN ? 3 : 2, i))
+		i = 0;
 	const uint4 dv = *reinterpret_cast<const uint4 *>(a.desc + i);
 	uint4 rv = *reinterpret_cast<const uint4 *>(a.res + i);
 	const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
@@ -1192,22 +1213,764 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
  * payload sum here and go to the bulk list; every other frame is deferred
  * to the exception kernel.
  */
+/* Hardware hazards the compiler cannot see in inline asm (its hazard
+ * recognizer only knows the memory instructions it emitted itself):
+ *  - a VALU write of an SGPR (v_readfirstlane of a base address) followed
+ *    by a VMEM instruction reading that SGPR needs 5 wait states: every
+ *    scalar-base store below starts with s_nop 6 (7, a margin over 5);
+ *  - a VALU write of the data VGPRs of a preceding store of more than 8
+ *    bytes: the compiler puts 2 wait states there on gfx950 (one was seen
+ *    to corrupt the data of the last lanes of 16-lane groups), the 12- and
+ *    16-byte stores end with s_nop 2 (3).
+ */
+
+/* Output stores of the fast kernels' tile loop, as inline asm.  The
+ * compiler's wait insertion treats vmcnt as out of order once loads and
+ * stores are both pending (on gfx9-class targets they share the counter),
+ * so every wait it places for a descriptor load behind a store would be a
+ * full vmcnt(0); the hardware retires them in issue order
+ * (MI355X_MICROARCH.md), and stores need no wait of their own here.
+ * Asm stores are invisible to that tracking, and its waits for the loads
+ * it sees stay counted.  (A counted wait is then also a wait for older
+ * asm stores: it only ever waits more, never less.)  The kernels that read
+ * these bytes back (rx_tail) wait with vmcnt(0) first. */
+__device__ __forceinline__ void st_asm_b8(void *p, uint32_t v)
+{
+	asm volatile("global_store_byte %0, %1, off" :: "v"(p), "v"(v) : "memory");
+}
+
+__device__ __forceinline__ void st_asm_b32(void *p, uint32_t v)
+{
+	asm volatile("global_store_dword %0, %1, off" :: "v"(p), "v"(v) : "memory");
+}
+
+__device__ __forceinline__ void st_asm_b128_nt(void *p, uint4 r)
+{
+	const v4u_t v = {r.x, r.y, r.z, r.w};
+	asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 2" :: "v"(p), "v"(v) : "memory");
+}
+
+__device__ __forceinline__ void st_asm_b128(void *p, uint4 r)
+{
+	const v4u_t v = {r.x, r.y, r.z, r.w};
+	asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 2" :: "v"(p), "v"(v) : "memory");
+}
+
+typedef unsigned int v3u_t __attribute__((ext_vector_type(3)));
+__device__ __forceinline__ void st_asm_b96(void *p, uint32_t x, uint32_t y, uint32_t z)
+{
+	const v3u_t v = {x, y, z};
+	asm volatile("global_store_dwordx3 %0, %1, off\n\ts_nop 2" :: "v"(p), "v"(v) : "memory");
+}
+
+/* Wave-uniform 64-bit value in SGPRs.  __builtin_amdgcn_readfirstlane
+ * returns int: each half goes through uint32_t before widening, or the low
+ * half would be sign-extended over the high one. */
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v)
+{
+	const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+	const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+	return ((uint64_t)hi << 32) | lo;
+}
+
+/* A wave-uniform pointer in SGPRs (the compiler cannot see that a value
+ * derived from the wave index is uniform). */
+template <typename T>
+__device__ __forceinline__ T *uniform_ptr(T *p)
+{
+	return (T *)(uintptr_t)uniform_u64((uint64_t)(uintptr_t)p);
+}
+
+/* The same in the scalar-base form: a wave-uniform 64-bit base in SGPRs
+ * and a 32-bit per-lane byte offset, so no 64-bit address is held in
+ * VGPRs across the loop. */
+__device__ __forceinline__ void st_asm_sb8(const void *base, uint32_t off, uint32_t v)
+{
+	asm volatile("s_nop 6\n\tglobal_store_byte %0, %1, %2" :: "v"(off), "v"(v), "s"(base)
+		     : "memory");
+}
+
+__device__ __forceinline__ void st_asm_sb32(const void *base, uint32_t off, uint32_t v)
+{
+	asm volatile("s_nop 6\n\tglobal_store_dword %0, %1, %2" :: "v"(off), "v"(v), "s"(base)
+		     : "memory");
+}
+
+__device__ __forceinline__ void st_asm_sb128(const void *base, uint32_t off, uint4 r, bool nt)
+{
+	const v4u_t v = {r.x, r.y, r.z, r.w};
+	if (nt)
+		asm volatile("s_nop 6\n\tglobal_store_dwordx4 %0, %1, %2 nt\n\ts_nop 2"
+			     :: "v"(off), "v"(v), "s"(base) : "memory");
+	else
+		asm volatile("s_nop 6\n\tglobal_store_dwordx4 %0, %1, %2\n\ts_nop 2"
+			     :: "v"(off), "v"(v), "s"(base) : "memory");
+}
+
+__device__ __forceinline__ void st_asm_sb96(const void *base, uint32_t off, uint32_t x,
+					    uint32_t y, uint32_t z)
+{
+	const v3u_t v = {x, y, z};
+	asm volatile("s_nop 6\n\tglobal_store_dwordx3 %0, %1, %2\n\ts_nop 2"
+		     :: "v"(off), "v"(v), "s"(base) : "memory");
+}
+
+/* Per-wave state of the fast kernels' tile loop. */
+struct FastWave {
+	uint32_t cnt[CNT_FRAG + 1];       /* wave-uniform counters         */
+	uint64_t my_bytes;                /* per lane                      */
+	uint32_t xq_n, xout, bq_n, bout;  /* queued / flushed deferrals
+					   * (uniform): exception, bulk    */
+	uint32_t *xq, *bq;                /* LDS queues, 2 x 64 entries    */
+	uint32_t *xl, *bl;                /* this wave's list regions      */
+};
+
+/* Append the frames of the lanes with want set to a list: LDS queue in
+ * lane order, flushed 64 entries at a time to this wave's region. */
+__device__ __forceinline__ void defer_append(bool want, uint64_t i, uint32_t *q,
+					     uint32_t &qn, uint32_t *gl,
+					     uint32_t &gout, int lane)
+{
+	const uint64_t dm = __ballot(want);
+	if (!dm)
+		return;
+	const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+		(uint32_t)(dm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0));
+	if (want)
+		q[qn + rank] = (uint32_t)i;
+	qn += (uint32_t)__popcll(dm);
+	if (qn >= (uint32_t)kWave) {
+		__builtin_amdgcn_wave_barrier();
+		st_asm_b32(gl + gout + lane, q[lane]);
+		gout += kWave;
+		const uint32_t rest = q[kWave + lane];
+		__builtin_amdgcn_wave_barrier();
+		q[lane] = rest;
+		qn -= kWave;
+	}
+}
+
+/*
+ * One tile of the fast kernels, after its 64-byte windows are in F:
+ * fast-shape classification, deferral of the other frames, and for fast
+ * frames the checksums, flow key, hash, tuple, record, verdict and
+ * counters.  Frames of the fast shape (Ethernet + 0..2 VLAN tags + IPv4
+ * ihl 5, not a fragment, + UDP/TCP) whose checksum range lies in the window
+ * are finished here; fast-shape frames with a longer range get everything
+ * but the payload sum and go to the bulk list; every other frame goes to
+ * the exception list.
+ */
+/* A fast tile's outputs, kept in registers from its step to the next one,
+ * whose stores they are (xdp_rx_db_kernel).  The flow key of a fast-shape
+ * frame varies only in saddr, daddr, ports and protocol (IPv4 mapped into
+ * ::ffff:0:0/96), so the record, the verdict and the V4 or network_tuple
+ * layouts all rebuild from these words. */
+struct TileOut {
+	uint64_t t0;       /* first frame of the tile (wave-uniform)        */
+	uint32_t li;       /* this lane's frame in the tile                 */
+	uint32_t fl;       /* bit 0: verdict store, bit 1: record and tuple */
+	uint32_t verdict;
+	uint32_t sa, da, ports, proto, vid;
+	uint4 rec;
+};
+
+/* The stores of a TileOut: buffer stores over the tile's records, a lane
+ * with nothing to store at an offset past the resource's size (dropped by
+ * the hardware); no branches but the configuration's (uniform). */
+__device__ __forceinline__ void store_tile(const RxArgs &a, const TileOut &o)
+{
+	constexpr uint32_t kOff = 0x80000000u;
+	constexpr int kFmt = 0x00020000;      /* gfx9 raw buffer dword 3 */
+	if (DBG_BAD(o.t0 >= a.n || (o.t0 & (kWave - 1)), 9, o.t0))
+		return;
+	const __amdgpu_buffer_rsrc_t rv =
+		__builtin_amdgcn_make_buffer_rsrc(a.verdict + o.t0, 0, kWave, kFmt);
+	__builtin_amdgcn_raw_buffer_store_b8((uint8_t)o.verdict, rv,
+					     (o.fl & 1) ? o.li : kOff, 0, 0);
+	const bool out = o.fl & 2;
+	if (a.res) {
+		const __amdgpu_buffer_rsrc_t rr =
+			__builtin_amdgcn_make_buffer_rsrc(a.res + o.t0, 0, 16 * kWave, kFmt);
+		__builtin_amdgcn_raw_buffer_store_b128(
+			(v4u_t){o.rec.x, o.rec.y, o.rec.z, o.rec.w}, rr,
+			out ? 16 * o.li : kOff, 0, 2 /* nt */);
+	}
+	if (a.tup && a.tuple_fmt == XDPGPU_TUPLE_V4) {
+		const __amdgpu_buffer_rsrc_t rt =
+			__builtin_amdgcn_make_buffer_rsrc(a.tup + 16 * o.t0, 0, 16 * kWave, kFmt);
+		__builtin_amdgcn_raw_buffer_store_b128(
+			(v4u_t){o.sa, o.da, o.ports, o.proto | (2u << 8) | (o.vid << 16)}, rt,
+			out ? 16 * o.li : kOff, 0, 2);
+	} else if (a.tup && a.tuple_fmt == XDPGPU_TUPLE_NET) {
+		const __amdgpu_buffer_rsrc_t rt =
+			__builtin_amdgcn_make_buffer_rsrc(a.tup + 44 * o.t0, 0, 44 * kWave, kFmt);
+		const uint32_t b = out ? 44 * o.li : kOff;
+		__builtin_amdgcn_raw_buffer_store_b128((v4u_t){0u, 0u, 0xffff0000u, o.sa}, rt,
+						       b, 0, 2);
+		__builtin_amdgcn_raw_buffer_store_b128((v4u_t){o.ports & 0xffff, 0u, 0u,
+							       0xffff0000u}, rt,
+						       out ? b + 16 : kOff, 0, 2);
+		__builtin_amdgcn_raw_buffer_store_b96((v3u_t){o.da, o.ports >> 16,
+							     o.proto | (2u << 16)}, rt,
+						      out ? b + 32 : kOff, 0, 2);
+	}
+}
+
+/* Append without an LDS queue: each deferred lane stores its index at its
+ * rank (a partial line per store; deferrals are rare on the fast shapes). */
+__device__ __forceinline__ void defer_direct(bool want, uint64_t i, uint32_t *gl,
+					     uint32_t &gout, int lane, uint32_t xcap)
+{
+	const uint64_t dm = __ballot(want);
+	if (!dm)
+		return;
+	const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+		(uint32_t)(dm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0));
+	if (want && !DBG_BAD(gout + rank >= xcap, 7, gout + rank))
+		st_asm_sb32(uniform_ptr(gl), (gout + rank) * 4u, (uint32_t)i);
+	gout += (uint32_t)__popcll(dm);
+}
+
+template <bool LQ, bool ST = true>
+__device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[18],
+					  uint4 dv, uint64_t i, bool active,
+					  bool dma, int lane, FastWave &w,
+					  TileOut *to = nullptr)
+{
+	const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
+	const uint32_t len = dv.z;
+	const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
+	const bool staged = dma & active & (len >= 14) & ((uint64_t)len <= a.usize) &
+			    (eff <= a.usize - len) & !(eff & 15) &
+			    (eff + 64 <= ((a.usize + 15) & ~15ull));
+
+	/* 2. fast-shape classification, branch free (bitwise &/| on
+	 * flags, selects).  r[j] = frame dword j + nv */
+	const bool v1 = le_is_vlan(F[3] & 0xffff);
+	const bool v2 = v1 & le_is_vlan(F[4] & 0xffff);
+	const uint32_t nv = (uint32_t)v1 + (uint32_t)v2;
+	/* masks, not selects: a select chain over F is turned into a
+	 * dynamically indexed private array (scratch) by the compiler */
+	const uint32_t m2 = 0u - (uint32_t)v2;
+	const uint32_t m1 = (0u - (uint32_t)v1) & ~m2;
+	const uint32_t m0 = ~(m1 | m2);
+	uint32_t r[16];
+#pragma unroll
+	for (int j = 3; j < 16; j++)
+		r[j] = (F[j] & m0) | (F[j + 1] & m1) | (F[j + 2] & m2);
+	const uint32_t l3 = 14 + 4 * nv, l4 = l3 + 20;
+	const uint32_t tot = bswap16(r[4] & 0xffff);
+	const uint32_t proto = r[5] >> 24;
+	const bool udp = proto == 17;
+	const uint32_t thl = ((r[11] >> 20) & 0xf) * 4;
+	const uint32_t cl = udp ? bswap16(r[9] >> 16) : tot - 20;
+	const bool ok_udp = (len >= l4 + 8) & (cl >= 8) & (l4 + cl <= l3 + tot);
+	const bool ok_tcp = (len >= l4 + 20) & (thl >= 20) & (l4 + thl <= len) &
+			    (cl >= thl);
+	bool fast = (!a.force_generic) & staged &
+		    ((r[3] & 0x00ffffffu) == 0x00450008u) &
+		    ((r[5] & 0xff3fu) == 0) & (udp | (proto == 6)) &
+		    (tot >= 20) & (l3 + tot <= len) & (udp ? ok_udp : ok_tcp);
+	/* a checksum range (with udp_csum's odd over-read byte) that ends
+	 * past the window: the bulk kernel adds the payload sum */
+	const bool shape = fast;
+	fast = shape & (l4 + cl + (cl & 1) <= 64u);
+	const bool bulk = shape & !fast & (a.res != nullptr);
+
+	/* 3. defer the frames of other shapes to the exception list and
+	 * the long ones to the bulk list of this wave */
+	if constexpr (LQ) {
+		defer_append(active && !fast && !bulk, i, w.xq, w.xq_n, w.xl, w.xout, lane);
+		defer_append(bulk, i, w.bq, w.bq_n, w.bl, w.bout, lane);
+	} else {
+		defer_direct(active && !fast && !bulk, i, w.xl, w.xout, lane, a.xregion);
+		defer_direct(bulk, i, w.bl, w.bout, lane, a.xregion);
+	}
+
+	/* 4. fast frames: flow key, hash, tuple, checksums, verdict */
+	const uint32_t sa = (r[6] >> 16) | (r[7] << 16);
+	const uint32_t da = (r[7] >> 16) | (r[8] << 16);
+	const uint32_t ports = (r[8] >> 16) | (r[9] << 16);
+	/* IPv4 header sum, check word (r6 low half) excluded */
+	const uint64_t s3 = (uint64_t)(r[3] & 0xffff0000u) + r[4] + r[5] +
+			    (r[6] & 0xffff0000u) + r[7] + (r[8] & 0xffffu);
+	const uint32_t c3 = r[6] & 0xffff;
+	const uint32_t c4 = udp ? (r[10] & 0xffff) : (r[12] >> 16);
+	/* L4 sum over [34, end) of the shifted frame with the pseudo
+	 * header, check word excluded; udp_csum's odd-length over-read
+	 * byte included (lib_checksum.h:142-179).  For a bulk frame the
+	 * window part: frame bytes [l4, 64) (F[16], F[17] are zero). */
+	const int32_t e = (int32_t)(34 + cl + (cl & 1));
+	uint64_t s4 = (uint64_t)(r[8] & 0xffff0000u) + sa + da +
+		      ((uint64_t)(proto + cl) << 8);
+#pragma unroll
+	for (int j = 9; j < 16; j++) {
+		uint32_t m = first_bytes(e - 4 * j);
+		if (j == 10)
+			m &= udp ? 0xffff0000u : 0xffffffffu;
+		if (j == 12)
+			m &= udp ? 0xffffffffu : 0x0000ffffu;
+		s4 += r[j] & m;
+	}
+	const uint32_t l3c = ~fold16(s3) & 0xffff;
+	const bool l3_ok = fold16(s3 + c3) == 0xffff;
+	const uint32_t sum4 = fold16(s4);
+	const uint32_t l4c = ~sum4 & 0xffff;
+	const bool absent = udp && c4 == 0;
+	const bool l4_ok = absent || (~fold16((uint64_t)sum4 + c4) & 0xffff) == 0;
+	const bool drop = (a.flags & XDPGPU_CFG_VERIFY_CSUM) && (!l3_ok || !l4_ok);
+	uint32_t key[11] = {0, 0, 0xffff0000u, sa, ports & 0xffff,
+			    0, 0, 0xffff0000u, da, ports >> 16,
+			    proto | (2u << 16)};
+	/* a bulk frame's record carries its window sum in the l4_csum field
+	 * and its check word in l4_off until the bulk pass completes it */
+	uint4 rec;
+	rec.x = jhash_key44(key, a.initval);
+	rec.y = l3c | ((fast ? l4c : sum4) << 16);
+	rec.z = XDPGPU_F_IP | XDPGPU_F_L4 | (nv ? XDPGPU_F_VLAN : 0u) |
+		(l3_ok ? XDPGPU_F_L3_OK : 0u) |
+		(fast && l4_ok ? XDPGPU_F_L4_OK : 0u) |
+		(fast && absent ? XDPGPU_F_L4_ABSENT : 0u) |
+		(proto << 8) | (l3 << 16) | (nv << 24);
+	rec.w = (fast ? l4 : c4) | (cl << 16);
+	const uint32_t vid = nv ? (bswap16(F[3] >> 16) & 0x0fff) : 0u;
+	const uint4 tv4 = make_uint4(sa, da, ports, proto | (2u << 8) | (vid << 16));
+	const bool out = fast || bulk;
+	if constexpr (LQ) {
+		if (out) {
+			/* the tile's first frame index (wave-uniform): scalar
+			 * bases, per-lane offsets of at most 64 records */
+			const uint64_t t0 = uniform_u64(i);
+			uint32_t li = (uint32_t)(i - t0);
+			if (fast)
+				st_asm_sb8(a.verdict + t0, li,
+					   drop ? XDPGPU_DROP : XDPGPU_REDIRECT);
+			if (a.res)
+				st_asm_sb128(a.res + t0, 16 * li, rec, true);
+			if (a.tup) {
+				if (a.tuple_fmt == XDPGPU_TUPLE_V4) {
+					st_asm_sb128(a.tup + 16 * t0, 16 * li, tv4, true);
+				} else if (a.tuple_fmt == XDPGPU_TUPLE_NET) {
+					/* 44-byte records: dword aligned */
+					const uint8_t *tb = a.tup + 44 * t0;
+					st_asm_sb128(tb, 44 * li,
+						     make_uint4(key[0], key[1], key[2], key[3]),
+						     false);
+					st_asm_sb128(tb, 44 * li + 16,
+						     make_uint4(key[4], key[5], key[6], key[7]),
+						     false);
+					st_asm_sb96(tb, 44 * li + 32, key[8], key[9], key[10]);
+				}
+			}
+		}
+	} else if constexpr (ST) {
+		/* the outputs, stored by the next step (store_tile) */
+		to->t0 = uniform_u64(i);   /* all lanes active: lane 0 */
+		to->li = (uint32_t)(i - to->t0);
+		to->fl = (fast ? 1u : 0u) | (out ? 2u : 0u);
+		to->verdict = drop ? XDPGPU_DROP : XDPGPU_REDIRECT;
+		to->sa = sa;
+		to->da = da;
+		to->ports = ports;
+		to->proto = proto;
+		to->vid = vid;
+		to->rec = rec;
+	}
+	w.my_bytes += fast ? len : 0;
+	/* counters (wave-uniform: ballots outside divergent code) */
+	if (a.stats) {
+		w.cnt[CNT_FRAMES] += __popcll(__ballot(fast));
+		w.cnt[CNT_VERDICT0 + XDPGPU_DROP] += __popcll(__ballot(fast && drop));
+		w.cnt[CNT_VERDICT0 + XDPGPU_REDIRECT] += __popcll(__ballot(fast && !drop));
+		w.cnt[CNT_L3_BAD] += __popcll(__ballot(fast && !l3_ok));
+		w.cnt[CNT_L4_BAD] += __popcll(__ballot(fast && !l4_ok));
+		w.cnt[CNT_L4_ABSENT] += __popcll(__ballot(fast && absent));
+	}
+}
+
+/* End of a fast kernel's tile loop: the queued deferrals to the wave's
+ * list regions and the list lengths to global memory. */
+__device__ __forceinline__ void rx_flush_lists(const RxArgs &a, const FastWave &w,
+					       uint64_t wgid, int lane)
+{
+	__builtin_amdgcn_wave_barrier();
+	if ((uint32_t)lane < w.xq_n)
+		w.xl[w.xout + lane] = w.xq[lane];
+	if ((uint32_t)lane < w.bq_n)
+		w.bl[w.bout + lane] = w.bq[lane];
+	if (lane == 0) {
+		a.xcount[wgid] = w.xout + w.xq_n;
+		a.bcount[wgid] = w.bout + w.bq_n;
+		a.ycount[wgid] = 0;   /* filled by the exception pass */
+	}
+}
+
+/* Counters of a wave into its block's LDS slot (lane 0; the block's
+ * slot goes to global memory in block_stats_flush). */
+__device__ __forceinline__ void wave_stats_to_lds(const RxArgs &a,
+						  unsigned long long *blk_cnt,
+						  const uint32_t (&cnt)[CNT_FRAG + 1],
+						  uint64_t my_bytes, int lane)
+{
+	if (!a.stats)
+		return;
+	const uint64_t bytes = wave_sum64(my_bytes);
+	if (lane == 0) {
+		atomicAdd(&blk_cnt[CNT_BYTES], (unsigned long long)bytes);
+#pragma unroll
+		for (int k = 0; k <= CNT_FRAG; k++)
+			if (k != CNT_BYTES && cnt[k])
+				atomicAdd(&blk_cnt[k], (unsigned long long)cnt[k]);
+	}
+}
+
+/*
+ * Tail phase of the double-buffered fast kernel: the wave finishes its own
+ * deferred frames in the order of the separate kernels (exception batches,
+ * then the bulk list, then the exception frames' deferred payload sums),
+ * reusing its LDS: win (64 rows of 17 dwords) and gtab (64 u64) for the
+ * exception batches, meta (64 uint4) and part (256 uint4) for the bulk
+ * batches.  Its lists were written by this wave alone: a vmcnt(0) wait
+ * before each pass orders those stores before these loads.
+ */
+__device__ __forceinline__ void rx_tail(const RxArgs &a, const FastWave &w,
+					uint64_t wgid, int lane, uint32_t *win,
+					uint64_t *gtab, uint4 *meta, uint4 *part4,
+					uint32_t (&cnt)[CNT_FRAG + 1], uint64_t &my_bytes)
+{
+	const uint32_t xc = w.xout + w.xq_n, bc = w.bout + w.bq_n;
+	uint4 *yl = a.ylist + wgid * a.xregion;
+	uint32_t *yc = a.ycount + wgid;
+	lds_dma_landed();
+	for (uint32_t b = 0; b < xc; b += kWave) {
+		const bool act = b + lane < xc;
+		uint64_t i = act ? w.xl[b + lane] : 0;
+		const bool bad = act && DBG_BAD(i >= a.n, 1, i);
+		i = bad ? 0 : i;
+		generic_batch<64>(a, win, gtab, lane, i, act && !bad, yl, yc, cnt, my_bytes);
+	}
+	lds_dma_landed();
+	for (uint32_t b = 0; b < bc; b += kWave)
+		bulk_batch<4, true, false, 16>(a, meta, part4, lane, w.bl + b,
+					       bc - b < (uint32_t)kWave ? bc - b : kWave,
+					       cnt, my_bytes);
+	/* the count the exception batches' atomics left (read at the L2,
+	 * where they were made) */
+	uint32_t ycn = 0;
+	if (lane == 0)
+		ycn = atomicAdd(yc, 0u);
+	ycn = __builtin_amdgcn_readfirstlane(ycn);
+	for (uint32_t b = 0; b < ycn; b += kWave)
+		bulk_batch<4, true, true, 16>(a, meta, part4, lane, yl + b,
+					      ycn - b < (uint32_t)kWave ? ycn - b : kWave,
+					      cnt, my_bytes);
+}
+
+/*
+ * Fast kernel, double-buffered (the default RX launch).
+ *
+ * Each wave keeps two tiles' window DMAs in flight: tile k is read from
+ * its LDS buffer while tile k+1's DMA is landing in the other one, and
+ * tile k+2's DMA goes into tile k's buffer once tile k is done.  The two
+ * buffers are distinct __shared__ variables, so the compiler's LDS-DMA
+ * tracking tells them apart; the explicit wait is a counted vmcnt:
+ *
+ *   per iteration, in order: [wait] [read buffer k] [tile k: compute,
+ *   deferrals, stores] [DMA tile k+2 -> buffer k (4 ops)] [descriptor
+ *   load, tile k+3 (1 op)]
+ *
+ * so at the start of iteration k at least 6 vector-memory ops (the
+ * descriptor load of iteration k-2, the 4 DMA ops and the descriptor load
+ * of iteration k-1) were issued after tile k's DMA; vmcnt counts loads,
+ * stores and LDS-DMA together in issue order (MI355X_MICROARCH.md), so
+ * vmcnt(6) means tile k's windows have landed, while tile k+1's DMA may
+ * still be in flight.  Every DMA and descriptor load is issued
+ * unconditionally (past the end they read the UMEM's first 64 bytes and
+ * the last descriptor), which keeps the count a lower bound.
+ *
+ * 4 waves per SIMD (the two buffers need 160 KB of LDS per CU at that
+ * occupancy), 128 VGPRs: room for the tail phase (rx_tail) inline, so
+ * one launch does the whole batch.
+ */
+/* One tile's inputs out of the double-buffered LDS, in one asm block:
+ * the counted wait vmcnt(5) (see xdp_rx_db_kernel), this lane's 64-byte
+ * window
+ * (four conflict-free ds_read_b128) and the descriptor of the tile two
+ * steps ahead (one ds_read_b128), then the wait for the reads.  In asm
+ * because no compiler-visible access may touch LDS the DMA writes: its
+ * wait insertion would add vmcnt(0) (it treats LDS-DMA and other vector
+ * memory ops as completing out of order), and in one block so that no
+ * use of the results is scheduled before their lgkmcnt wait. */
+typedef __attribute__((address_space(3))) uint4 lds_uint4_t;
+__device__ __forceinline__ void read_tile_db(const uint4 *win, const uint4 *dslot,
+					     int lane, uint32_t (&F)[18], uint4 &dn)
+{
+	const int sw = (lane >> 2) & 3;
+	const lds_uint4_t *lw = (const lds_uint4_t *)win;
+	const lds_uint4_t *ld = (const lds_uint4_t *)dslot;
+	const uint32_t a0 = (uint32_t)(uintptr_t)(lw + 4 * lane + (0 ^ sw));
+	const uint32_t a1 = (uint32_t)(uintptr_t)(lw + 4 * lane + (1 ^ sw));
+	const uint32_t a2 = (uint32_t)(uintptr_t)(lw + 4 * lane + (2 ^ sw));
+	const uint32_t a3 = (uint32_t)(uintptr_t)(lw + 4 * lane + (3 ^ sw));
+	const uint32_t ad = (uint32_t)(uintptr_t)(ld + lane);
+	v4u_t v0, v1, v2, v3, vd;
+	asm volatile("s_waitcnt vmcnt(5)\n\t"
+		     "ds_read_b128 %0, %5\n\t"
+		     "ds_read_b128 %1, %6\n\t"
+		     "ds_read_b128 %2, %7\n\t"
+		     "ds_read_b128 %3, %8\n\t"
+		     "ds_read_b128 %4, %9\n\t"
+		     "s_waitcnt lgkmcnt(0)"
+		     : "=&v"(v0), "=&v"(v1), "=&v"(v2), "=&v"(v3), "=&v"(vd)
+		     : "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(ad)
+		     : "memory");
+	F[0] = v0.x; F[1] = v0.y; F[2] = v0.z; F[3] = v0.w;
+	F[4] = v1.x; F[5] = v1.y; F[6] = v1.z; F[7] = v1.w;
+	F[8] = v2.x; F[9] = v2.y; F[10] = v2.z; F[11] = v2.w;
+	F[12] = v3.x; F[13] = v3.y; F[14] = v3.z; F[15] = v3.w;
+	F[16] = F[17] = 0;
+	dn = make_uint4(vd.x, vd.y, vd.z, vd.w);
+}
+
+/* Per-wave LDS of the double-buffered kernel, in uint4: two window buffers
+ * (256 each) and two descriptor slots (64 each).  16 waves per CU x 10 KiB
+ * = the CU's 160 KiB. */
+constexpr int kDbWave = 2 * 256 + 2 * 64;
+
+/*
+ * Fast kernel, double-buffered: the default RX launch.
+ *
+ * Each wave keeps two tiles in flight: the window DMA of tile k+1 (and the
+ * descriptor DMA of tiles k+2, k+3) land while tile k is processed.  Step k
+ * on tile t_k, buffer and slot b = k & 1, in issue order:
+ *
+ *   [wait vmcnt(5); read window t_k from W[b], descriptor t_{k+2} from D[b]]
+ *   [DMA windows of t_{k+2} -> W[b]: 4 ops] [DMA descriptors t_{k+4} -> D[b]:
+ *   1 op] [tile t_k: compute, deferral and output stores]
+ *
+ * Descriptor t_{k+2} was DMA'd at step k-2, after the window DMA of t_k,
+ * and step k-1 issued 5 loads (its DMAs) after both: vmcnt(5) leaves at
+ * most 5 vector-memory ops outstanding, and those 5 DMAs are the youngest
+ * loads, so both of step k's inputs have landed.  This counts on loads
+ * (LDS-DMA) completing in issue order among themselves, and on nothing
+ * else: stores count in vmcnt too but may retire before older loads (a
+ * wait that also counted the output stores, vmcnt(10), read stale windows
+ * on 3 of 1 M frames), so they are never counted on; pending stores only
+ * make the wait longer.  Every DMA is issued unconditionally (past the
+ * batch end a window DMA reads the UMEM's first 64 bytes and a descriptor
+ * DMA the last descriptor), which keeps 5 a lower bound, and the prologue
+ * issues its DMAs in an order that meets it for steps 0 and 1.  The
+ * descriptor of t_k itself (for the compute) was read at step k-2 and
+ * travels in registers.
+ *
+ * Nothing the loop consumes from memory is a compiler-visible load
+ * (read_tile_db), so the compiler's wait insertion, which treats vmcnt as
+ * out of order once LDS-DMA is pending, never adds a vmcnt(0) to the loop.
+ * The output stores are buffer stores issued unconditionally (a lane with
+ * nothing to store is out of the resource's range), so the loop has no
+ * store branches.  Deferred frames are stored directly to the wave's lists
+ * (no LDS queue), counters go to a per-wave slot (no LDS), and the tail
+ * phase (rx_tail) runs in the same launch on the same LDS once the last DMA
+ * has landed.
+ *
+ * 4 waves per SIMD (the LDS), 128 VGPRs.
+ */
+/* DIAG (diagnostic A/B, cfg.tune bits 16-17): 1 = no compute (the
+ * window's XOR stored as verdict, record and tuple: the same memory
+ * traffic), 2 = the full compute with no output stores. */
+template <bool FRAGS, int DIAG = 0>
+__global__ __launch_bounds__(kBlock, 4) void xdp_rx_db_kernel(RxArgs a)
+{
+	__shared__ uint4 lds_all[kWavesPerBlock * kDbWave];
+
+	const int lane = threadIdx.x & (kWave - 1);
+	/* the wave index in an SGPR: every per-wave base (LDS buffers, list
+	 * regions) is then scalar, and no such pointer occupies VGPRs (where
+	 * the allocator spilled one to scratch, and each reload waited
+	 * vmcnt(0)).  The LDS-DMA ordering does not rest on the compiler's
+	 * view of these pointers (read_tile_db). */
+	const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+	uint4 *wl = lds_all + wid * kDbWave;
+	uint4 *win0 = wl, *win1 = wl + 256, *dsl0 = wl + 512, *dsl1 = wl + 576;
+
+	const uint32_t nfr = a.ndev ? (uint32_t)min((unsigned long long)a.n, *a.ndev)
+				    : a.n;
+	const uint64_t ntiles = ((uint64_t)nfr + kWave - 1) / kWave;
+	const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+	const uint64_t wgid = (uint64_t)blockIdx.x * kWavesPerBlock + wid;
+	FastWave w = {};
+	w.xl = a.xlist + wgid * a.xregion;
+	w.bl = a.blist + wgid * a.xregion;
+
+	const bool dma = !a.force_generic && a.usize >= 64;
+	/* descriptor index of lane's frame in tile tt, clamped to the batch */
+	auto desc_at = [&](uint64_t tt) -> uint64_t {
+		const uint64_t i = tt * kWave + lane;
+		return i < nfr ? i : nfr - 1;
+	};
+	/* DMA of a tile's 64-byte windows into buf (see xdp_rx_kernel); the
+	 * frame offsets reach the loading lanes by lane shuffles */
+	auto issue_win = [&](uint4 dv, bool live, uint4 *buf) {
+		const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
+		const uint32_t len = dv.z;
+		const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
+		const bool ok = live & dma & (len >= 14) & ((uint64_t)len <= a.usize) &
+				(eff <= a.usize - len) & !(eff & 15) &
+				(eff + 64 <= ((a.usize + 15) & ~15ull));
+		const uint64_t e = ok ? eff : 0ull;
+#pragma unroll
+		for (int k = 0; k < 4; k++) {
+			const int f = 16 * k + (lane >> 2);
+			const int c = (lane & 3) ^ ((f >> 2) & 3);
+			uint64_t ef =
+				((uint64_t)(uint32_t)__shfl((int)(uint32_t)(e >> 32), f, kWave) << 32) |
+				(uint32_t)__shfl((int)(uint32_t)e, f, kWave);
+			if (DBG_BAD(ef + 16 * c + 16 > ((a.usize + 15) & ~15ull), 4, ef))
+				ef = 0;
+			__builtin_amdgcn_global_load_lds(
+				(const void *)(a.umem + ef + 16 * c),
+				(lds_void_t *)(buf + kWave * k), 16, 0, 2 /* nt */);
+		}
+	};
+	/* DMA of a tile's 64 descriptors into a slot (lane l: descriptor l) */
+	auto issue_desc = [&](uint64_t tt, uint4 *slot) {
+		uint64_t di = desc_at(tt);
+		if (DBG_BAD(di >= nfr, 5, di))
+			di = 0;
+		__builtin_amdgcn_global_load_lds((const void *)(a.desc + di),
+						 (lds_void_t *)slot, 16, 0, 0);
+	};
+	/* the previous step's outputs, stored after this step's wait: by the
+	 * next wait they are a step old, and the counted wait (which pending
+	 * stores lengthen) seldom finds them outstanding */
+	TileOut pend = {};
+	bool have = false;
+	/* step on tile t: returns the descriptor of tile t + 2 strides */
+	auto step = [&](uint64_t t, uint4 *win, uint4 *dsl, uint4 dv) -> uint4 {
+		const uint64_t i = t * kWave + lane;
+		bool skip = false;
+		if constexpr (FRAGS) {
+			const uint32_t contd = dv.w & XDPGPU_PKT_CONTD;
+			uint32_t prev = (uint32_t)__shfl_up((int)contd, 1, kWave);
+			if (lane == 0)
+				prev = t ? a.desc[t * kWave - 1].options & XDPGPU_PKT_CONTD : 0u;
+			skip = (contd | prev) != 0;
+		}
+		const bool active = (i < nfr) & !skip;
+		uint32_t F[18];
+		uint4 dn;
+		read_tile_db(win, dsl, lane, F, dn);
+		if constexpr (DIAG != 1 && DIAG != 2) {
+			if (have)
+				store_tile(a, pend);
+		}
+		issue_win(dn, t + 2 * nwaves < ntiles, win);
+		issue_desc(t + 4 * nwaves, dsl);
+		if constexpr (DIAG == 1) {
+			uint32_t x = dv.x ^ dv.z;
+#pragma unroll
+			for (int k = 0; k < 16; k++)
+				x ^= F[k];
+			const uint64_t t0 = uniform_u64(i);
+			const uint32_t li = (uint32_t)(i - t0);
+			const __amdgpu_buffer_rsrc_t rv =
+				__builtin_amdgcn_make_buffer_rsrc(a.verdict + t0, 0, kWave, 0x00020000);
+			const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+				a.res + t0, 0, 16 * kWave, 0x00020000);
+			const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
+				a.tup + 16 * t0, 0, 16 * kWave, 0x00020000);
+			const uint32_t off = active ? li : 0x80000000u;
+			__builtin_amdgcn_raw_buffer_store_b8((uint8_t)x, rv, off, 0, 0);
+			__builtin_amdgcn_raw_buffer_store_b128((v4u_t){x, x, x, x}, rr,
+							       active ? 16 * li : off, 0, 2);
+			__builtin_amdgcn_raw_buffer_store_b128((v4u_t){x, 0, x, 0}, rt,
+							       active ? 16 * li : off, 0, 2);
+		} else {
+			fast_tile<false, DIAG != 2>(a, F, dv, i, active, dma, lane, w, &pend);
+			have = true;
+		}
+		return dn;
+	};
+
+	uint64_t t = wgid;
+	if (t < ntiles) {
+		/* prologue: descriptors of the first two tiles in registers;
+		 * then, in this order, descriptor DMA t+2, window DMA t, descriptor
+		 * DMA t+3, window DMA t+1: at least 5 ops younger than both of
+		 * step 0's and of step 1's inputs */
+		const uint4 d0 = *reinterpret_cast<const uint4 *>(a.desc + desc_at(t));
+		const uint4 d1 = *reinterpret_cast<const uint4 *>(a.desc + desc_at(t + nwaves));
+		issue_desc(t + 2 * nwaves, dsl0);
+		issue_win(d0, true, win0);
+		issue_desc(t + 3 * nwaves, dsl1);
+		issue_win(d1, t + nwaves < ntiles, win1);
+		uint4 dc0 = d0, dc1 = d1;
+		for (;;) {
+			const uint4 n0 = step(t, win0, dsl0, dc0);
+			t += nwaves;
+			if (t >= ntiles)
+				break;
+			const uint4 n1 = step(t, win1, dsl1, dc1);
+			t += nwaves;
+			if (t >= ntiles)
+				break;
+			dc0 = n0;
+			dc1 = n1;
+		}
+	}
+	if constexpr (DIAG != 1 && DIAG != 2) {
+		if (have)
+			store_tile(a, pend);   /* the last tile's outputs */
+	}
+	if (lane == 0) {
+		a.xcount[wgid] = w.xout;
+		a.bcount[wgid] = w.bout;
+		a.ycount[wgid] = 0;   /* filled by the exception pass */
+	}
+
+	/* tail phase: the wave's own deferred frames, on the same LDS once
+	 * every DMA has landed (rx_tail waits) */
+	rx_tail(a, w, wgid, lane, reinterpret_cast<uint32_t *>(wl),
+		reinterpret_cast<uint64_t *>(wl + 272), wl, wl + kWave, w.cnt, w.my_bytes);
+
+	/* counters: this wave's own slot (kMaxRxBlocks..: per-wave slots) */
+	if (a.stats) {
+		const uint64_t bytes = wave_sum64(w.my_bytes);
+		unsigned long long *slot = a.stats + (kMaxRxBlocks + wgid) * CNT_SLOT;
+		if (lane <= CNT_FRAG && !DBG_BAD(kMaxRxBlocks + wgid >= kStatSlots, 8, wgid)) {
+			uint64_t v = 0;
+#pragma unroll
+			for (int k = 0; k <= CNT_FRAG; k++)
+				if (lane == k)
+					v = k == CNT_BYTES ? bytes : w.cnt[k];
+			if (v)
+				slot[lane] += v;
+		}
+	}
+}
+
+/* Per-wave LDS of the fast kernel, in uint4: the tile loop's window buffer
+ * (256), descriptor table (32) and two deferral queues (32 each); the tail
+ * phase reuses the same bytes for the exception pass's windows (272) and
+ * table (32), then the bulk pass's meta (64) and partial sums (256). */
+constexpr int kRxLdsWave = 256 + 32 + 32 + 32;
+static_assert(kRxLdsWave >= 64 * 17 / 4 + 32 && kRxLdsWave >= 64 + 256,
+	      "tail phases fit the loop's LDS");
+
 template <int MINW, bool FRAGS>
 __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 {
 	constexpr int XQ = 2 * kWave;      /* deferral queues per wave */
-	__shared__ uint4 buf_all[kWavesPerBlock * 4 * kWave];
-	__shared__ uint64_t dtab_all[kWavesPerBlock * kWave];
-	__shared__ uint32_t xq_all[kWavesPerBlock * XQ];
-	__shared__ uint32_t bq_all[kWavesPerBlock * XQ];
+	__shared__ uint4 lds_all[kWavesPerBlock * kRxLdsWave];
 	__shared__ unsigned long long blk_cnt[CNT_SLOT];
 
 	const int lane = threadIdx.x & (kWave - 1);
 	const int wid = threadIdx.x / kWave;
-	uint4 *buf = buf_all + wid * 4 * kWave;
-	uint64_t *dtab = dtab_all + wid * kWave;
-	uint32_t *xq = xq_all + wid * XQ;
-	uint32_t *bq = bq_all + wid * XQ;
+	uint4 *wlds = lds_all + wid * kRxLdsWave;
+	uint4 *buf = wlds;
+	uint64_t *dtab = reinterpret_cast<uint64_t *>(wlds + 4 * kWave);
+	uint32_t *xq = reinterpret_cast<uint32_t *>(wlds + 4 * kWave + 32);
+	uint32_t *bq = xq + XQ;
 
 	if (threadIdx.x < CNT_SLOT)
 		blk_cnt[threadIdx.x] = 0;
@@ -1222,42 +1985,11 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 	const uint64_t wgid = (uint64_t)blockIdx.x * kWavesPerBlock + wid;
 	uint32_t *xl = a.xlist + wgid * a.xregion;
 	uint32_t *bl = a.blist + wgid * a.xregion;
-	uint32_t cnt[CNT_FRAG + 1] = {};   /* wave-uniform */
-	uint64_t my_bytes = 0;
-	/* queued / flushed deferrals (uniform): exception and bulk lists */
-	uint32_t xq_n = 0, xout = 0, bq_n = 0, bout = 0;
-
-	/* append the frames of the lanes with want set to a list: LDS queue
-	 * in lane order, flushed 64 entries at a time either to this wave's
-	 * region (ctr null) or to a device-wide compact list whose length ctr
-	 * counts (one atomic per 64 entries) */
-	auto defer = [&](bool want, uint64_t i, uint32_t *q, uint32_t &qn,
-			 uint32_t *gl, uint32_t &gout, uint32_t *ctr) {
-		const uint64_t dm = __ballot(want);
-		if (!dm)
-			return;
-		const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
-			(uint32_t)(dm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0));
-		if (want)
-			q[qn + rank] = (uint32_t)i;
-		qn += (uint32_t)__popcll(dm);
-		if (qn >= (uint32_t)kWave) {
-			__builtin_amdgcn_wave_barrier();
-			uint32_t at = gout;
-			if (ctr) {
-				uint32_t base = 0;
-				if (lane == 0)
-					base = atomicAdd(ctr, (uint32_t)kWave);
-				at = __builtin_amdgcn_readfirstlane(base);
-			}
-			gl[at + lane] = q[lane];
-			gout += kWave;
-			const uint32_t rest = q[kWave + lane];
-			__builtin_amdgcn_wave_barrier();
-			q[lane] = rest;
-			qn -= kWave;
-		}
-	};
+	FastWave w = {};
+	w.xq = xq;
+	w.bq = bq;
+	w.xl = xl;
+	w.bl = bl;
 
 	/* the DMA of an invalid frame reads the UMEM's first 64 bytes */
 	const bool dma = !a.force_generic && a.usize >= 64;
@@ -1318,6 +2050,7 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 		/* 1. this lane's window out of LDS (4 conflict-free b128 reads),
 		 * then the next tile's DMA and descriptors */
 		uint32_t F[18];
+		lds_dma_landed();
 		{
 			const int sw = (lane >> 2) & 3;
 #pragma unroll
@@ -1330,147 +2063,17 @@ __global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
 			}
 			F[16] = F[17] = 0;
 		}
-		__builtin_amdgcn_s_waitcnt(0xc07f);   /* lgkmcnt(0): buf read */
+		lds_reads_done();
 		__builtin_amdgcn_wave_barrier();
 		dcur = dnext;
 		issue(dcur, t + nwaves < ntiles);
 		dnext = ld_desc(t + 2 * nwaves);
 
-		const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
-		const uint32_t len = dv.z;
-		const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
-		const bool staged = dma & active & (len >= 14) & ((uint64_t)len <= a.usize) &
-				    (eff <= a.usize - len) & !(eff & 15) &
-				    (eff + 64 <= ((a.usize + 15) & ~15ull));
-
-		/* 2. fast-shape classification, branch free (bitwise &/| on
-		 * flags, selects).  r[j] = frame dword j + nv */
-		const bool v1 = le_is_vlan(F[3] & 0xffff);
-		const bool v2 = v1 & le_is_vlan(F[4] & 0xffff);
-		const uint32_t nv = (uint32_t)v1 + (uint32_t)v2;
-		/* masks, not selects: a select chain over F is turned into a
-		 * dynamically indexed private array (scratch) by the compiler */
-		const uint32_t m2 = 0u - (uint32_t)v2;
-		const uint32_t m1 = (0u - (uint32_t)v1) & ~m2;
-		const uint32_t m0 = ~(m1 | m2);
-		uint32_t r[16];
-#pragma unroll
-		for (int j = 3; j < 16; j++)
-			r[j] = (F[j] & m0) | (F[j + 1] & m1) | (F[j + 2] & m2);
-		const uint32_t l3 = 14 + 4 * nv, l4 = l3 + 20;
-		const uint32_t tot = bswap16(r[4] & 0xffff);
-		const uint32_t proto = r[5] >> 24;
-		const bool udp = proto == 17;
-		const uint32_t thl = ((r[11] >> 20) & 0xf) * 4;
-		const uint32_t cl = udp ? bswap16(r[9] >> 16) : tot - 20;
-		const bool ok_udp = (len >= l4 + 8) & (cl >= 8) & (l4 + cl <= l3 + tot);
-		const bool ok_tcp = (len >= l4 + 20) & (thl >= 20) & (l4 + thl <= len) &
-				    (cl >= thl);
-		bool fast = (!a.force_generic) & staged &
-			    ((r[3] & 0x00ffffffu) == 0x00450008u) &
-			    ((r[5] & 0xff3fu) == 0) & (udp | (proto == 6)) &
-			    (tot >= 20) & (l3 + tot <= len) & (udp ? ok_udp : ok_tcp);
-		/* a checksum range (with udp_csum's odd over-read byte) that ends
-		 * past the window: the bulk kernel adds the payload sum */
-		const bool shape = fast;
-		fast = shape & (l4 + cl + (cl & 1) <= 64u);
-		const bool bulk = shape & !fast & (a.res != nullptr);
-
-		/* 3. defer the frames of other shapes to the exception list and
-		 * the long ones to the bulk list of this wave */
-		defer(active && !fast && !bulk, i, xq, xq_n, xl, xout, nullptr);
-		defer(bulk, i, bq, bq_n, bl, bout, nullptr);
-
-		/* 4. fast frames: flow key, hash, tuple, checksums, verdict */
-		const uint32_t sa = (r[6] >> 16) | (r[7] << 16);
-		const uint32_t da = (r[7] >> 16) | (r[8] << 16);
-		const uint32_t ports = (r[8] >> 16) | (r[9] << 16);
-		/* IPv4 header sum, check word (r6 low half) excluded */
-		const uint64_t s3 = (uint64_t)(r[3] & 0xffff0000u) + r[4] + r[5] +
-				    (r[6] & 0xffff0000u) + r[7] + (r[8] & 0xffffu);
-		const uint32_t c3 = r[6] & 0xffff;
-		const uint32_t c4 = udp ? (r[10] & 0xffff) : (r[12] >> 16);
-		/* L4 sum over [34, end) of the shifted frame with the pseudo
-		 * header, check word excluded; udp_csum's odd-length over-read
-		 * byte included (lib_checksum.h:142-179).  For a bulk frame the
-		 * window part: frame bytes [l4, 64) (F[16], F[17] are zero). */
-		const int32_t e = (int32_t)(34 + cl + (cl & 1));
-		uint64_t s4 = (uint64_t)(r[8] & 0xffff0000u) + sa + da +
-			      ((uint64_t)(proto + cl) << 8);
-#pragma unroll
-		for (int j = 9; j < 16; j++) {
-			uint32_t m = first_bytes(e - 4 * j);
-			if (j == 10)
-				m &= udp ? 0xffff0000u : 0xffffffffu;
-			if (j == 12)
-				m &= udp ? 0xffffffffu : 0x0000ffffu;
-			s4 += r[j] & m;
-		}
-		const uint32_t l3c = ~fold16(s3) & 0xffff;
-		const bool l3_ok = fold16(s3 + c3) == 0xffff;
-		const uint32_t sum4 = fold16(s4);
-		const uint32_t l4c = ~sum4 & 0xffff;
-		const bool absent = udp && c4 == 0;
-		const bool l4_ok = absent || (~fold16((uint64_t)sum4 + c4) & 0xffff) == 0;
-		const bool drop = (a.flags & XDPGPU_CFG_VERIFY_CSUM) && (!l3_ok || !l4_ok);
-		if (fast || bulk) {
-			uint32_t key[11] = {0, 0, 0xffff0000u, sa, ports & 0xffff,
-					    0, 0, 0xffff0000u, da, ports >> 16,
-					    proto | (2u << 16)};
-			/* a bulk frame's record carries its window sum in the
-			 * l4_csum field and its check word in l4_off until the
-			 * bulk kernel completes it */
-			uint4 rec;
-			rec.x = jhash_key44(key, a.initval);
-			rec.y = l3c | ((fast ? l4c : sum4) << 16);
-			rec.z = XDPGPU_F_IP | XDPGPU_F_L4 | (nv ? XDPGPU_F_VLAN : 0u) |
-				(l3_ok ? XDPGPU_F_L3_OK : 0u) |
-				(fast && l4_ok ? XDPGPU_F_L4_OK : 0u) |
-				(fast && absent ? XDPGPU_F_L4_ABSENT : 0u) |
-				(proto << 8) | (l3 << 16) | (nv << 24);
-			rec.w = (fast ? l4 : c4) | (cl << 16);
-			if (fast)
-				a.verdict[i] = (uint8_t)(drop ? XDPGPU_DROP : XDPGPU_REDIRECT);
-			if (a.res)
-				st_nt16(a.res + i, rec);
-			if (a.tup) {
-				if (a.tuple_fmt == XDPGPU_TUPLE_V4) {
-					const uint32_t vid =
-						nv ? (bswap16(F[3] >> 16) & 0x0fff) : 0u;
-					st_nt16(a.tup + 16 * i,
-						make_uint4(sa, da, ports,
-							   proto | (2u << 8) | (vid << 16)));
-				} else if (a.tuple_fmt == XDPGPU_TUPLE_NET) {
-					uint32_t *tp = reinterpret_cast<uint32_t *>(a.tup + 44 * i);
-#pragma unroll
-					for (int j = 0; j < 11; j++)
-						tp[j] = key[j];
-				}
-			}
-			my_bytes += fast ? len : 0;
-		}
-		/* counters (wave-uniform: ballots outside divergent code) */
-		if (a.stats) {
-			cnt[CNT_FRAMES] += __popcll(__ballot(fast));
-			cnt[CNT_VERDICT0 + XDPGPU_DROP] += __popcll(__ballot(fast && drop));
-			cnt[CNT_VERDICT0 + XDPGPU_REDIRECT] += __popcll(__ballot(fast && !drop));
-			cnt[CNT_L3_BAD] += __popcll(__ballot(fast && !l3_ok));
-			cnt[CNT_L4_BAD] += __popcll(__ballot(fast && !l4_ok));
-			cnt[CNT_L4_ABSENT] += __popcll(__ballot(fast && absent));
-		}
+		fast_tile<true>(a, F, dv, i, active, dma, lane, w);
 	}
-	__builtin_amdgcn_wave_barrier();
-	if ((uint32_t)lane < xq_n)
-		xl[xout + lane] = xq[lane];
-	if ((uint32_t)lane < bq_n)
-		bl[bout + lane] = bq[lane];
-	if (lane == 0) {
-		a.xcount[wgid] = xout + xq_n;
-		a.bcount[wgid] = bout + bq_n;
-		a.ycount[wgid] = 0;   /* filled by the exception kernel */
-	}
+	rx_flush_lists(a, w, wgid, lane);
 
-	block_stats_flush(a, blk_cnt, cnt, my_bytes, lane);
+	block_stats_flush(a, blk_cnt, w.cnt, w.my_bytes, lane);
 }
 
 
@@ -1700,6 +2303,40 @@ static hipError_t launch_sized(RxArgs a, uint32_t max_blocks,
 	return e;
 }
 
+/* The default RX launch: one double-buffered fast kernel with its tail
+ * phase (xdp_rx_db_kernel). */
+static hipError_t launch_db(RxArgs a, uint32_t max_blocks, hipStream_t stream,
+			    hipEvent_t *ev)
+{
+	uint32_t cap = a.frags ? resident_blocks<xdp_rx_db_kernel<true>>()
+			       : resident_blocks<xdp_rx_db_kernel<false>>();
+	const uint32_t diag = a.diag;
+	if (cap < max_blocks)
+		max_blocks = cap;
+	const uint32_t blocks = rx_grid_blocks(a.n, max_blocks);
+	a.xregion = rx_xregion(a.n, blocks);
+	a.nregions = blocks * kWavesPerBlock;
+	if (ev)
+		(void)hipEventRecord(ev[0], stream);
+	if (a.frags)
+		hipLaunchKernelGGL((xdp_rx_db_kernel<true>), dim3(blocks), dim3(kBlock), 0,
+				   stream, a);
+	else if (diag == 1)
+		hipLaunchKernelGGL((xdp_rx_db_kernel<false, 1>), dim3(blocks), dim3(kBlock), 0,
+				   stream, a);
+	else if (diag == 2)
+		hipLaunchKernelGGL((xdp_rx_db_kernel<false, 2>), dim3(blocks), dim3(kBlock), 0,
+				   stream, a);
+	else
+		hipLaunchKernelGGL((xdp_rx_db_kernel<false>), dim3(blocks), dim3(kBlock), 0,
+				   stream, a);
+	const hipError_t e = hipGetLastError();
+	if (ev && e == hipSuccess)
+		for (int k = 1; k < 4; k++)
+			(void)hipEventRecord(ev[k], stream);
+	return e;
+}
+
 uint32_t rx_xregion(uint32_t n, uint32_t blocks)
 {
 	const uint64_t ntiles = ((uint64_t)n + kWave - 1) / kWave;
@@ -1714,6 +2351,15 @@ hipError_t launch_rx(const RxArgs &a, uint32_t window, uint32_t max_blocks,
 	/* bits 10-11: bulk-kernel loads per lane and step (0: 4 non-temporal,
 	 * 1: 4 non-temporal in 8-lane groups, 2: 2 non-temporal, 3: 4) */
 	const uint32_t bu = (tune >> 10) & 3;
+	/* default: one double-buffered launch; the three-kernel form for the
+	 * 128-byte exception window and the diagnostic variants (bit 15
+	 * forces it); bits 16-17: the double-buffered kernel's diagnostic
+	 * variants (no compute, no stores) */
+	if (window != 128 && !(tune & 0x8fffu)) {
+		RxArgs b = a;
+		b.diag = (tune >> 16) & 3;
+		return launch_db(b, max_blocks, stream, ev);
+	}
 	if (window == 128)
 		return launch_sized<128, 1>(a, max_blocks, stream, bu, ev);
 	if (waves == 6)
@@ -1780,6 +2426,19 @@ __global__ __launch_bounds__(kBlock) void ip_fast_csum_kernel(
 		s += (uint32_t)h[o] | ((uint32_t)h[o + 1] << 8);
 	out[i] = (uint16_t)(~fold16(s) & 0xffff);
 }
+
+#ifdef XDPGPU_DBG
+} // namespace xdpgpu
+extern "C" int xdpgpu_debug_read(unsigned long long *out)
+{
+	if (hipMemcpyFromSymbol(out, HIP_SYMBOL(xdpgpu::g_dbg), sizeof(xdpgpu::g_dbg)) !=
+	    hipSuccess)
+		return -5;
+	static const unsigned long long z[64] = {};
+	return hipMemcpyToSymbol(HIP_SYMBOL(xdpgpu::g_dbg), z, sizeof(z)) == hipSuccess ? 0 : -5;
+}
+namespace xdpgpu {
+#endif
 
 hipError_t launch_jhash(const uint8_t *keys, uint32_t key_len,
 			uint32_t stride, uint32_t n, uint32_t initval,

@@ -34,7 +34,7 @@ constexpr uint32_t kDefaultMaxBatch = 1u << 20;
 struct Slot {
 	hipStream_t stream = nullptr;
 	hipEvent_t done = nullptr;
-	unsigned long long *d_stats = nullptr; /* kMaxRxBlocks * CNT_SLOT */
+	unsigned long long *d_stats = nullptr; /* kStatSlots * CNT_SLOT */
 	xdpgpu_desc *d_desc = nullptr;
 	uint8_t *d_verdict = nullptr;
 	xdpgpu_result *d_res = nullptr;
@@ -244,7 +244,7 @@ int xdpgpu_init(const xdpgpu_cfg *cfg, xdpgpu_ctx **out)
 			(uint32_t)prop.multiProcessorCount * 8u);
 		for (uint32_t i = 0; i < kSlots && !rc; i++) {
 			Slot &s = ctx->slot[i];
-			size_t stat_bytes = (size_t)kMaxRxBlocks * CNT_SLOT * 8;
+			size_t stat_bytes = (size_t)kStatSlots * CNT_SLOT * 8;
 			if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||
 			    hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess ||
 			    hipEventCreateWithFlags(&s.scr_ev, hipEventDisableTiming) != hipSuccess ||
@@ -997,11 +997,11 @@ int xdpgpu_stats(xdpgpu_ctx *ctx, struct xdpgpu_stats *out)
 	HIP_TRY(ctx, hipSetDevice(ctx->cfg.device));
 	HIP_TRY(ctx, hipDeviceSynchronize());
 	memset(out, 0, sizeof(*out));
-	static thread_local unsigned long long host[kMaxRxBlocks * CNT_SLOT];
+	static thread_local unsigned long long host[kStatSlots * CNT_SLOT];
 	for (uint32_t i = 0; i < kSlots; i++) {
 		HIP_TRY(ctx, hipMemcpy(host, ctx->slot[i].d_stats, sizeof(host),
 				       hipMemcpyDeviceToHost));
-		for (uint32_t b = 0; b < kMaxRxBlocks; b++) {
+		for (uint32_t b = 0; b < kStatSlots; b++) {
 			const unsigned long long *c = host + (size_t)b * CNT_SLOT;
 			out->frames += c[CNT_FRAMES];
 			out->bytes += c[CNT_BYTES];
@@ -1024,7 +1024,7 @@ int xdpgpu_stats_reset(xdpgpu_ctx *ctx)
 	HIP_TRY(ctx, hipDeviceSynchronize());
 	for (uint32_t i = 0; i < kSlots; i++)
 		HIP_TRY(ctx, hipMemset(ctx->slot[i].d_stats, 0,
-				       (size_t)kMaxRxBlocks * CNT_SLOT * 8));
+				       (size_t)kStatSlots * CNT_SLOT * 8));
 	HIP_TRY(ctx, hipDeviceSynchronize());
 	return 0;
 }

@@ -45,6 +45,28 @@ static uint32_t resident_blocks_dev(uint32_t cap)
 	return c;
 }
 
+/* Ordering of a wave's LDS-DMA (global_load_lds) tile staging, made
+ * explicit.  The builtins __builtin_amdgcn_s_waitcnt and wave_barrier are
+ * IntrNoMem intrinsics: they do not keep LDS loads from moving across them,
+ * so the order of "read tile t's windows from LDS" and "DMA tile t+1 into
+ * the same LDS" would rest on the compiler's alias analysis of the DMA
+ * destination (and its vmcnt insertion on the same analysis).  Inline asm
+ * with a memory clobber is a barrier for both the IR and the machine
+ * scheduler, and the wait instruction itself is emitted as written.
+ *  - lds_dma_landed(): before reading LDS a DMA wrote (read after write):
+ *    every vector memory op of this wave, the DMA included, has completed.
+ *  - lds_reads_done(): before issuing a DMA into LDS this wave has just
+ *    read (write after read): the reads have returned their data. */
+__device__ __forceinline__ void lds_dma_landed()
+{
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+__device__ __forceinline__ void lds_reads_done()
+{
+	asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
 /* Per-block counter slot layout (u64 each); slots summed by xdpgpu_stats. */
 enum {
 	CNT_FRAMES = 0,
@@ -60,6 +82,9 @@ enum {
 /* Upper bound on the RX kernel grid (blocks of 256 threads): 8 per CU on a
  * 256-CU MI355X.  Sizes the per-block counter area. */
 constexpr uint32_t kMaxRxBlocks = 2048;
+/* Counter slots of a context slot: one per block of the per-block kernels,
+ * then one per wave of the double-buffered RX kernel (xdp_rx_db_kernel). */
+constexpr uint32_t kStatSlots = kMaxRxBlocks * 5;
 
 struct RxArgs {
 	uint8_t *umem;
@@ -89,6 +114,8 @@ struct RxArgs {
 	uint32_t force_generic;    /* 1: defer every frame (diagnostic)     */
 	uint32_t frags;            /* XDPGPU_CFG_FRAGS: skip the descriptors
 				    * of packets of several (frags.hip)     */
+	uint32_t diag;             /* set by the launcher: cfg.tune bits 16-17
+				    * (diagnostic kernel variants)          */
 	const unsigned long long *ndev; /* nullable: the frame count lives on
 				    * the device (the bounce batch of
 				    * frags.hip); n is then its upper bound */

@@ -16,6 +16,24 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running")
 
 
+@pytest.fixture(autouse=True)
+def _gpu_drain(request):
+    """A GPU test ends with the device drained and a fresh allocation used,
+    so that an asynchronously reported device error fails the test whose
+    kernels raised it, not the next one."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    torch = sys.modules.get("torch")
+    if torch is None or not torch.cuda.is_initialized():
+        return
+    torch.cuda.synchronize()
+    probe = torch.zeros(4096, dtype=torch.uint8, device="cuda:0")
+    probe.add_(1)
+    assert int(probe.sum().item()) == 4096
+    torch.cuda.synchronize()
+
+
 @pytest.fixture(scope="session")
 def golden():
     import json

@@ -174,7 +174,7 @@ def test_oracle_flag_off_ignores_options():
 
 # ------------------------------------------------------------------ GPU
 @pytest.mark.gpu
-@pytest.mark.parametrize("tune", [0, 512])
+@pytest.mark.parametrize("tune", [0, 1 << 15, 512])
 @pytest.mark.parametrize("name", NAMES)
 @pytest.mark.parametrize("skew", [False, True])
 def test_gpu_packets_vs_oracle(name, skew, tune):

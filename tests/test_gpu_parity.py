@@ -27,11 +27,12 @@ def to_dev(a: np.ndarray, pad: int = 64):
     return t
 
 
-# kernel variants (cfg.tune): default; every frame through the exception
+# kernel variants (cfg.tune): default (one fused launch); the three-kernel
+# form (bit 15); every frame through the exception
 # kernel (its long payload sums deferred to the bulk kernel); the same with
 # the exception kernel keeping its payload sums; 6-wave fast kernel with the
 # 4-load plain bulk kernel
-TUNES = [0, 512, 512 | 256, 6 | (3 << 10), 1 << 10]
+TUNES = [0, 1 << 15, 512, 512 | 256, 6 | (3 << 10), 1 << 10]
 
 
 def run_dev(umem, descs, flags=0x5, initval=0, fmt=1, window=64, tune=0):

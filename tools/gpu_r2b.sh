@@ -1,0 +1,5 @@
+set -e
+mkdir -p gpurun_out
+echo "== c2"; timeout -k 10 120 python -u tools/tune_rx.py --variants ceil,64:0,64:32768 --rounds 7
+echo "== 1500"; timeout -k 10 120 python -u tools/tune_rx.py --frames 2097152 --size 1500 --variants 64:0,64:32768 --rounds 5
+echo "== imix"; timeout -k 10 120 python -u tools/tune_rx.py --frames 16777216 --kind 1 --seed 0x5EED0003 --variants 64:0,64:32768 --rounds 5

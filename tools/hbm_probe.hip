@@ -202,6 +202,62 @@ __global__ __launch_bounds__(256) void k_rxlds(const uint4 *desc, const uint8_t 
 	}
 }
 
+/* Verdict store shapes (round 2): VS 0 = one byte per lane (64 B per
+ * wave-instruction, a half line; the neighbouring tile's wave writes the
+ * other half), 1 = no verdict store, 2 = two tiles' verdicts as one 128-B
+ * line per wave (lane l stores the u16 of frames 2l, 2l+1 of the tile
+ * pair), 3 = as 0 but tiles dealt to waves in contiguous runs (each 128-B
+ * verdict line has one writer).  Plain loads, nt stores, one tile pair per
+ * iteration. */
+template <int VS>
+__global__ __launch_bounds__(256) void k_rxpair(const uint4 *desc, const uint4 *frames,
+						uint4 *res, uint4 *tup, uint8_t *verd,
+						size_t nframes)
+{
+	const size_t pairs = nframes / 128;
+	const int lane = threadIdx.x & 63;
+	const size_t wave = blockIdx.x * 4ull + (threadIdx.x >> 6);
+	const size_t nw = (size_t)gridDim.x * 4;
+	size_t p0 = wave, pstep = nw, pend = pairs;
+	if (VS == 3) {
+		const size_t per = (pairs + nw - 1) / nw;
+		p0 = wave * per;
+		pstep = 1;
+		pend = p0 + per < pairs ? p0 + per : pairs;
+	}
+	for (size_t p = p0; p < pend; p += pstep) {
+		uint32_t xv[2];
+#pragma unroll
+		for (int u = 0; u < 2; u++) {
+			const size_t t = 2 * p + u;
+			const size_t i = t * 64 + lane;
+			const uint4 d = desc[i];
+			uint4 f[4];
+#pragma unroll
+			for (int k = 0; k < 4; k++)
+				f[k] = frames[t * 256 + k * 64 + lane];
+			uint32_t x = d.x ^ d.z;
+#pragma unroll
+			for (int k = 0; k < 4; k++)
+				x ^= f[k].x ^ f[k].y ^ f[k].z ^ f[k].w;
+			const uint4 r = make_uint4(x, x + 1, x + 2, x + 3);
+			nts(r, res + i);
+			nts(r, tup + i);
+			xv[u] = x & 0xff;
+			if (VS == 0 || VS == 3)
+				verd[i] = (uint8_t)x;
+		}
+		if (VS == 2) {
+			/* frames 2l, 2l+1 of the pair: tile (l >= 32), lanes 2l mod 64, +1 */
+			const int s0 = (2 * lane) & 63, s1 = (2 * lane + 1) & 63;
+			const uint32_t a0 = __shfl(xv[0], s0), a1 = __shfl(xv[0], s1);
+			const uint32_t b0 = __shfl(xv[1], s0), b1 = __shfl(xv[1], s1);
+			const uint32_t v = lane < 32 ? (a0 | (a1 << 8)) : (b0 | (b1 << 8));
+			reinterpret_cast<uint16_t *>(verd + p * 128)[lane] = (uint16_t)v;
+		}
+	}
+}
+
 static float time_it(void (*fn)(void *), void *arg, int reps)
 {
 	hipEvent_t a, b;
@@ -238,6 +294,9 @@ template <bool NT, int U>
 static void run_direct(void *) { hipLaunchKernelGGL((k_rxdirect<NT, U>), dim3(C.grid), dim3(256), 0, 0, C.desc, C.a, C.res, C.tup, C.verd, C.frames); }
 template <bool NT, int U>
 static void run_mix(void *) { hipLaunchKernelGGL((k_rxmix<NT, U>), dim3(C.grid), dim3(256), 0, 0, C.desc, C.a, C.res, C.tup, C.verd, C.frames); }
+
+template <int VS>
+static void run_pair(void *) { hipLaunchKernelGGL((k_rxpair<VS>), dim3(C.grid), dim3(256), 0, 0, C.desc, C.a, C.res, C.tup, C.verd, C.frames); }
 
 /* bulk payload probes: bytes [64, 1500) of frames at stride 1536 */
 template <int U, bool NT>
@@ -342,6 +401,7 @@ int main(int argc, char **argv)
 {
 	if (argc > 1 && !strcmp(argv[1], "bulk"))
 		return bulk_main();
+	const bool pair_only = argc > 1 && !strcmp(argv[1], "pair");
 	const size_t frames = 16ull << 20;
 	C.frames = frames;
 	C.n16 = frames * 64 / 16;              /* 1 GiB */
@@ -365,10 +425,28 @@ int main(int argc, char **argv)
 	}
 	const int grids[] = {1024, 2048, 4096, 8192};
 	for (int gi = 0; gi < 4; gi++) {
-		if (argc > 1 && gi < 2) continue;
+		if (argc > 1 && !pair_only && gi < 2) continue;
 		C.grid = grids[gi];
 		const double gb = C.n16 * 16 / 1e9;
 		float t;
+		if (pair_only) {
+			const double mb = frames * 113.0 / 1e9;
+			for (int rep = 0; rep < 2; rep++) {
+				t = time_it(run_mix<false, 1>, 0, 20);
+				printf("grid %5d rx_mix        %7.1f GB/s  %.4f ms\n", C.grid, mb / t * 1e3, t);
+				t = time_it(run_pair<0>, 0, 20);
+				printf("grid %5d pair_byte     %7.1f GB/s  %.4f ms\n", C.grid, mb / t * 1e3, t);
+				t = time_it(run_pair<1>, 0, 20);
+				printf("grid %5d pair_noverd   %7.1f GB/s  %.4f ms (of the same 113 B)\n", C.grid, mb / t * 1e3, t);
+				t = time_it(run_pair<2>, 0, 20);
+				printf("grid %5d pair_line     %7.1f GB/s  %.4f ms\n", C.grid, mb / t * 1e3, t);
+				t = time_it(run_pair<3>, 0, 20);
+				printf("grid %5d pair_contig   %7.1f GB/s  %.4f ms\n", C.grid, mb / t * 1e3, t);
+				t = time_it(run_lds, 0, 20);
+				printf("grid %5d rx_lds        %7.1f GB/s  %.4f ms\n", C.grid, mb / t * 1e3, t);
+			}
+			continue;
+		}
 		t = time_it(run_read, 0, 20);
 		printf("grid %5d read      %7.1f GB/s\n", C.grid, gb / t * 1e3);
 		t = time_it(run_read_nt, 0, 20);
