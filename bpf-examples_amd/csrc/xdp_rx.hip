@@ -56,6 +56,27 @@ __device__ __forceinline__ bool dbg_bad(bool bad, uint32_t code, uint64_t val)
 #define DBG_BAD(c, code, v) false
 #endif
 
+/* Timing builds (-DXDPGPU_STAMPS, tools/dbg_build.sh stamps): each wave of
+ * the double-buffered kernel records s_memrealtime (100 MHz) at its start,
+ * at the end of its tile loop and at its end, read by xdpgpu_stamps_read. */
+#ifdef XDPGPU_STAMPS
+constexpr int kStampWaves = 8192;
+__device__ unsigned long long g_stamp[4 * kStampWaves];
+/* k == 0 also records where the wave runs: HW_ID | XCC_ID << 32 */
+#define STAMP(wgid, lane, k)                                                   \
+	do {                                                                   \
+		if ((lane) == 0 && (wgid) < (uint64_t)kStampWaves) {           \
+			g_stamp[4 * (wgid) + (k)] = __builtin_amdgcn_s_memrealtime(); \
+			if ((k) == 0)                                          \
+				g_stamp[4 * (wgid) + 3] =                      \
+					(unsigned long long)(uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) | \
+					((unsigned long long)(uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32); \
+		}                                                              \
+	} while (0)
+#else
+#define STAMP(wgid, lane, k) do { } while (0)
+#endif
+
 /* ------------------------------------------------------------------ */
 /* one's-complement helpers                                            */
 
@@ -1322,7 +1343,10 @@ struct FastWave {
 	uint32_t xq_n, xout, bq_n, bout;  /* queued / flushed deferrals
 					   * (uniform): exception, bulk    */
 	uint32_t *xq, *bq;                /* LDS queues, 2 x 64 entries    */
-	uint32_t *xl, *bl;                /* this wave's list regions      */
+	uint32_t *xl, *bl;                /* this wave's list regions (the
+					   * block's: xdp_rx_db_kernel)    */
+	uint32_t *lcount;                 /* xdp_rx_db_kernel: the block's
+					   * list lengths in LDS (2)       */
 };
 
 /* Append the frames of the lanes with want set to a list: LDS queue in
@@ -1374,61 +1398,79 @@ struct TileOut {
 	uint4 rec;
 };
 
-/* The stores of a TileOut: buffer stores over the tile's records, a lane
- * with nothing to store at an offset past the resource's size (dropped by
- * the hardware); no branches but the configuration's (uniform). */
+/* The stores of a TileOut: exactly kTileStores buffer stores over the
+ * tile's records whatever the configuration (the double-buffered kernel's
+ * counted wait relies on the number), a lane with nothing to store, and a
+ * store the configuration does not need, at an offset past its resource's
+ * size (dropped by the hardware); no branches. */
+constexpr int kTileStores = 5;
 __device__ __forceinline__ void store_tile(const RxArgs &a, const TileOut &o)
 {
 	constexpr uint32_t kOff = 0x80000000u;
 	constexpr int kFmt = 0x00020000;      /* gfx9 raw buffer dword 3 */
-	if (DBG_BAD(o.t0 >= a.n || (o.t0 & (kWave - 1)), 9, o.t0))
-		return;
+	const bool bad = DBG_BAD(o.t0 >= a.n || (o.t0 & (kWave - 1)), 9, o.t0);
+	const uint32_t fl = bad ? 0u : o.fl;
 	const __amdgpu_buffer_rsrc_t rv =
 		__builtin_amdgcn_make_buffer_rsrc(a.verdict + o.t0, 0, kWave, kFmt);
 	__builtin_amdgcn_raw_buffer_store_b8((uint8_t)o.verdict, rv,
-					     (o.fl & 1) ? o.li : kOff, 0, 0);
-	const bool out = o.fl & 2;
-	if (a.res) {
-		const __amdgpu_buffer_rsrc_t rr =
-			__builtin_amdgcn_make_buffer_rsrc(a.res + o.t0, 0, 16 * kWave, kFmt);
-		__builtin_amdgcn_raw_buffer_store_b128(
-			(v4u_t){o.rec.x, o.rec.y, o.rec.z, o.rec.w}, rr,
-			out ? 16 * o.li : kOff, 0, 2 /* nt */);
-	}
-	if (a.tup && a.tuple_fmt == XDPGPU_TUPLE_V4) {
-		const __amdgpu_buffer_rsrc_t rt =
-			__builtin_amdgcn_make_buffer_rsrc(a.tup + 16 * o.t0, 0, 16 * kWave, kFmt);
-		__builtin_amdgcn_raw_buffer_store_b128(
-			(v4u_t){o.sa, o.da, o.ports, o.proto | (2u << 8) | (o.vid << 16)}, rt,
-			out ? 16 * o.li : kOff, 0, 2);
-	} else if (a.tup && a.tuple_fmt == XDPGPU_TUPLE_NET) {
-		const __amdgpu_buffer_rsrc_t rt =
-			__builtin_amdgcn_make_buffer_rsrc(a.tup + 44 * o.t0, 0, 44 * kWave, kFmt);
-		const uint32_t b = out ? 44 * o.li : kOff;
-		__builtin_amdgcn_raw_buffer_store_b128((v4u_t){0u, 0u, 0xffff0000u, o.sa}, rt,
-						       b, 0, 2);
-		__builtin_amdgcn_raw_buffer_store_b128((v4u_t){o.ports & 0xffff, 0u, 0u,
-							       0xffff0000u}, rt,
-						       out ? b + 16 : kOff, 0, 2);
-		__builtin_amdgcn_raw_buffer_store_b96((v3u_t){o.da, o.ports >> 16,
-							     o.proto | (2u << 16)}, rt,
-						      out ? b + 32 : kOff, 0, 2);
-	}
+					     (fl & 1) ? o.li : kOff, 0, 0);
+	const bool out = fl & 2;
+	/* a missing output: a resource of no records over the verdicts */
+	const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+		a.res ? (void *)(a.res + o.t0) : (void *)a.verdict, 0,
+		a.res ? 16 * kWave : 0, kFmt);
+	__builtin_amdgcn_raw_buffer_store_b128((v4u_t){o.rec.x, o.rec.y, o.rec.z, o.rec.w},
+					       rr, out ? 16 * o.li : kOff, 0, 2 /* nt */);
+	const bool net = a.tuple_fmt == XDPGPU_TUPLE_NET;
+	const bool tup = a.tup && (net || a.tuple_fmt == XDPGPU_TUPLE_V4);
+	const uint32_t tb = net ? 44u : 16u;
+	const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
+		tup ? (void *)(a.tup + tb * o.t0) : (void *)a.verdict, 0,
+		tup ? (int)(tb * kWave) : 0, kFmt);
+	const uint32_t b = out ? tb * o.li : kOff;
+	const v4u_t w0 = net ? (v4u_t){0u, 0u, 0xffff0000u, o.sa}
+			     : (v4u_t){o.sa, o.da, o.ports, o.proto | (2u << 8) | (o.vid << 16)};
+	__builtin_amdgcn_raw_buffer_store_b128(w0, rt, b, 0, 2);
+	__builtin_amdgcn_raw_buffer_store_b128((v4u_t){o.ports & 0xffff, 0u, 0u, 0xffff0000u},
+					       rt, net && out ? b + 16 : kOff, 0, 2);
+	__builtin_amdgcn_raw_buffer_store_b96((v3u_t){o.da, o.ports >> 16, o.proto | (2u << 16)},
+					      rt, net && out ? b + 32 : kOff, 0, 2);
 }
 
-/* Append without an LDS queue: each deferred lane stores its index at its
- * rank (a partial line per store; deferrals are rare on the fast shapes). */
+/* Lane 0's fetch-and-add of v on an LDS counter, returned to every lane.
+ * In asm, waiting for its own result: a compiler-visible LDS atomic gets a
+ * vmcnt(0) in front of it while LDS-DMA is pending (the compiler cannot
+ * tell the counter from the DMA's destination). */
+__device__ __forceinline__ uint32_t lds_fetch_add(uint32_t *ctr, uint32_t v, int lane)
+{
+	uint32_t r = 0;
+	if (lane == 0) {
+		const uint32_t addr =
+			(uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t *)ctr;
+		asm volatile("ds_add_rtn_u32 %0, %1, %2\n\t"
+			     "s_waitcnt lgkmcnt(0)"
+			     : "=v"(r)
+			     : "v"(addr), "v"(v)
+			     : "memory");
+	}
+	return (uint32_t)__builtin_amdgcn_readfirstlane(r);
+}
+
+/* Append to the block's list without an LDS queue: the wave reserves its
+ * entries with one LDS atomic on the list's length, and each deferred lane
+ * stores its index at its rank (a partial line per store; deferrals are
+ * rare on the fast shapes). */
 __device__ __forceinline__ void defer_direct(bool want, uint64_t i, uint32_t *gl,
-					     uint32_t &gout, int lane, uint32_t xcap)
+					     uint32_t *lcount, int lane, uint32_t xcap)
 {
 	const uint64_t dm = __ballot(want);
 	if (!dm)
 		return;
+	const uint32_t base = lds_fetch_add(lcount, (uint32_t)__popcll(dm), lane);
 	const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
 		(uint32_t)(dm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0));
-	if (want && !DBG_BAD(gout + rank >= xcap, 7, gout + rank))
-		st_asm_sb32(uniform_ptr(gl), (gout + rank) * 4u, (uint32_t)i);
-	gout += (uint32_t)__popcll(dm);
+	if (want && !DBG_BAD(base + rank >= xcap, 7, base + rank))
+		st_asm_sb32(uniform_ptr(gl), (base + rank) * 4u, (uint32_t)i);
 }
 
 template <bool LQ, bool ST = true>
@@ -1483,8 +1525,8 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 		defer_append(active && !fast && !bulk, i, w.xq, w.xq_n, w.xl, w.xout, lane);
 		defer_append(bulk, i, w.bq, w.bq_n, w.bl, w.bout, lane);
 	} else {
-		defer_direct(active && !fast && !bulk, i, w.xl, w.xout, lane, a.xregion);
-		defer_direct(bulk, i, w.bl, w.bout, lane, a.xregion);
+		defer_direct(active && !fast && !bulk, i, w.xl, w.lcount, lane, a.xregion);
+		defer_direct(bulk, i, w.bl, w.lcount + 1, lane, a.xregion);
 	}
 
 	/* 4. fast frames: flow key, hash, tuple, checksums, verdict */
@@ -1625,24 +1667,28 @@ __device__ __forceinline__ void wave_stats_to_lds(const RxArgs &a,
 }
 
 /*
- * Tail phase of the double-buffered fast kernel: the wave finishes its own
+ * Tail phase of the double-buffered fast kernel: the block finishes its
  * deferred frames in the order of the separate kernels (exception batches,
  * then the bulk list, then the exception frames' deferred payload sums),
- * reusing its LDS: win (64 rows of 17 dwords) and gtab (64 u64) for the
- * exception batches, meta (64 uint4) and part (256 uint4) for the bulk
- * batches.  Its lists were written by this wave alone: a vmcnt(0) wait
- * before each pass orders those stores before these loads.
+ * the batches of each pass split over its waves; each wave reuses its own
+ * LDS: win (64 rows of 17 dwords) and gtab (64 u64) for the exception
+ * batches, meta (64 uint4) and part (256 uint4) for the bulk batches.
+ * Called by every wave of the block (barriers) after a vmcnt(0) and a
+ * barrier that end the tile loop.  A wave's vmcnt(0) before each barrier
+ * makes its list entries, outputs and payload-list entries visible to the
+ * block's other waves, whose L1 lines for them are never loaded before
+ * (read-once lists).
  */
 __device__ __forceinline__ void rx_tail(const RxArgs &a, const FastWave &w,
-					uint64_t wgid, int lane, uint32_t *win,
+					uint64_t rb, uint32_t xc, uint32_t bc,
+					int wid, int nw, int lane, uint32_t *win,
 					uint64_t *gtab, uint4 *meta, uint4 *part4,
 					uint32_t (&cnt)[CNT_FRAG + 1], uint64_t &my_bytes)
 {
-	const uint32_t xc = w.xout + w.xq_n, bc = w.bout + w.bq_n;
-	uint4 *yl = a.ylist + wgid * a.xregion;
-	uint32_t *yc = a.ycount + wgid;
-	lds_dma_landed();
-	for (uint32_t b = 0; b < xc; b += kWave) {
+	uint4 *yl = a.ylist + rb * a.xregion;
+	uint32_t *yc = a.ycount + rb;
+	const uint32_t stride = (uint32_t)nw * kWave;
+	for (uint32_t b = (uint32_t)wid * kWave; b < xc; b += stride) {
 		const bool act = b + lane < xc;
 		uint64_t i = act ? w.xl[b + lane] : 0;
 		const bool bad = act && DBG_BAD(i >= a.n, 1, i);
@@ -1650,7 +1696,8 @@ __device__ __forceinline__ void rx_tail(const RxArgs &a, const FastWave &w,
 		generic_batch<64>(a, win, gtab, lane, i, act && !bad, yl, yc, cnt, my_bytes);
 	}
 	lds_dma_landed();
-	for (uint32_t b = 0; b < bc; b += kWave)
+	__syncthreads();
+	for (uint32_t b = (uint32_t)wid * kWave; b < bc; b += stride)
 		bulk_batch<4, true, false, 16>(a, meta, part4, lane, w.bl + b,
 					       bc - b < (uint32_t)kWave ? bc - b : kWave,
 					       cnt, my_bytes);
@@ -1660,7 +1707,7 @@ __device__ __forceinline__ void rx_tail(const RxArgs &a, const FastWave &w,
 	if (lane == 0)
 		ycn = atomicAdd(yc, 0u);
 	ycn = __builtin_amdgcn_readfirstlane(ycn);
-	for (uint32_t b = 0; b < ycn; b += kWave)
+	for (uint32_t b = (uint32_t)wid * kWave; b < ycn; b += stride)
 		bulk_batch<4, true, true, 16>(a, meta, part4, lane, yl + b,
 					      ycn - b < (uint32_t)kWave ? ycn - b : kWave,
 					      cnt, my_bytes);
@@ -1702,6 +1749,7 @@ __device__ __forceinline__ void rx_tail(const RxArgs &a, const FastWave &w,
  * memory ops as completing out of order), and in one block so that no
  * use of the results is scheduled before their lgkmcnt wait. */
 typedef __attribute__((address_space(3))) uint4 lds_uint4_t;
+template <int N>
 __device__ __forceinline__ void read_tile_db(const uint4 *win, const uint4 *dslot,
 					     int lane, uint32_t (&F)[18], uint4 &dn)
 {
@@ -1714,16 +1762,22 @@ __device__ __forceinline__ void read_tile_db(const uint4 *win, const uint4 *dslo
 	const uint32_t a3 = (uint32_t)(uintptr_t)(lw + 4 * lane + (3 ^ sw));
 	const uint32_t ad = (uint32_t)(uintptr_t)(ld + lane);
 	v4u_t v0, v1, v2, v3, vd;
-	asm volatile("s_waitcnt vmcnt(5)\n\t"
-		     "ds_read_b128 %0, %5\n\t"
-		     "ds_read_b128 %1, %6\n\t"
-		     "ds_read_b128 %2, %7\n\t"
-		     "ds_read_b128 %3, %8\n\t"
-		     "ds_read_b128 %4, %9\n\t"
-		     "s_waitcnt lgkmcnt(0)"
-		     : "=&v"(v0), "=&v"(v1), "=&v"(v2), "=&v"(v3), "=&v"(vd)
-		     : "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(ad)
-		     : "memory");
+#define XDP_READ_TILE(N)                                                        \
+	asm volatile("s_waitcnt vmcnt(" #N ")\n\t"                              \
+		     "ds_read_b128 %0, %5\n\t"                                  \
+		     "ds_read_b128 %1, %6\n\t"                                  \
+		     "ds_read_b128 %2, %7\n\t"                                  \
+		     "ds_read_b128 %3, %8\n\t"                                  \
+		     "ds_read_b128 %4, %9\n\t"                                  \
+		     "s_waitcnt lgkmcnt(0)"                                     \
+		     : "=&v"(v0), "=&v"(v1), "=&v"(v2), "=&v"(v3), "=&v"(vd)    \
+		     : "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(ad)              \
+		     : "memory")
+	if constexpr (N == 10)
+		XDP_READ_TILE(10);
+	else
+		XDP_READ_TILE(5);
+#undef XDP_READ_TILE
 	F[0] = v0.x; F[1] = v0.y; F[2] = v0.z; F[3] = v0.w;
 	F[4] = v1.x; F[5] = v1.y; F[6] = v1.z; F[7] = v1.w;
 	F[8] = v2.x; F[9] = v2.y; F[10] = v2.z; F[11] = v2.w;
@@ -1733,9 +1787,11 @@ __device__ __forceinline__ void read_tile_db(const uint4 *win, const uint4 *dslo
 }
 
 /* Per-wave LDS of the double-buffered kernel, in uint4: two window buffers
- * (256 each) and two descriptor slots (64 each).  16 waves per CU x 10 KiB
- * = the CU's 160 KiB. */
+ * (256 each) and two descriptor slots (64 each), 10 KiB; kCuWaves waves per
+ * block, one block per CU. */
 constexpr int kDbWave = 2 * 256 + 2 * 64;
+constexpr int kCuWaves = 15;
+constexpr int kCuBlock = kCuWaves * kWave;
 
 /*
  * Fast kernel, double-buffered: the default RX launch.
@@ -1744,65 +1800,100 @@ constexpr int kDbWave = 2 * 256 + 2 * 64;
  * descriptor DMA of tiles k+2, k+3) land while tile k is processed.  Step k
  * on tile t_k, buffer and slot b = k & 1, in issue order:
  *
- *   [wait vmcnt(5); read window t_k from W[b], descriptor t_{k+2} from D[b]]
- *   [DMA windows of t_{k+2} -> W[b]: 4 ops] [DMA descriptors t_{k+4} -> D[b]:
- *   1 op] [tile t_k: compute, deferral and output stores]
+ *   [wait vmcnt(10); read window t_k from W[b], descriptor t_{k+2} from
+ *   D[b]] [output stores of t_{k-1}: kTileStores = 5 ops] [DMA windows of
+ *   t_{k+2} -> W[b]: 4 ops] [DMA descriptors t_{k+4} -> D[b]: 1 op]
+ *   [tile t_k: compute, deferral stores; outputs kept for step k+1]
  *
  * Descriptor t_{k+2} was DMA'd at step k-2, after the window DMA of t_k,
- * and step k-1 issued 5 loads (its DMAs) after both: vmcnt(5) leaves at
- * most 5 vector-memory ops outstanding, and those 5 DMAs are the youngest
- * loads, so both of step k's inputs have landed.  This counts on loads
- * (LDS-DMA) completing in issue order among themselves, and on nothing
- * else: stores count in vmcnt too but may retire before older loads (a
- * wait that also counted the output stores, vmcnt(10), read stale windows
- * on 3 of 1 M frames), so they are never counted on; pending stores only
- * make the wait longer.  Every DMA is issued unconditionally (past the
- * batch end a window DMA reads the UMEM's first 64 bytes and a descriptor
- * DMA the last descriptor), which keeps 5 a lower bound, and the prologue
- * issues its DMAs in an order that meets it for steps 0 and 1.  The
- * descriptor of t_k itself (for the compute) was read at step k-2 and
- * travels in registers.
+ * and step k-1 issued 10 ops (5 stores, 5 DMAs) after both; vmcnt counts
+ * loads, stores and LDS-DMA together in issue order, so vmcnt(10) means
+ * both of step k's inputs have landed while the previous step's stores
+ * may still be in flight (a wait that also covered them, vmcnt(5), cost
+ * 11 % on config 2).  The count is exact only because every step issues
+ * the same ops: store_tile always issues its 5 stores (those a
+ * configuration does not need go out of range and are dropped), every DMA
+ * is issued unconditionally (past the batch end a window DMA reads the
+ * UMEM's first 64 bytes and a descriptor DMA the last descriptor), and the
+ * deferral stores only add younger ops.  The prologue issues its DMAs and
+ * one empty store_tile in an order that meets the count for steps 0 and 1.
+ * (An earlier vmcnt(10) that assumed 5 stores where a configuration
+ * issued 3 read stale windows: the count must not depend on the
+ * configuration.)  The descriptor of t_k itself (for the compute) was read
+ * at step k-2 and travels in registers.
  *
  * Nothing the loop consumes from memory is a compiler-visible load
  * (read_tile_db), so the compiler's wait insertion, which treats vmcnt as
  * out of order once LDS-DMA is pending, never adds a vmcnt(0) to the loop.
  * The output stores are buffer stores issued unconditionally (a lane with
  * nothing to store is out of the resource's range), so the loop has no
- * store branches.  Deferred frames are stored directly to the wave's lists
- * (no LDS queue), counters go to a per-wave slot (no LDS), and the tail
- * phase (rx_tail) runs in the same launch on the same LDS once the last DMA
- * has landed.
+ * store branches.
  *
- * 4 waves per SIMD (the LDS), 128 VGPRs.
+ * One block per CU, kCuWaves waves, tiles claimed at run time.  With a
+ * static share per wave (64 tiles each on config 2) the waves of a CU
+ * finished 140-170 us apart in a 370 us launch, in the order they were
+ * dispatched (rank correlation 0.94, tools/stamps.py): the SIMD's issue
+ * arbitration favours its oldest wave, which ran its share twice as fast
+ * as the youngest.  So the block's tiles (b, b + nb, b + 2 nb, ... for
+ * block b of nb) are handed out by an LDS counter, one claim per step,
+ * made 5 steps ahead of the tile's compute (the pipeline needs the tile
+ * for its descriptor DMA 4 steps ahead): an LDS atomic, waited on by
+ * lgkmcnt, never by vmcnt.  Deferred frames go to the block's lists (an
+ * LDS atomic reserves each wave's entries), counters to a per-wave slot,
+ * and the tail phase (rx_tail) splits the block's lists over its waves in
+ * the same launch, on the same LDS, once the last DMA has landed.
+ *
+ * 15 waves per CU (4, 4, 4, 3 per SIMD: 15 x 10 KiB of buffers and the
+ * block's counters in the CU's 160 KiB), 128 VGPRs.
  */
 /* DIAG (diagnostic A/B, cfg.tune bits 16-17): 1 = no compute (the
  * window's XOR stored as verdict, record and tuple: the same memory
  * traffic), 2 = the full compute with no output stores. */
 template <bool FRAGS, int DIAG = 0>
-__global__ __launch_bounds__(kBlock, 4) void xdp_rx_db_kernel(RxArgs a)
+__global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 {
-	__shared__ uint4 lds_all[kWavesPerBlock * kDbWave];
+	__shared__ uint4 lds_all[kCuWaves * kDbWave];
+	/* the block's tile claims and list lengths (exception, bulk) */
+	__shared__ uint32_t ctl[4];
+	/* the counted wait: the 5 DMAs of the step before and, but for the
+	 * no-store variant, the kTileStores output stores issued after them
+	 * (kept in the count, so that no step waits for stores) */
+	constexpr int kWaitN = DIAG == 2 ? 5 : 5 + kTileStores;
+	static_assert(kWaitN == 5 || kWaitN == 10, "read_tile_db's waits");
 
 	const int lane = threadIdx.x & (kWave - 1);
-	/* the wave index in an SGPR: every per-wave base (LDS buffers, list
-	 * regions) is then scalar, and no such pointer occupies VGPRs (where
-	 * the allocator spilled one to scratch, and each reload waited
+	/* the wave index in an SGPR: every per-wave base (LDS buffers) is
+	 * then scalar, and no such pointer occupies VGPRs (where the
+	 * allocator spilled one to scratch, and each reload waited
 	 * vmcnt(0)).  The LDS-DMA ordering does not rest on the compiler's
 	 * view of these pointers (read_tile_db). */
 	const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
 	uint4 *wl = lds_all + wid * kDbWave;
 	uint4 *win0 = wl, *win1 = wl + 256, *dsl0 = wl + 512, *dsl1 = wl + 576;
+	const uint64_t rb = blockIdx.x, nb = gridDim.x;
+	const uint64_t wgid = rb * kCuWaves + wid;
+
+	if (threadIdx.x == 0) {
+		ctl[0] = ctl[1] = ctl[2] = 0;
+		a.ycount[rb] = 0;      /* filled by the exception pass */
+	}
+	lds_dma_landed();
+	__syncthreads();
 
 	const uint32_t nfr = a.ndev ? (uint32_t)min((unsigned long long)a.n, *a.ndev)
 				    : a.n;
 	const uint64_t ntiles = ((uint64_t)nfr + kWave - 1) / kWave;
-	const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
-	const uint64_t wgid = (uint64_t)blockIdx.x * kWavesPerBlock + wid;
 	FastWave w = {};
-	w.xl = a.xlist + wgid * a.xregion;
-	w.bl = a.blist + wgid * a.xregion;
+	w.xl = a.xlist + rb * a.xregion;
+	w.bl = a.blist + rb * a.xregion;
+	w.lcount = ctl + 1;
+	STAMP(wgid, lane, 0);
 
 	const bool dma = !a.force_generic && a.usize >= 64;
+	/* the block's next cnt tiles: b + k nb for k = the claim .. + cnt-1 */
+	auto claim = [&](uint32_t cnt) -> uint64_t {
+		return rb + (uint64_t)lds_fetch_add(&ctl[0], cnt, lane) * nb;
+	};
 	/* descriptor index of lane's frame in tile tt, clamped to the batch */
 	auto desc_at = [&](uint64_t tt) -> uint64_t {
 		const uint64_t i = tt * kWave + lane;
@@ -1840,13 +1931,15 @@ __global__ __launch_bounds__(kBlock, 4) void xdp_rx_db_kernel(RxArgs a)
 		__builtin_amdgcn_global_load_lds((const void *)(a.desc + di),
 						 (lds_void_t *)slot, 16, 0, 0);
 	};
-	/* the previous step's outputs, stored after this step's wait: by the
-	 * next wait they are a step old, and the counted wait (which pending
-	 * stores lengthen) seldom finds them outstanding */
+	/* the previous step's outputs, stored after this step's wait (the
+	 * first step stores an empty TileOut: every lane out of range) */
 	TileOut pend = {};
-	bool have = false;
-	/* step on tile t: returns the descriptor of tile t + 2 strides */
-	auto step = [&](uint64_t t, uint4 *win, uint4 *dsl, uint4 dv) -> uint4 {
+	/* step on tile t, whose descriptor dv travels in registers: the
+	 * window DMA of tile tw (2 steps ahead, its descriptor from the slot:
+	 * returned), the descriptor DMA of tile td (4 ahead), the claim of
+	 * the tile 5 ahead (into tn) */
+	auto step = [&](uint64_t t, uint4 *win, uint4 *dsl, uint4 dv, uint64_t tw,
+			uint64_t td, uint64_t &tn) -> uint4 {
 		const uint64_t i = t * kWave + lane;
 		bool skip = false;
 		if constexpr (FRAGS) {
@@ -1859,20 +1952,19 @@ __global__ __launch_bounds__(kBlock, 4) void xdp_rx_db_kernel(RxArgs a)
 		const bool active = (i < nfr) & !skip;
 		uint32_t F[18];
 		uint4 dn;
-		read_tile_db(win, dsl, lane, F, dn);
-		if constexpr (DIAG != 1 && DIAG != 2) {
-			if (have)
-				store_tile(a, pend);
-		}
-		issue_win(dn, t + 2 * nwaves < ntiles, win);
-		issue_desc(t + 4 * nwaves, dsl);
+		read_tile_db<kWaitN>(win, dsl, lane, F, dn);
+		if constexpr (DIAG != 1 && DIAG != 2)
+			store_tile(a, pend);
+		issue_win(dn, tw < ntiles, win);
+		issue_desc(td, dsl);
+		tn = claim(1);
 		if constexpr (DIAG == 1) {
 			uint32_t x = dv.x ^ dv.z;
 #pragma unroll
 			for (int k = 0; k < 16; k++)
 				x ^= F[k];
-			const uint64_t t0 = uniform_u64(i);
-			const uint32_t li = (uint32_t)(i - t0);
+			const uint64_t t0 = t * kWave;
+			const uint32_t li = (uint32_t)lane;
 			const __amdgpu_buffer_rsrc_t rv =
 				__builtin_amdgcn_make_buffer_rsrc(a.verdict + t0, 0, kWave, 0x00020000);
 			const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
@@ -1887,50 +1979,54 @@ __global__ __launch_bounds__(kBlock, 4) void xdp_rx_db_kernel(RxArgs a)
 							       active ? 16 * li : off, 0, 2);
 		} else {
 			fast_tile<false, DIAG != 2>(a, F, dv, i, active, dma, lane, w, &pend);
-			have = true;
 		}
 		return dn;
 	};
 
-	uint64_t t = wgid;
-	if (t < ntiles) {
+	/* the wave's tiles T0 < T1 < ...: the first five claimed at once */
+	const uint64_t first = claim(5);
+	uint64_t q0 = first, q1 = first + nb, q2 = first + 2 * nb, q3 = first + 3 * nb,
+		 q4 = first + 4 * nb, q5;
+	if (q0 < ntiles) {
 		/* prologue: descriptors of the first two tiles in registers;
-		 * then, in this order, descriptor DMA t+2, window DMA t, descriptor
-		 * DMA t+3, window DMA t+1: at least 5 ops younger than both of
-		 * step 0's and of step 1's inputs */
-		const uint4 d0 = *reinterpret_cast<const uint4 *>(a.desc + desc_at(t));
-		const uint4 d1 = *reinterpret_cast<const uint4 *>(a.desc + desc_at(t + nwaves));
-		issue_desc(t + 2 * nwaves, dsl0);
+		 * then, in this order, descriptor DMA T2, window DMA T0,
+		 * descriptor DMA T3, window DMA T1: at least 5 ops younger than
+		 * both of step 0's and of step 1's inputs */
+		const uint4 d0 = *reinterpret_cast<const uint4 *>(a.desc + desc_at(q0));
+		const uint4 d1 = *reinterpret_cast<const uint4 *>(a.desc + desc_at(q1));
+		issue_desc(q2, dsl0);
 		issue_win(d0, true, win0);
-		issue_desc(t + 3 * nwaves, dsl1);
-		issue_win(d1, t + nwaves < ntiles, win1);
+		issue_desc(q3, dsl1);
+		issue_win(d1, q1 < ntiles, win1);
+		/* kTileStores ops younger than step 0's and step 1's windows
+		 * (dropped: every lane out of range), as every later step has
+		 * the previous step's stores */
+		if constexpr (DIAG != 2)
+			store_tile(a, pend);
 		uint4 dc0 = d0, dc1 = d1;
 		for (;;) {
-			const uint4 n0 = step(t, win0, dsl0, dc0);
-			t += nwaves;
-			if (t >= ntiles)
+			const uint4 n0 = step(q0, win0, dsl0, dc0, q2, q4, q5);
+			q0 = q1; q1 = q2; q2 = q3; q3 = q4; q4 = q5;
+			if (q0 >= ntiles)
 				break;
-			const uint4 n1 = step(t, win1, dsl1, dc1);
-			t += nwaves;
-			if (t >= ntiles)
+			const uint4 n1 = step(q0, win1, dsl1, dc1, q2, q4, q5);
+			q0 = q1; q1 = q2; q2 = q3; q3 = q4; q4 = q5;
+			if (q0 >= ntiles)
 				break;
 			dc0 = n0;
 			dc1 = n1;
 		}
-	}
-	if constexpr (DIAG != 1 && DIAG != 2) {
-		if (have)
+		if constexpr (DIAG != 1 && DIAG != 2)
 			store_tile(a, pend);   /* the last tile's outputs */
 	}
-	if (lane == 0) {
-		a.xcount[wgid] = w.xout;
-		a.bcount[wgid] = w.bout;
-		a.ycount[wgid] = 0;   /* filled by the exception pass */
-	}
+	STAMP(wgid, lane, 1);
 
-	/* tail phase: the wave's own deferred frames, on the same LDS once
-	 * every DMA has landed (rx_tail waits) */
-	rx_tail(a, w, wgid, lane, reinterpret_cast<uint32_t *>(wl),
+	/* tail phase: the block's deferred frames, split over its waves, on
+	 * the same LDS once every DMA has landed (rx_tail waits) */
+	lds_dma_landed();
+	__syncthreads();
+	const uint32_t xc = ctl[1], bc = ctl[2];
+	rx_tail(a, w, rb, xc, bc, wid, kCuWaves, lane, reinterpret_cast<uint32_t *>(wl),
 		reinterpret_cast<uint64_t *>(wl + 272), wl, wl + kWave, w.cnt, w.my_bytes);
 
 	/* counters: this wave's own slot (kMaxRxBlocks..: per-wave slots) */
@@ -1947,6 +2043,7 @@ __global__ __launch_bounds__(kBlock, 4) void xdp_rx_db_kernel(RxArgs a)
 				slot[lane] += v;
 		}
 	}
+	STAMP(wgid, lane, 2);
 }
 
 /* Per-wave LDS of the fast kernel, in uint4: the tile loop's window buffer
@@ -2308,28 +2405,32 @@ static hipError_t launch_sized(RxArgs a, uint32_t max_blocks,
 static hipError_t launch_db(RxArgs a, uint32_t max_blocks, hipStream_t stream,
 			    hipEvent_t *ev)
 {
-	uint32_t cap = a.frags ? resident_blocks<xdp_rx_db_kernel<true>>()
-			       : resident_blocks<xdp_rx_db_kernel<false>>();
+	uint32_t cap = a.frags ? resident_blocks_dev<xdp_rx_db_kernel<true>, kCuBlock>(kMaxRxBlocks)
+			       : resident_blocks_dev<xdp_rx_db_kernel<false>, kCuBlock>(kMaxRxBlocks);
 	const uint32_t diag = a.diag;
 	if (cap < max_blocks)
 		max_blocks = cap;
-	const uint32_t blocks = rx_grid_blocks(a.n, max_blocks);
-	a.xregion = rx_xregion(a.n, blocks);
-	a.nregions = blocks * kWavesPerBlock;
+	/* one block per CU, fewer when the batch has fewer tiles than waves */
+	const uint64_t ntiles = ((uint64_t)a.n + kWave - 1) / kWave;
+	uint64_t blocks = (ntiles + kCuWaves - 1) / kCuWaves;
+	if (blocks > max_blocks)
+		blocks = max_blocks;
+	if (blocks == 0)
+		blocks = 1;
+	/* list regions per block: its share of the tiles */
+	a.xregion = (uint32_t)(((ntiles + blocks - 1) / blocks) * kWave);
+	a.nregions = (uint32_t)blocks;
 	if (ev)
 		(void)hipEventRecord(ev[0], stream);
+	const dim3 grid((uint32_t)blocks), blk(kCuBlock);
 	if (a.frags)
-		hipLaunchKernelGGL((xdp_rx_db_kernel<true>), dim3(blocks), dim3(kBlock), 0,
-				   stream, a);
+		hipLaunchKernelGGL((xdp_rx_db_kernel<true>), grid, blk, 0, stream, a);
 	else if (diag == 1)
-		hipLaunchKernelGGL((xdp_rx_db_kernel<false, 1>), dim3(blocks), dim3(kBlock), 0,
-				   stream, a);
+		hipLaunchKernelGGL((xdp_rx_db_kernel<false, 1>), grid, blk, 0, stream, a);
 	else if (diag == 2)
-		hipLaunchKernelGGL((xdp_rx_db_kernel<false, 2>), dim3(blocks), dim3(kBlock), 0,
-				   stream, a);
+		hipLaunchKernelGGL((xdp_rx_db_kernel<false, 2>), grid, blk, 0, stream, a);
 	else
-		hipLaunchKernelGGL((xdp_rx_db_kernel<false>), dim3(blocks), dim3(kBlock), 0,
-				   stream, a);
+		hipLaunchKernelGGL((xdp_rx_db_kernel<false>), grid, blk, 0, stream, a);
 	const hipError_t e = hipGetLastError();
 	if (ev && e == hipSuccess)
 		for (int k = 1; k < 4; k++)
@@ -2426,6 +2527,18 @@ __global__ __launch_bounds__(kBlock) void ip_fast_csum_kernel(
 		s += (uint32_t)h[o] | ((uint32_t)h[o + 1] << 8);
 	out[i] = (uint16_t)(~fold16(s) & 0xffff);
 }
+
+#ifdef XDPGPU_STAMPS
+} // namespace xdpgpu
+extern "C" int xdpgpu_stamps_read(unsigned long long *out)
+{
+	if (hipMemcpyFromSymbol(out, HIP_SYMBOL(xdpgpu::g_stamp), sizeof(xdpgpu::g_stamp)) !=
+	    hipSuccess)
+		return -5;
+	return 0;
+}
+namespace xdpgpu {
+#endif
 
 #ifdef XDPGPU_DBG
 } // namespace xdpgpu
