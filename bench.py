@@ -6,23 +6,25 @@ UMEM pool, xdpsock geometry), one pool shard per GPU (config 5 at N > 1).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
-A step = one RX launch (fast, bulk and exception kernels, back to back on
-one stream) over the whole 16 M-frame shard resident in HBM.  Timing: W
-untimed steps, barrier + synchronize, K timed steps, synchronize + barrier,
-max over ranks.  value = frames processed by all ranks / that time (Mpps,
-whole job).  The roofline figure is the algorithmic bytes of a launch
-(113 B/frame) over the launch's kernel time from HIP events
-recorded on the launch stream around each of the three kernels
-(xdpgpu_kernel_times), in a second pass of K launches on a context with
-XDPGPU_CFG_TIMING so the events do not perturb the timed steps; the
-per-kernel split is reported beside it (the event packets add a few us per
-kernel, so the split is conservative).  traffic
-is the HBM bytes per launch from the committed rocprofv3 PMC summary
-(profiles/r01_pmc.json, tools/pmc_profile.sh).  The CPU baseline is the
-oracle (oracle/xdp_oracle.c, a restatement of the reference C) timed on this
-host, rank 0 at N = 1 only, on a bounded sample.  Secondary lines: config 2
-geometry at 1500 B, config 3 (16 M IMIX, 44 B network_tuple) and config 4
-(16 M x 128 B nat64 ingress).
+A step = one RX launch (xdp_rx_db_kernel: one block per CU, the tile loop
+and the deferred-frame tail in one kernel) over the whole 16 M-frame shard
+resident in HBM.  Timing: W untimed steps, barrier + synchronize, K timed
+steps, synchronize + barrier, max over ranks.  value = frames processed by
+all ranks / that time (Mpps, whole job).  The roofline figure is the
+algorithmic bytes of a launch (113 B/frame) over the
+launch's kernel time from HIP events recorded on the launch stream around
+the kernel (xdpgpu_kernel_times), in a second pass of K launches on a
+context with XDPGPU_CFG_TIMING so the events do not perturb the timed
+steps.  traffic is the HBM bytes per launch from the committed rocprofv3
+PMC summary (profiles/*_pmc.json, tools/pmc_profile.sh).  The CPU baseline
+is the lean CPU leg (oracle/cpu_leg.c: the same outputs as the oracle,
+checked on the sample) on this host's cores, rank 0 at N = 1 only, on a
+bounded sample: one pinned thread, then one thread per CPU of the affinity
+set, with the CPU model and the calibration probe beside the reference
+headers' own routines (oracle/_ref).  Secondary lines: config 2 geometry
+at 1500 B, config 3 (16 M IMIX, 44 B network_tuple), config 4 (16 M x
+128 B nat64 ingress), multi-buffer 9000 B packets and the ICMPv6 echo
+responder.
 """
 from __future__ import annotations
 
@@ -44,7 +46,7 @@ import shard  # noqa: E402
 import xdpgpu  # noqa: E402
 
 BYTES_PER_FRAME = 16 + 64 + 16 + 16 + 1   # desc + frame + result + tuple + verdict
-RX_KERNELS = ("xdp_rx_kernel", "xdp_rx_bulk_kernel", "xdp_rx_generic_kernel")
+RX_KERNELS = ("xdp_rx_db_kernel",)
 HBM_PEAK_GBS = 8000.0                      # MI355X HBM3E, MI355X_MICROARCH.md
 METRIC = ("Mpps + GB/s device-resident parse+csum+jhash, 64B & 1500B frames, "
           "1/2/4/8 GPU")
@@ -95,8 +97,22 @@ def kernel_breakdown(tctx, d_umem, usize, d_desc, n, d_v, d_res, d_tup, stream,
     return tctx.kernel_times()
 
 
-def cpu_baseline(umem, descs, budget_s: float = 10.0):
-    """The oracle (restated reference C) on this host's cores."""
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(umem, descs, flags, fmt, budget_s: float = 10.0):
+    """The lean CPU leg (oracle/cpu_leg.c) on this host's cores: one pinned
+    thread, then one thread per CPU of the affinity set; its outputs checked
+    against the oracle on part of the sample; the calibration probe (the
+    survey probe's work) beside the reference headers' routines."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     oracle.lib()
@@ -104,21 +120,35 @@ def cpu_baseline(umem, descs, budget_s: float = 10.0):
         cores = len(os.sched_getaffinity(0))
     except AttributeError:
         cores = os.cpu_count() or 1
-    threads = max(1, min(16, cores))
     sample = descs[: 1 << 21]
-    # calibrate on one pass, then size the run to ~budget_s of wall time
-    t1 = oracle.bench(umem, sample[: 1 << 18], 1, 1)
-    st_mpps = (1 << 18) / t1 / 1e6
-    dt = oracle.bench(umem, sample, threads, 1)
+    one = sample[: 1 << 19]
+    t1, _ = oracle.leg_bench(umem, one, 1, 1, True, flags, 0, fmt)
+    reps1 = max(1, int(3.0 / max(t1, 1e-3)))
+    t1, _ = oracle.leg_bench(umem, one, 1, reps1, True, flags, 0, fmt)
+    st_mpps = len(one) * reps1 / t1 / 1e6
+    dt, _ = oracle.leg_bench(umem, sample, cores, 1, True, flags, 0, fmt)
     reps = max(1, int(budget_s / max(dt, 1e-3)))
-    dt = oracle.bench(umem, sample, threads, reps)
+    dt, (v, res, tup) = oracle.leg_bench(umem, sample, cores, reps, True, flags, 0, fmt)
     mpps = len(sample) * reps / dt / 1e6
-    return {"value": round(mpps, 2), "unit": "Mpps", "cores": threads,
-            "kind": "port",
+    k = 1 << 16
+    ov, ores, otup, _ = oracle.process(umem, sample[:k], flags, 0, fmt)
+    checked = bool(np.array_equal(v[:k], ov) and
+                   res[:k].tobytes() == ores.tobytes() and
+                   tup[: k * xdpgpu.TUPLE_BYTES[fmt]].tobytes() == otup.tobytes())
+    mine, ref = oracle.probe_pair(umem, sample[: 1 << 20], 3)
+    cal = {"probe": "parse + IPv4 csum + UDP csum + jhash(13 B), 1 thread",
+           "leg_mpps": round((1 << 20) / mine / 1e6, 1),
+           "reference_headers_mpps": round((1 << 20) / ref / 1e6, 1) if ref else None}
+    if ref:
+        cal["leg_over_reference"] = round(ref / mine, 3)
+    return {"value": round(mpps, 2), "unit": "Mpps", "cores": cores,
+            "kind": "port", "cpu_model": cpu_model(),
             "gbps": round(mpps * 1e6 * BYTES_PER_FRAME / 1e9, 2),
             "single_thread_mpps": round(st_mpps, 2),
-            "sample": f"{len(sample)} config-2 frames x {reps} passes of oracle/xdp_oracle.c "
-                      f"(gcc -O2) on {threads} threads ({dt:.1f} s)"}
+            "outputs_match_oracle": checked, "calibration": cal,
+            "sample": f"{len(sample)} config-2 frames x {reps} passes of oracle/cpu_leg.c "
+                      f"(gcc -O2) on {cores} threads pinned one per CPU ({dt:.1f} s); "
+                      f"1 pinned thread: {len(one)} frames x {reps1} passes"}
 
 
 def pmc_traffic(n: int, size: int):
@@ -247,6 +277,54 @@ def frags_run(dev, stream, n, steps, local, size=9000, chunk=4096):
     return out
 
 
+def echo_run(dev, stream, n, steps, local, size=128, ppm=200000):
+    """The ICMPv6 echo responder (af_xdp_user.c:968-1040) as a throughput
+    mode: n frames of which ppm / 1e6 are echo requests, rewritten in place
+    into replies (TX).  The rewrite changes the UMEM, so every step
+    restores the pool from a pristine device copy first (outside the timed
+    region); each launch is timed with HIP events on its stream."""
+    u, ds, ex = xdpgpu.pool_generate(n, xdpgpu.POOL_UDP4, size, 0x5EED0042,
+                                     ppm_echo6=ppm)
+    # the generator expects REDIRECT for a request (no responder): TX here
+    eff = (ds["addr"] & ((1 << 48) - 1)) + (ds["addr"] >> 48)
+    req = ((u[eff + 12] == 0x86) & (u[eff + 13] == 0xDD) & (u[eff + 20] == 58) &
+           (u[eff + 54] == 128) & (ds["len"] >= 62) & (ex == xdpgpu.REDIRECT))
+    want = np.where(req, xdpgpu.TX, ex).astype(np.uint8)
+    pristine = to_dev(u, dev)
+    work = torch.empty_like(pristine)
+    d_desc = to_dev(ds, dev, 0)
+    d_v = torch.empty(n, dtype=torch.uint8, device=dev)
+    d_res = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    d_tup = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    ms = []
+    with xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT | xdpgpu.CFG_ICMP6_ECHO, 0,
+                       xdpgpu.TUPLE_V4, 64) as g:
+        for k in range(steps + 2):
+            with torch.cuda.stream(stream):
+                work.copy_(pristine, non_blocking=True)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            g.process_dev(work, u.nbytes, d_desc, n, d_v, d_res, d_tup, stream)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            if k >= 2:
+                ms.append(e0.elapsed_time(e1))
+    v = d_v.cpu().numpy()
+    ok = bool(np.array_equal(v, want))
+    t = float(np.mean(ms))
+    ntx = int(req.sum())
+    algo = n * (16 + 16 + 16 + 1) + int(ds["len"].astype(np.int64).sum()) + ntx * 64
+    out = {"workload": f"{n} x {size}B frames, {ppm / 1e4:.0f} % ICMPv6 echo requests "
+                       "answered in place (XDPGPU_CFG_ICMP6_ECHO)",
+           "frames": n, "tx_frames": ntx, "mpps": round(n / t / 1e3, 1),
+           "kernel_ms": round(t, 4), "algorithmic_bytes_per_launch": algo,
+           "gbps": round(algo / t / 1e6, 1),
+           "roofline_frac": round(algo / t / 1e6 / HBM_PEAK_GBS, 4), "verdicts_ok": ok}
+    del pristine, work, d_desc, d_v, d_res, d_tup
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -257,8 +335,8 @@ def main():
     ap.add_argument("--window", type=int, default=64)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
-    ap.add_argument("--legs", default="1500,imix,nat64,frags",
-                    help="secondary workloads: comma list of 1500, imix, nat64, frags")
+    ap.add_argument("--legs", default="1500,imix,nat64,frags,echo",
+                    help="secondary workloads: comma list of 1500, imix, nat64, frags, echo")
     ap.add_argument("--imix-frames", type=int, default=16 << 20)
     ap.add_argument("--nat64-frames", type=int, default=16 << 20)
     ap.add_argument("--e2e", action="store_true", help="also time the host path")
@@ -267,9 +345,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)      # before RCCL binds the rank
     if world > 1:
         dist.init_process_group("nccl")
-    torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
     # config 2 shard (config 5 at N > 1: same per-GPU content, seed offset)
@@ -334,6 +412,8 @@ def main():
                                                    local)
         if "frags" in legs:
             secondary["multibuffer_9000B"] = frags_run(dev, stream, 1 << 16, steps2, local)
+        if "echo" in legs:
+            secondary["icmp6_echo"] = echo_run(dev, stream, 8 << 20, steps2, local)
 
     e2e = None
     if args.e2e and rank == 0 and world == 1:
@@ -343,29 +423,33 @@ def main():
                           max_batch=1 << 20)
         h.register_umem(umem)
         B = 1 << 20
-        v3 = np.zeros(n3, np.uint8)
-        r3 = np.zeros(n3, xdpgpu.RESULT_DTYPE)
-        t3 = np.zeros(n3, xdpgpu.TUPLE4_DTYPE)
-        sub = [np.ascontiguousarray(descs[lo:lo + B]) for lo in range(0, n3, B)]
+        # page-locked descriptor and output arrays (xdpgpu_host_alloc), as
+        # an RX loop keeps them
+        hb = [xdpgpu.HostBuffer(n3, dt) for dt in
+              (xdpgpu.DESC_DTYPE, np.uint8, xdpgpu.RESULT_DTYPE, xdpgpu.TUPLE4_DTYPE)]
+        d3, v3, r3, t3 = (b.array for b in hb)
+        d3[:] = descs[:n3]
         for rep in range(2):
             t0 = time.perf_counter()
-            for k, d in enumerate(sub):
+            for k, lo in enumerate(range(0, n3, B)):
                 slot = k & 1
                 if k >= 2:
                     h.wait(slot)
-                lo = k * B
-                h.submit(slot, d, v3[lo:lo + len(d)], r3[lo:lo + len(d)],
-                         t3[lo:lo + len(d)])
+                hi = min(n3, lo + B)
+                h.submit(slot, d3[lo:hi], v3[lo:hi], r3[lo:hi], t3[lo:hi])
             h.wait(0)
             h.wait(1)
             te = time.perf_counter() - t0
         e2e = {"mpps": round(n3 / te / 1e6, 1), "frames": n3, "batch": B,
+               "pinned_buffers": True,
                "verdicts_ok": bool(np.array_equal(v3, expect[:n3]))}
         h.close()
+        for b in hb:
+            b.close()
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(umem, descs)
+        cpu = cpu_baseline(umem, descs, xdpgpu.CFG_DEFAULT, xdpgpu.TUPLE_V4)
 
     if rank == 0:
         traffic = pmc_traffic(n, args.size)

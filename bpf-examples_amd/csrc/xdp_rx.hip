@@ -57,18 +57,19 @@ __device__ __forceinline__ bool dbg_bad(bool bad, uint32_t code, uint64_t val)
 #endif
 
 /* Timing builds (-DXDPGPU_STAMPS, tools/dbg_build.sh stamps): each wave of
- * the double-buffered kernel records s_memrealtime (100 MHz) at its start,
- * at the end of its tile loop and at its end, read by xdpgpu_stamps_read. */
+ * the double-buffered kernel records s_memrealtime (100 MHz) at its start
+ * (0), the end of its tile loop (1), its end (2), the ends of its tail's
+ * exception (4) and bulk (5) passes; read by xdpgpu_stamps_read. */
 #ifdef XDPGPU_STAMPS
 constexpr int kStampWaves = 8192;
-__device__ unsigned long long g_stamp[4 * kStampWaves];
+__device__ unsigned long long g_stamp[8 * kStampWaves];
 /* k == 0 also records where the wave runs: HW_ID | XCC_ID << 32 */
 #define STAMP(wgid, lane, k)                                                   \
 	do {                                                                   \
 		if ((lane) == 0 && (wgid) < (uint64_t)kStampWaves) {           \
-			g_stamp[4 * (wgid) + (k)] = __builtin_amdgcn_s_memrealtime(); \
+			g_stamp[8 * (wgid) + (k)] = __builtin_amdgcn_s_memrealtime(); \
 			if ((k) == 0)                                          \
-				g_stamp[4 * (wgid) + 3] =                      \
+				g_stamp[8 * (wgid) + 3] =                      \
 					(unsigned long long)(uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) | \
 					((unsigned long long)(uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32); \
 		}                                                              \
@@ -1080,7 +1081,7 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 					   uint64_t &my_bytes)
 {
 	uint32_t *part = reinterpret_cast<uint32_t *>(part4);
-	static_assert(G == 16 || G == 8, "group of 16 or 8 lanes per frame");
+	static_assert(G == 16 || G == 8 || G == 4, "group of 16, 8 or 4 lanes per frame");
 	const uint32_t sub = lane & (G - 1);
 	const bool act = (uint32_t)lane < nb;
 	uint4 ye = make_uint4(0, 0, 0, 0);
@@ -1146,8 +1147,9 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 		if (dq) {
 			if (done) {
 				part[16 * k + sub] = acc;
-				if constexpr (G == 8)
-					part[16 * k + 8 + sub] = 0;
+#pragma unroll
+				for (int z = 1; z < 16 / G; z++)
+					part[16 * k + G * z + sub] = 0;
 				acc = 0;
 				k = nxt + (uint32_t)__popcll(dq & ((1ull << (lane & ~(G - 1))) - 1));
 				live = k < nb;
@@ -1430,11 +1432,19 @@ __device__ __forceinline__ void store_tile(const RxArgs &a, const TileOut &o)
 	const uint32_t b = out ? tb * o.li : kOff;
 	const v4u_t w0 = net ? (v4u_t){0u, 0u, 0xffff0000u, o.sa}
 			     : (v4u_t){o.sa, o.da, o.ports, o.proto | (2u << 8) | (o.vid << 16)};
-	__builtin_amdgcn_raw_buffer_store_b128(w0, rt, b, 0, 2);
+	/* 16-byte tuples: whole lines, streamed (nt).  44-byte tuples: the
+	 * lanes' 16-byte pieces straddle lines that other stores of the tile
+	 * complete, so they stay in L2 to merge there (nt: 2x the loop time on
+	 * IMIX) */
+	if (net) {
+		__builtin_amdgcn_raw_buffer_store_b128(w0, rt, b, 0, 0);
+	} else {
+		__builtin_amdgcn_raw_buffer_store_b128(w0, rt, b, 0, 2);
+	}
 	__builtin_amdgcn_raw_buffer_store_b128((v4u_t){o.ports & 0xffff, 0u, 0u, 0xffff0000u},
-					       rt, net && out ? b + 16 : kOff, 0, 2);
+					       rt, net && out ? b + 16 : kOff, 0, 0);
 	__builtin_amdgcn_raw_buffer_store_b96((v3u_t){o.da, o.ports >> 16, o.proto | (2u << 16)},
-					      rt, net && out ? b + 32 : kOff, 0, 2);
+					      rt, net && out ? b + 32 : kOff, 0, 0);
 }
 
 /* Lane 0's fetch-and-add of v on an LDS counter, returned to every lane.
@@ -1668,9 +1678,9 @@ __device__ __forceinline__ void wave_stats_to_lds(const RxArgs &a,
 
 /*
  * Tail phase of the double-buffered fast kernel: the block finishes its
- * deferred frames in the order of the separate kernels (exception batches,
- * then the bulk list, then the exception frames' deferred payload sums),
- * the batches of each pass split over its waves; each wave reuses its own
+ * deferred frames, the exception batches, the bulk batches and the
+ * exception frames' deferred payload sums, from one queue of batches (an
+ * LDS counter, ctl[3]); each wave reuses its own
  * LDS: win (64 rows of 17 dwords) and gtab (64 u64) for the exception
  * batches, meta (64 uint4) and part (256 uint4) for the bulk batches.
  * Called by every wave of the block (barriers) after a vmcnt(0) and a
@@ -1679,38 +1689,80 @@ __device__ __forceinline__ void wave_stats_to_lds(const RxArgs &a,
  * block's other waves, whose L1 lines for them are never loaded before
  * (read-once lists).
  */
+/* the tail's payload streaming: groups of kTailG lanes per frame, kTailU
+ * 16-byte loads per lane and step (1 KiB per frame and step; 4-lane
+ * groups of 8 loads, every load of a 570-byte IMIX payload useful, ran
+ * 8 % slower on IMIX and 13 % on 1500 B: the loads of an instruction
+ * then touch 16 frames) */
+#ifndef XDP_TAIL_G
+#define XDP_TAIL_G 16
+#endif
+#ifndef XDP_TAIL_U
+#define XDP_TAIL_U 4
+#endif
+constexpr int kTailG = XDP_TAIL_G, kTailU = XDP_TAIL_U;
 __device__ __forceinline__ void rx_tail(const RxArgs &a, const FastWave &w,
 					uint64_t rb, uint32_t xc, uint32_t bc,
-					int wid, int nw, int lane, uint32_t *win,
+					int wid, int nw, uint32_t *ctl, int lane,
+					uint32_t *win,
 					uint64_t *gtab, uint4 *meta, uint4 *part4,
 					uint32_t (&cnt)[CNT_FRAG + 1], uint64_t &my_bytes)
 {
 	uint4 *yl = a.ylist + rb * a.xregion;
 	uint32_t *yc = a.ycount + rb;
-	const uint32_t stride = (uint32_t)nw * kWave;
-	for (uint32_t b = (uint32_t)wid * kWave; b < xc; b += stride) {
-		const bool act = b + lane < xc;
-		uint64_t i = act ? w.xl[b + lane] : 0;
-		const bool bad = act && DBG_BAD(i >= a.n, 1, i);
-		i = bad ? 0 : i;
-		generic_batch<64>(a, win, gtab, lane, i, act && !bad, yl, yc, cnt, my_bytes);
+	/* One queue of batches, each wave claiming the next: the exception
+	 * batches (which list the exception frames' long payloads), the bulk
+	 * batches, then those payload batches.  A wave that reaches the
+	 * payload batches first waits until every exception batch is done
+	 * (ctl[5] counts them, each after a vmcnt(0) that makes its list
+	 * entries visible): by then only batches already claimed remain. */
+	const uint32_t nbb = (bc + kWave - 1) / kWave, nxb = (xc + kWave - 1) / kWave;
+	uint32_t ycn = 0, nyb = 0;
+	bool ready = nxb == 0;
+	for (;;) {
+		const uint32_t q = lds_fetch_add(ctl + 3, 1, lane);
+		if (q < nxb) {
+			const uint32_t b = q * kWave;
+			const bool act = b + lane < xc;
+			uint64_t i = act ? w.xl[b + lane] : 0;
+			const bool bad = act && DBG_BAD(i >= a.n, 1, i);
+			i = bad ? 0 : i;
+			generic_batch<64>(a, win, gtab, lane, i, act && !bad, yl, yc, cnt,
+					  my_bytes);
+			lds_dma_landed();
+			(void)lds_fetch_add(ctl + 5, 1, lane);
+			continue;
+		}
+		if (q < nxb + nbb) {
+			const uint32_t b = (q - nxb) * kWave;
+			bulk_batch<kTailU, true, false, kTailG>(a, meta, part4, lane, w.bl + b,
+								bc - b < (uint32_t)kWave ? bc - b : kWave,
+								cnt, my_bytes);
+			continue;
+		}
+		if (!ready) {
+			while (lds_fetch_add(ctl + 5, 0, lane) < nxb)
+				__builtin_amdgcn_s_sleep(2);
+			ready = true;
+		}
+		if (!nyb && !ycn) {
+			/* the count the exception batches' atomics left (read at
+			 * the L2, where they were made) */
+			if (lane == 0)
+				ycn = atomicAdd(yc, 0u);
+			ycn = __builtin_amdgcn_readfirstlane(ycn);
+			nyb = (ycn + kWave - 1) / kWave;
+		}
+		const uint32_t yq = q - nxb - nbb;
+		if (yq >= nyb)
+			break;
+		const uint32_t b = yq * kWave;
+		bulk_batch<kTailU, true, true, kTailG>(a, meta, part4, lane, yl + b,
+						      ycn - b < (uint32_t)kWave ? ycn - b : kWave,
+						      cnt, my_bytes);
 	}
-	lds_dma_landed();
-	__syncthreads();
-	for (uint32_t b = (uint32_t)wid * kWave; b < bc; b += stride)
-		bulk_batch<4, true, false, 16>(a, meta, part4, lane, w.bl + b,
-					       bc - b < (uint32_t)kWave ? bc - b : kWave,
-					       cnt, my_bytes);
-	/* the count the exception batches' atomics left (read at the L2,
-	 * where they were made) */
-	uint32_t ycn = 0;
-	if (lane == 0)
-		ycn = atomicAdd(yc, 0u);
-	ycn = __builtin_amdgcn_readfirstlane(ycn);
-	for (uint32_t b = (uint32_t)wid * kWave; b < ycn; b += stride)
-		bulk_batch<4, true, true, 16>(a, meta, part4, lane, yl + b,
-					      ycn - b < (uint32_t)kWave ? ycn - b : kWave,
-					      cnt, my_bytes);
+	STAMP(rb * nw + wid, lane, 4);
+	STAMP(rb * nw + wid, lane, 5);
 }
 
 /*
@@ -1853,8 +1905,9 @@ template <bool FRAGS, int DIAG = 0>
 __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 {
 	__shared__ uint4 lds_all[kCuWaves * kDbWave];
-	/* the block's tile claims and list lengths (exception, bulk) */
-	__shared__ uint32_t ctl[4];
+	/* the block's tile claims, list lengths (exception, bulk) and the
+	 * tail's batch claims (its two passes) */
+	__shared__ uint32_t ctl[8];
 	/* the counted wait: the 5 DMAs of the step before and, but for the
 	 * no-store variant, the kTileStores output stores issued after them
 	 * (kept in the count, so that no step waits for stores) */
@@ -1874,7 +1927,7 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 	const uint64_t wgid = rb * kCuWaves + wid;
 
 	if (threadIdx.x == 0) {
-		ctl[0] = ctl[1] = ctl[2] = 0;
+		ctl[0] = ctl[1] = ctl[2] = ctl[3] = ctl[4] = ctl[5] = 0;
 		a.ycount[rb] = 0;      /* filled by the exception pass */
 	}
 	lds_dma_landed();
@@ -2026,7 +2079,7 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 	lds_dma_landed();
 	__syncthreads();
 	const uint32_t xc = ctl[1], bc = ctl[2];
-	rx_tail(a, w, rb, xc, bc, wid, kCuWaves, lane, reinterpret_cast<uint32_t *>(wl),
+	rx_tail(a, w, rb, xc, bc, wid, kCuWaves, ctl, lane, reinterpret_cast<uint32_t *>(wl),
 		reinterpret_cast<uint64_t *>(wl + 272), wl, wl + kWave, w.cnt, w.my_bytes);
 
 	/* counters: this wave's own slot (kMaxRxBlocks..: per-wave slots) */

@@ -132,6 +132,8 @@ def ref_lib() -> Optional[C.CDLL]:
         r.ref_jhash_2words.restype = u32
         r.ref_jhash_1word.argtypes = [u32, u32]
         r.ref_jhash_1word.restype = u32
+        r.ref_probe.argtypes = [vp, C.c_uint64, vp, u32, u32, C.POINTER(C.c_uint64)]
+        r.ref_probe.restype = C.c_double
         _r = r
     return _r
 
@@ -218,3 +220,74 @@ def v6addr_to_v4(a6: bytes, plen: int):
     pref = C.create_string_buffer(16)
     ok = o.oracle_v6addr_to_v4(buf(a6), plen, a4, pref)
     return (bytes(a4.raw[:4]), bytes(pref.raw[:16])) if ok else None
+
+
+def _leg_lib() -> C.CDLL:
+    o = lib()
+    if not hasattr(o, "_leg_bound"):
+        vp, u32, u64 = C.c_void_p, C.c_uint32, C.c_uint64
+        o.cpu_leg_process.argtypes = [vp, u64, vp, u32, u32, u32, u32, vp, vp, vp, vp]
+        o.cpu_leg_process.restype = u32
+        o.cpu_leg_bench.argtypes = [vp, u64, vp, u32, u32, u32, u32, vp, vp, vp, u32, u32,
+                                    C.c_int]
+        o.cpu_leg_bench.restype = C.c_double
+        o.cpu_leg_probe.argtypes = [vp, u64, vp, u32, u32, C.POINTER(C.c_uint64)]
+        o.cpu_leg_probe.restype = C.c_double
+        o._leg_bound = True
+    return o
+
+
+def leg_process(umem: np.ndarray, descs: np.ndarray, flags: int = 0x5,
+                initval: int = 0, tuple_fmt: int = 1):
+    """The lean CPU leg (oracle/cpu_leg.c): same outputs as process();
+    also returns how many frames took its fast shape."""
+    o = _leg_lib()
+    descs = np.ascontiguousarray(descs, DESC_DTYPE)
+    n = len(descs)
+    verdict = np.zeros(n, np.uint8)
+    res = np.zeros(n, RESULT_DTYPE)
+    tb = TUPLE_BYTES[tuple_fmt]
+    tup = np.zeros(n * tb if tb else 1, np.uint8)
+    st = OStats()
+    nfast = o.cpu_leg_process(umem.ctypes.data, umem.nbytes, descs.ctypes.data, n, flags,
+                              initval, tuple_fmt, verdict.ctypes.data, res.ctypes.data,
+                              tup.ctypes.data if tb else None, C.byref(st))
+    stats = {"frames": st.frames, "bytes": st.bytes, "verdict": list(st.verdict),
+             "l3_bad": st.l3_bad, "l4_bad": st.l4_bad, "l4_absent": st.l4_absent,
+             "frag": st.frag}
+    return verdict, res, tup, stats, nfast
+
+
+def leg_bench(umem: np.ndarray, descs: np.ndarray, threads: int, reps: int, pin: bool,
+              flags: int = 0x5, initval: int = 0, tuple_fmt: int = 1):
+    """Wall seconds for `reps` passes of the lean leg over descs on
+    `threads` threads (pinned to the affinity set's CPUs when pin), and the
+    outputs of the last pass."""
+    o = _leg_lib()
+    descs = np.ascontiguousarray(descs, DESC_DTYPE)
+    n = len(descs)
+    verdict = np.zeros(n, np.uint8)
+    res = np.zeros(n, RESULT_DTYPE)
+    tb = TUPLE_BYTES[tuple_fmt]
+    tup = np.zeros(max(1, n * tb), np.uint8)
+    dt = o.cpu_leg_bench(umem.ctypes.data, umem.nbytes, descs.ctypes.data, n, flags,
+                         initval, tuple_fmt, verdict.ctypes.data, res.ctypes.data,
+                         tup.ctypes.data if tb else None, threads, reps, 1 if pin else 0)
+    return dt, (verdict, res, tup)
+
+
+def probe_pair(umem: np.ndarray, descs: np.ndarray, reps: int):
+    """Seconds of the survey probe's work (parse, IPv4 and UDP checksums,
+    13-byte jhash) per pass on one thread: (this leg's arithmetic, the
+    reference headers' routines or None off this container)."""
+    o = _leg_lib()
+    descs = np.ascontiguousarray(descs, DESC_DTYPE)
+    acc = C.c_uint64(0)
+    mine = o.cpu_leg_probe(umem.ctypes.data, umem.nbytes, descs.ctypes.data, len(descs),
+                           reps, C.byref(acc)) / reps
+    r = ref_lib()
+    ref = None
+    if r is not None:
+        ref = r.ref_probe(umem.ctypes.data, umem.nbytes, descs.ctypes.data, len(descs),
+                          reps, C.byref(acc)) / reps
+    return mine, ref

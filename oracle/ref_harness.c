@@ -32,3 +32,57 @@ uint32_t ref_jhash2(const uint32_t *k, uint32_t len, uint32_t initval) { return 
 uint32_t ref_jhash_3words(uint32_t a, uint32_t b, uint32_t c, uint32_t iv) { return jhash_3words(a, b, c, iv); }
 uint32_t ref_jhash_2words(uint32_t a, uint32_t b, uint32_t iv) { return jhash_2words(a, b, iv); }
 uint32_t ref_jhash_1word(uint32_t a, uint32_t iv) { return jhash_1word(a, iv); }
+
+/* Calibration probe (SURVEY.md §5 "survey probe"): per frame a minimal
+ * Ethernet/VLAN/IPv4/UDP parse, ip_fast_csum over the IPv4 header,
+ * udp_csum over the UDP datagram and jhash of 13 bytes (addresses, ports,
+ * protocol), all by the reference headers' own routines; the same work as
+ * cpu_leg_probe (oracle/cpu_leg.c).  Returns wall seconds of reps passes on
+ * the calling thread; *acc receives a value of the results (kept live). */
+#include <string.h>
+#include <time.h>
+
+struct ref_desc { uint64_t addr; uint32_t len; uint32_t options; };
+
+double ref_probe(const uint8_t *umem, uint64_t umem_size, const struct ref_desc *d,
+		 uint32_t n, uint32_t reps, uint64_t *acc)
+{
+	struct timespec t0, t1;
+	uint64_t x = 0;
+	uint32_t r, i;
+
+	clock_gettime(CLOCK_MONOTONIC, &t0);
+	for (r = 0; r < reps; r++) {
+		for (i = 0; i < n; i++) {
+			const uint64_t eff = (d[i].addr & ((1ull << 48) - 1)) + (d[i].addr >> 48);
+			const uint32_t len = d[i].len;
+			const uint8_t *p = umem + eff;
+			uint32_t l3 = 14, cl, sa, da;
+			uint16_t et;
+			uint8_t key[13];
+
+			if (len < 42 || eff > umem_size - len)
+				continue;
+			memcpy(&et, p + 12, 2);
+			if (et == htons(0x8100))
+				l3 = 18;
+			memcpy(&et, p + l3 - 2, 2);
+			if (et != htons(0x0800) || p[l3] != 0x45 || p[l3 + 9] != 17)
+				continue;
+			x += (uint16_t)ip_fast_csum(p + l3, 5);
+			cl = ntohs(*(const uint16_t *)(p + l3 + 24));
+			if (l3 + 20 + cl > len)
+				continue;
+			memcpy(&sa, p + l3 + 12, 4);
+			memcpy(&da, p + l3 + 16, 4);
+			x += udp_csum(sa, da, cl, 17, (__u16 *)(p + l3 + 20));
+			memcpy(key, p + l3 + 12, 8);
+			memcpy(key + 8, p + l3 + 20, 4);
+			key[12] = 17;
+			x += jhash(key, 13, 0);
+		}
+	}
+	clock_gettime(CLOCK_MONOTONIC, &t1);
+	*acc = x;
+	return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}

@@ -783,6 +783,37 @@ static void emit_tuple(const struct frame_out *o, uint32_t fmt, void *tuples,
 	}
 }
 
+/* One single-descriptor frame with oracle_process's outputs at index i (the
+ * lean CPU leg's path for every frame outside its fast shape). */
+void oracle_frame_one(uint8_t *umem, uint64_t umem_size, const struct xdpgpu_desc *d,
+		      uint32_t cfg_flags, uint32_t initval, uint32_t tuple_fmt,
+		      uint32_t i, uint8_t *verdict, struct xdpgpu_result *res,
+		      void *tuples, struct xdpgpu_stats *stats)
+{
+	struct frame_out o;
+
+	frame_pipeline(umem, umem_size, d, cfg_flags, initval, &o);
+	if (o.verdict == XDPGPU_ABORTED || o.verdict == XDPGPU_PASS) {
+		uint8_t v = o.verdict;
+
+		memset(&o, 0, sizeof(o));
+		o.verdict = v;
+	}
+	verdict[i] = o.verdict;
+	if (res)
+		res[i] = o.r;
+	emit_tuple(&o, tuple_fmt, tuples, i);
+	if (stats) {
+		stats->frames++;
+		stats->bytes += d->len;
+		stats->verdict[o.verdict]++;
+		stats->l3_bad += o.l3_bad;
+		stats->l4_bad += o.l4_bad;
+		stats->l4_absent += o.l4_absent;
+		stats->frag += o.frag;
+	}
+}
+
 int oracle_process(uint8_t *umem, uint64_t umem_size,
 		   const struct xdpgpu_desc *descs, uint32_t n,
 		   uint32_t cfg_flags, uint32_t initval, uint32_t tuple_fmt,

@@ -4,12 +4,13 @@
 #           xdpgpu_debug_read
 #   stamps  -DXDPGPU_STAMPS: per-wave s_memrealtime stamps,
 #           xdpgpu_stamps_read
+#   NAME "DEFINES"  any other name: an A/B build with those -D flags
 set -eu
 kind=${1:-dbg}
 case $kind in
 dbg) def=-DXDPGPU_DBG ;;
 stamps) def=-DXDPGPU_STAMPS ;;
-*) echo "unknown build $kind" >&2; exit 2 ;;
+*) def=${2:?"defines for build $kind"} ;;
 esac
 root=$(git rev-parse --show-toplevel)
 out=$root/build/$kind

@@ -18,27 +18,29 @@ import xdpgpu  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 16 << 20
 tune = int(sys.argv[2], 0) if len(sys.argv) > 2 else 0
+kind = int(sys.argv[3]) if len(sys.argv) > 3 else xdpgpu.POOL_UDP4
+fmt = int(sys.argv[4]) if len(sys.argv) > 4 else xdpgpu.TUPLE_V4
 lib = xdpgpu.load_library()
 lib.xdpgpu_stamps_read.argtypes = [C.c_void_p]
-umem, descs, _ = xdpgpu.pool_generate(n, xdpgpu.POOL_UDP4, 64, 0x5EED0002)
+umem, descs, _ = xdpgpu.pool_generate(n, kind, 64, 0x5EED0002 if kind == 0 else 0x5EED0003)
 dev = torch.device("cuda:0")
 d_umem = torch.zeros(umem.nbytes + 64, dtype=torch.uint8, device=dev)
 d_umem[: umem.nbytes].copy_(torch.from_numpy(umem))
 d_desc = torch.from_numpy(descs.view(np.uint8)).to(dev)
 d_v = torch.empty(n, dtype=torch.uint8, device=dev)
 d_res = torch.empty(n * 16, dtype=torch.uint8, device=dev)
-d_tup = torch.empty(n * 16, dtype=torch.uint8, device=dev)
-ctx = xdpgpu.XdpGpu(0, xdpgpu.CFG_DEFAULT, 0, xdpgpu.TUPLE_V4, 64, tune=tune)
-st = np.zeros(4 * 8192, np.uint64)
+d_tup = torch.empty(n * 44, dtype=torch.uint8, device=dev)
+ctx = xdpgpu.XdpGpu(0, xdpgpu.CFG_DEFAULT, 0, fmt, 64, tune=tune)
+st = np.zeros(8 * 8192, np.uint64)
 for rep in range(6):
     st[:] = 0
     ctx.process_dev(d_umem, umem.nbytes, d_desc, n, d_v, d_res, d_tup)
     torch.cuda.synchronize()
     lib.xdpgpu_stamps_read(st.ctypes.data)
-s4 = st.reshape(-1, 4)
+s4 = st.reshape(-1, 8)
 live = s4[:, 0] > 0
 hw = s4[live, 3]
-s = s4[live, :3].astype(np.int64)
+s = s4[live][:, [0, 1, 2, 4, 5]].astype(np.int64)
 t0 = s[:, 0].min()
 us = (s - t0) / 100.0            # 100 MHz ticks -> us
 waves = np.nonzero(live)[0]
@@ -49,7 +51,9 @@ def pct(a):
     return [round(float(x), 1) for x in np.percentile(a, [0, 10, 50, 90, 100])]
 
 
-out = {"waves": int(live.sum()), "start_us": pct(us[:, 0]), "loop_end_us": pct(us[:, 1]),
+out = {"waves": int(live.sum()), "tail_us": pct(us[:, 2] - us[:, 1]),
+       "tail_exception_us": pct(us[:, 3] - us[:, 1]), "tail_bulk_us": pct(us[:, 4] - us[:, 3]),
+       "tail_payload_us": pct(us[:, 2] - us[:, 4]), "start_us": pct(us[:, 0]), "loop_end_us": pct(us[:, 1]),
        "end_us": pct(us[:, 2]), "loop_us": pct(us[:, 1] - us[:, 0])}
 out["per_xcd_loop_end_median"] = [round(float(np.median(us[xcd == k, 1])), 1) for k in range(8)]
 out["per_xcd_loop_end_max"] = [round(float(us[xcd == k, 1].max()), 1) for k in range(8)]

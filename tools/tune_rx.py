@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EED0002)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--variants", default="ceil,64:0,64:256,64:512,128:0")
+    ap.add_argument("--fmt", type=int, default=xdpgpu.TUPLE_V4)
     args = ap.parse_args()
     n = args.frames
     umem, descs, expect = xdpgpu.pool_generate(n, args.kind, args.size, args.seed)
@@ -35,15 +36,16 @@ def main():
     d_desc = torch.from_numpy(descs.view(np.uint8)).to(dev)
     d_v = torch.empty(n, dtype=torch.uint8, device=dev)
     d_res = torch.empty(n * 16, dtype=torch.uint8, device=dev)
-    d_tup = torch.empty(n * 16, dtype=torch.uint8, device=dev)
-    bpf = 16 + int(descs["len"].mean()) + 16 + 16 + 1
+    tb = xdpgpu.TUPLE_BYTES[args.fmt]
+    d_tup = torch.empty(max(1, n * tb), dtype=torch.uint8, device=dev)
+    bpf = 16 + int(descs["len"].mean()) + 16 + tb + 1
     ctxs = {}
     for v in args.variants.split(","):
         if v == "ceil":
             ctxs[v] = xdpgpu.XdpGpu(0)
         else:
             w, t = (int(x) for x in v.split(":"))
-            ctxs[v] = xdpgpu.XdpGpu(0, xdpgpu.CFG_DEFAULT, 0, xdpgpu.TUPLE_V4, w, tune=t)
+            ctxs[v] = xdpgpu.XdpGpu(0, xdpgpu.CFG_DEFAULT, 0, args.fmt, w, tune=t)
     s = torch.cuda.Stream(dev)
     times = {v: [] for v in ctxs}
     ok = {}
@@ -65,7 +67,7 @@ def main():
         if v == "ceil":
             continue
         w, t = (int(x) for x in v.split(":"))
-        with xdpgpu.XdpGpu(0, xdpgpu.CFG_DEFAULT | xdpgpu.CFG_TIMING, 0, xdpgpu.TUPLE_V4, w,
+        with xdpgpu.XdpGpu(0, xdpgpu.CFG_DEFAULT | xdpgpu.CFG_TIMING, 0, args.fmt, w,
                            tune=t) as tc:
             tc.process_dev(d_umem, umem.nbytes, d_desc, n, d_v, d_res, d_tup, s)
             torch.cuda.synchronize()
