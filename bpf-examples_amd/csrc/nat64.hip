@@ -1027,17 +1027,38 @@ __device__ __forceinline__ void egress_tile(const Nat64Args &a, const Tables &T,
 	obuf[4 * lane + (3 ^ osw)] = make_uint4(n17, F[13], F[14], F[15]);
 }
 
+/* One block per CU (kCuWavesN waves), tiles claimed at run time from an LDS
+ * counter as in the RX kernel (xdp_rx.hip, xdp_rx_db_kernel): with a static
+ * share per wave the SIMD's issue arbitration, which favours its oldest
+ * wave, lets the waves of a CU finish far apart.  Block b's tiles are b,
+ * b + nb, ...; a wave claims the tile two steps ahead of its compute (the
+ * descriptor load and the window DMA run one and two steps ahead).  Slow
+ * frames go to the block's list (an LDS atomic reserves each wave's 64
+ * entries), which xdp_nat64_kernel walks as one region per block. */
+constexpr int kCuWavesN = 16;
+/* the window DMA's cache policy: plain, not non-temporal — the frame's
+ * lines are rewritten in place right after (an in-place rewrite of 64 of
+ * each 128 bytes: 0.83 ms per 16 M frames with plain loads, 1.18 ms with
+ * non-temporal ones, tools/hbm_probe stride) */
+#ifndef XDP_NAT64_WIN_AUX
+#define XDP_NAT64_WIN_AUX 0
+#endif
+constexpr int kWinAux = XDP_NAT64_WIN_AUX;
+constexpr int kCuBlockN = kCuWavesN * kWaveN;
+
 template <bool EG>
-__global__ __launch_bounds__(kBlockN) void xdp_nat64_fast_kernel(Nat64Args a)
+__global__ __launch_bounds__(kCuBlockN, 1) void xdp_nat64_fast_kernel(Nat64Args a)
 {
-	__shared__ uint4 buf_all[kWavesN * 4 * kWaveN];
-	__shared__ uint64_t dtab_all[kWavesN * kWaveN];
-	__shared__ uint32_t xq_all[kWavesN * 2 * kWaveN];
+	__shared__ uint4 buf_all[kCuWavesN * 4 * kWaveN];
+	__shared__ uint64_t dtab_all[kCuWavesN * kWaveN];
+	__shared__ uint32_t xq_all[kCuWavesN * 2 * kWaveN];
 	/* translated first 64 bytes of each frame, stored transposed */
-	__shared__ uint4 obuf_all[kWavesN * 4 * kWaveN];
-	__shared__ uint64_t otab_all[kWavesN * kWaveN];
+	__shared__ uint4 obuf_all[kCuWavesN * 4 * kWaveN];
+	__shared__ uint64_t otab_all[kCuWavesN * kWaveN];
+	/* the block's tile claims and slow-list length */
+	__shared__ uint32_t ctl[2];
 	const int lane = threadIdx.x & (kWaveN - 1);
-	const int wid = threadIdx.x / kWaveN;
+	const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveN);
 	uint4 *buf = buf_all + wid * 4 * kWaveN;
 	uint64_t *dtab = dtab_all + wid * kWaveN;
 	uint32_t *xq = xq_all + wid * 2 * kWaveN;
@@ -1045,13 +1066,25 @@ __global__ __launch_bounds__(kBlockN) void xdp_nat64_fast_kernel(Nat64Args a)
 	uint64_t *otab = otab_all + wid * kWaveN;
 	const Tables T = {a.v6map, a.v6nb, a.v4map, a.v4nb};
 
+	if (threadIdx.x == 0)
+		ctl[0] = ctl[1] = 0;
+	__syncthreads();
+
 	const uint64_t ntiles = ((uint64_t)a.n + kWaveN - 1) / kWaveN;
-	const uint64_t nwaves = (uint64_t)gridDim.x * kWavesN;
-	const uint64_t wgid = (uint64_t)blockIdx.x * kWavesN + wid;
-	uint32_t *xl = a.xlist + wgid * a.xregion;
-	uint32_t xq_n = 0, xout = 0;
+	const uint64_t rb = blockIdx.x, nb = gridDim.x;
+	uint32_t *xl = a.xlist + rb * a.xregion;
+	uint32_t xq_n = 0;
 	const uint64_t us16 = (a.usize + 15) & ~15ull;
 	const bool dma = a.usize >= 64;
+	auto claim = [&](uint32_t cnt) -> uint64_t {
+		return rb + (uint64_t)lds_fetch_add(&ctl[0], cnt, lane) * nb;
+	};
+	/* 64 queued slow frames to the block's list */
+	auto flush = [&](uint32_t cnt) {
+		const uint32_t base = lds_fetch_add(&ctl[1], cnt, lane);
+		if ((uint32_t)lane < cnt)
+			xl[base + lane] = xq[lane];
+	};
 
 	auto ld_desc = [&](uint64_t tt) -> uint4 {
 		uint64_t i = tt * kWaveN + lane;
@@ -1072,19 +1105,21 @@ __global__ __launch_bounds__(kBlockN) void xdp_nat64_fast_kernel(Nat64Args a)
 			const int c = (lane & 3) ^ ((f >> 2) & 3);
 			__builtin_amdgcn_global_load_lds(
 				(const void *)(a.umem + dtab[f] + 16 * c),
-				(lds_void_n *)(buf + kWaveN * k), 16, 0, 2);
+				(lds_void_n *)(buf + kWaveN * k), 16, 0, kWinAux);
 		}
 	};
 
-	uint64_t t = wgid;
+	/* the wave's tiles: qa (in the buffer), qb (its descriptor loaded) */
+	const uint64_t first = claim(2);
+	uint64_t qa = first, qb = first + nb;
 	uint4 dcur = make_uint4(0, 0, 0, 0), dnext = dcur;
-	if (t < ntiles) {
-		dcur = ld_desc(t);
-		dnext = ld_desc(t + nwaves);
+	if (qa < ntiles) {
+		dcur = ld_desc(qa);
+		dnext = ld_desc(qb);
 		issue(dcur, true);
 	}
-	for (; t < ntiles; t += nwaves) {
-		const uint64_t i = t * kWaveN + lane;
+	while (qa < ntiles) {
+		const uint64_t i = qa * kWaveN + lane;
 		const bool active = i < a.n;
 		const uint4 dv = dcur;
 		uint32_t F[16];
@@ -1103,8 +1138,9 @@ __global__ __launch_bounds__(kBlockN) void xdp_nat64_fast_kernel(Nat64Args a)
 		lds_reads_done();
 		__builtin_amdgcn_wave_barrier();
 		dcur = dnext;
-		issue(dcur, t + nwaves < ntiles);
-		dnext = ld_desc(t + 2 * nwaves);
+		issue(dcur, qb < ntiles);
+		const uint64_t qc = claim(1);
+		dnext = ld_desc(qc);
 
 		const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
 		const uint32_t len = dv.z;
@@ -1121,7 +1157,7 @@ __global__ __launch_bounds__(kBlockN) void xdp_nat64_fast_kernel(Nat64Args a)
 			ingress_tile(a, T, F, eff, len, valid, staged, obuf, otab, lane, act,
 				     slow, xlate);
 
-		/* slow frames to this wave's list */
+		/* slow frames to the block's list */
 		{
 			const uint64_t dm = __ballot(active && slow);
 			if (dm) {
@@ -1133,8 +1169,7 @@ __global__ __launch_bounds__(kBlockN) void xdp_nat64_fast_kernel(Nat64Args a)
 				xq_n += (uint32_t)__popcll(dm);
 				if (xq_n >= (uint32_t)kWaveN) {
 					__builtin_amdgcn_wave_barrier();
-					xl[xout + lane] = xq[lane];
-					xout += kWaveN;
+					flush(kWaveN);
 					const uint32_t rest = xq[kWaveN + lane];
 					__builtin_amdgcn_wave_barrier();
 					xq[lane] = rest;
@@ -1170,12 +1205,16 @@ __global__ __launch_bounds__(kBlockN) void xdp_nat64_fast_kernel(Nat64Args a)
 			}
 			*reinterpret_cast<uint4 *>(a.out + i) = od;
 		}
+		qa = qb;
+		qb = qc;
 	}
 	__builtin_amdgcn_wave_barrier();
-	if ((uint32_t)lane < xq_n)
-		xl[xout + lane] = xq[lane];
-	if (lane == 0)
-		a.xcount[wgid] = xout + xq_n;
+	if (xq_n)
+		flush(xq_n);
+	lds_dma_landed();
+	__syncthreads();
+	if (threadIdx.x == 0)
+		a.xcount[rb] = ctl[1];
 }
 
 template <auto KERN>
@@ -1184,13 +1223,14 @@ static uint32_t resident_n()
 	return resident_blocks_dev<KERN, kBlockN>(1024);
 }
 
+/* the fast kernel's grid: one block per CU, fewer for short batches */
 uint32_t nat64_grid(uint32_t n, uint32_t max_blocks)
 {
-	uint32_t cap = resident_n<xdp_nat64_fast_kernel<false>>();
+	uint32_t cap = resident_blocks_dev<xdp_nat64_fast_kernel<false>, kCuBlockN>(1024);
 	if (cap > max_blocks)
 		cap = max_blocks;
 	uint64_t tiles = ((uint64_t)n + kWaveN - 1) / kWaveN;
-	uint64_t blocks = (tiles + kWavesN - 1) / kWavesN;
+	uint64_t blocks = (tiles + kCuWavesN - 1) / kCuWavesN;
 	if (blocks > cap)
 		blocks = cap;
 	return blocks ? (uint32_t)blocks : 1u;
@@ -1201,15 +1241,16 @@ hipError_t launch_nat64(const Nat64Args &a0, uint32_t max_blocks, hipStream_t st
 	Nat64Args a = a0;
 	if (a.fast) {
 		const uint32_t blocks = nat64_grid(a.n, max_blocks);
-		a.nregions = blocks * kWavesN;
+		/* one slow-list region per block: its share of the tiles */
+		a.nregions = blocks;
 		const uint64_t tiles = ((uint64_t)a.n + kWaveN - 1) / kWaveN;
 		a.xregion = (uint32_t)(((tiles + a.nregions - 1) / a.nregions) * kWaveN);
 		if (a.cfg.direction == XDPGPU_NAT64_EGRESS)
 			hipLaunchKernelGGL(xdp_nat64_fast_kernel<true>, dim3(blocks),
-					   dim3(kBlockN), 0, stream, a);
+					   dim3(kCuBlockN), 0, stream, a);
 		else
 			hipLaunchKernelGGL(xdp_nat64_fast_kernel<false>, dim3(blocks),
-					   dim3(kBlockN), 0, stream, a);
+					   dim3(kCuBlockN), 0, stream, a);
 		hipError_t e = hipGetLastError();
 		if (e != hipSuccess)
 			return e;

@@ -1447,25 +1447,6 @@ __device__ __forceinline__ void store_tile(const RxArgs &a, const TileOut &o)
 					      rt, net && out ? b + 32 : kOff, 0, 0);
 }
 
-/* Lane 0's fetch-and-add of v on an LDS counter, returned to every lane.
- * In asm, waiting for its own result: a compiler-visible LDS atomic gets a
- * vmcnt(0) in front of it while LDS-DMA is pending (the compiler cannot
- * tell the counter from the DMA's destination). */
-__device__ __forceinline__ uint32_t lds_fetch_add(uint32_t *ctr, uint32_t v, int lane)
-{
-	uint32_t r = 0;
-	if (lane == 0) {
-		const uint32_t addr =
-			(uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t *)ctr;
-		asm volatile("ds_add_rtn_u32 %0, %1, %2\n\t"
-			     "s_waitcnt lgkmcnt(0)"
-			     : "=v"(r)
-			     : "v"(addr), "v"(v)
-			     : "memory");
-	}
-	return (uint32_t)__builtin_amdgcn_readfirstlane(r);
-}
-
 /* Append to the block's list without an LDS queue: the wave reserves its
  * entries with one LDS atomic on the list's length, and each deferred lane
  * stores its index at its rank (a partial line per store; deferrals are
@@ -2615,6 +2596,70 @@ hipError_t launch_jhash(const uint8_t *keys, uint32_t key_len,
 		return hipSuccess;
 	hipLaunchKernelGGL(jhash_kernel, dim3(blocks), dim3(kBlock), 0, stream,
 			   keys, key_len, stride, n, initval, out);
+	return hipGetLastError();
+}
+
+/* jhash2 (include/jhash.h:114-142) over n keys of nwords u32 at stride
+ * words (variant 0), or jhash_1word / 2words / 3words (jhash.h:145-170:
+ * __jhash_nwords with initval + JHASH_INITVAL + 4 nwords; variant =
+ * nwords, words past nwords zero). */
+__global__ __launch_bounds__(kBlock) void jhash_words_kernel(const uint32_t *words,
+							     uint32_t nwords,
+							     uint32_t stride, uint32_t n,
+							     uint32_t initval,
+							     uint32_t variant,
+							     uint32_t *out)
+{
+	const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+	if (i >= n)
+		return;
+	const uint32_t *k = words + i * stride;
+	uint32_t a, b, c;
+	if (variant) {
+		const uint32_t iv = initval + 0xdeadbeefu + (variant << 2);
+		a = k[0] + iv;
+		b = (variant > 1 ? k[1] : 0u) + iv;
+		c = (variant > 2 ? k[2] : 0u) + iv;
+		JH_FINAL(a, b, c);
+		out[i] = c;
+		return;
+	}
+	uint32_t len = nwords;
+	a = b = c = 0xdeadbeefu + (len << 2) + initval;
+	while (len > 3) {
+		a += k[0];
+		b += k[1];
+		c += k[2];
+		JH_MIX(a, b, c);
+		len -= 3;
+		k += 3;
+	}
+	switch (len) {
+	case 3:
+		c += k[2];
+		[[fallthrough]];
+	case 2:
+		b += k[1];
+		[[fallthrough]];
+	case 1:
+		a += k[0];
+		JH_FINAL(a, b, c);
+		break;
+	default:
+		break;
+	}
+	out[i] = c;
+}
+
+hipError_t launch_jhash_words(const uint32_t *words, uint32_t nwords, uint32_t stride,
+			      uint32_t n, uint32_t initval, uint32_t variant,
+			      uint32_t *out, hipStream_t stream)
+{
+	const uint32_t blocks = (n + kBlock - 1) / kBlock;
+	if (!blocks)
+		return hipSuccess;
+	hipLaunchKernelGGL(jhash_words_kernel, dim3(blocks), dim3(kBlock), 0, stream,
+			   words, nwords, stride, n, initval, variant, out);
 	return hipGetLastError();
 }
 

@@ -19,6 +19,8 @@
 #include <vector>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
 #include <new>
 
 #include "xdpgpu.h"
@@ -185,10 +187,59 @@ static void free_slot(Slot &s)
 	s = Slot();
 }
 
+/* Per-queue counters: the live contexts, and the counters of finished ones
+ * by queue (xdpgpu_queue_stats). */
+static std::mutex g_qmu;
+static std::vector<xdpgpu_ctx *> g_live;
+static std::map<uint32_t, struct xdpgpu_stats> g_retired;
+
+static void add_stats(struct xdpgpu_stats &to, const struct xdpgpu_stats &s)
+{
+	to.frames += s.frames;
+	to.bytes += s.bytes;
+	for (int v = 0; v < XDPGPU_NUM_VERDICTS; v++)
+		to.verdict[v] += s.verdict[v];
+	to.l3_bad += s.l3_bad;
+	to.l4_bad += s.l4_bad;
+	to.l4_absent += s.l4_absent;
+	to.frag += s.frag;
+}
+
+int xdpgpu_queue_stats(uint32_t queue_id, struct xdpgpu_stats *out)
+{
+	if (!out)
+		return -EINVAL;
+	memset(out, 0, sizeof(*out));
+	std::lock_guard<std::mutex> lk(g_qmu);
+	auto it = g_retired.find(queue_id);
+	if (it != g_retired.end())
+		add_stats(*out, it->second);
+	for (xdpgpu_ctx *c : g_live) {
+		if (c->cfg.queue_id != queue_id)
+			continue;
+		struct xdpgpu_stats s;
+		const int rc = xdpgpu_stats(c, &s);
+		if (rc)
+			return rc;
+		add_stats(*out, s);
+	}
+	return 0;
+}
+
 void xdpgpu_fini(xdpgpu_ctx *ctx)
 {
 	if (!ctx)
 		return;
+	{
+		std::lock_guard<std::mutex> lk(g_qmu);
+		auto it = std::find(g_live.begin(), g_live.end(), ctx);
+		if (it != g_live.end()) {
+			g_live.erase(it);
+			struct xdpgpu_stats s;
+			if (xdpgpu_stats(ctx, &s) == 0)
+				add_stats(g_retired[ctx->cfg.queue_id], s);
+		}
+	}
 	(void)hipSetDevice(ctx->cfg.device);
 	(void)hipDeviceSynchronize();
 	for (uint32_t i = 0; i < kSlots; i++)
@@ -270,6 +321,10 @@ int xdpgpu_init(const xdpgpu_cfg *cfg, xdpgpu_ctx **out)
 	if (rc) {
 		xdpgpu_fini(ctx);
 		return rc;
+	}
+	{
+		std::lock_guard<std::mutex> lk(g_qmu);
+		g_live.push_back(ctx);
 	}
 	*out = ctx;
 	return 0;
@@ -1038,6 +1093,31 @@ int xdpgpu_jhash_dev(xdpgpu_ctx *ctx, const void *d_keys, uint32_t key_len,
 	hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
 	HIP_TRY(ctx, launch_jhash((const uint8_t *)d_keys, key_len, key_stride,
 				  n, initval, d_out, st));
+	return 0;
+}
+
+int xdpgpu_jhash2_dev(xdpgpu_ctx *ctx, const uint32_t *d_words, uint32_t nwords,
+		      uint32_t word_stride, uint32_t n, uint32_t initval,
+		      uint32_t *d_out, void *stream)
+{
+	if (!ctx || (!d_words && n && nwords) || (!d_out && n) || word_stride < nwords)
+		return -EINVAL;
+	hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
+	HIP_TRY(ctx, launch_jhash_words(d_words, nwords, word_stride, n, initval, 0, d_out,
+					st));
+	return 0;
+}
+
+int xdpgpu_jhash_nwords_dev(xdpgpu_ctx *ctx, const uint32_t *d_words, uint32_t nwords,
+			    uint32_t word_stride, uint32_t n, uint32_t initval,
+			    uint32_t *d_out, void *stream)
+{
+	if (!ctx || nwords < 1 || nwords > 3 || (!d_words && n) || (!d_out && n) ||
+	    word_stride < nwords)
+		return -EINVAL;
+	hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
+	HIP_TRY(ctx, launch_jhash_words(d_words, nwords, word_stride, n, initval, nwords,
+					d_out, st));
 	return 0;
 }
 

@@ -67,6 +67,26 @@ __device__ __forceinline__ void lds_reads_done()
 	asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
+/* Lane 0's fetch-and-add of v on an LDS counter, returned to every lane.
+ * In asm, waiting for its own result: a compiler-visible LDS atomic gets a
+ * vmcnt(0) in front of it while LDS-DMA is pending (the compiler cannot
+ * tell the counter from the DMA's destination). */
+__device__ __forceinline__ uint32_t lds_fetch_add(uint32_t *ctr, uint32_t v, int lane)
+{
+	uint32_t r = 0;
+	if (lane == 0) {
+		const uint32_t addr =
+			(uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t *)ctr;
+		asm volatile("ds_add_rtn_u32 %0, %1, %2\n\t"
+			     "s_waitcnt lgkmcnt(0)"
+			     : "=v"(r)
+			     : "v"(addr), "v"(v)
+			     : "memory");
+	}
+	return (uint32_t)__builtin_amdgcn_readfirstlane(r);
+}
+
+
 /* Per-block counter slot layout (u64 each); slots summed by xdpgpu_stats. */
 enum {
 	CNT_FRAMES = 0,
@@ -125,6 +145,9 @@ struct RxArgs {
  * each of the fast, exception and bulk kernels (launch order) */
 hipError_t launch_rx(const RxArgs &a, uint32_t window, uint32_t max_blocks,
 		     hipStream_t stream, uint32_t tune, hipEvent_t *ev);
+hipError_t launch_jhash_words(const uint32_t *words, uint32_t nwords, uint32_t stride,
+			      uint32_t n, uint32_t initval, uint32_t variant,
+			      uint32_t *out, hipStream_t stream);
 uint32_t rx_grid_blocks(uint32_t n, uint32_t max_blocks);
 uint32_t rx_xregion(uint32_t n, uint32_t blocks);
 hipError_t launch_ceiling(const RxArgs &a, uint32_t blocks, hipStream_t stream);

@@ -85,7 +85,7 @@ class Cfg(C.Structure):
     _fields_ = [("device", C.c_int32), ("flags", C.c_uint32),
                 ("max_batch", C.c_uint32), ("jhash_initval", C.c_uint32),
                 ("tuple_fmt", C.c_uint32), ("window", C.c_uint32),
-                ("tune", C.c_uint32), ("rsvd", C.c_uint32)]
+                ("tune", C.c_uint32), ("queue_id", C.c_uint32)]
 
 
 class Stats(C.Structure):
@@ -145,7 +145,8 @@ EXPORTS = (
     "xdpgpu_device_count", "xdpgpu_last_error",
     "xdpgpu_abi_version", "xdpgpu_pool_size", "xdpgpu_pool_generate",
     "xdpgpu_pool_spec_default", "xdpgpu_hints_dev", "xdpgpu_host_alloc",
-    "xdpgpu_host_free",
+    "xdpgpu_host_free", "xdpgpu_jhash2_dev", "xdpgpu_jhash_nwords_dev",
+    "xdpgpu_queue_stats",
 )
 
 # struct xdpgpu_hints (XDP hints in front of a frame)
@@ -171,8 +172,11 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.xdpgpu_wait.argtypes = [vp, u32]
     lib.xdpgpu_process_dev.argtypes = [vp, vp, u64, vp, u32, vp, vp, vp, vp]
     lib.xdpgpu_stats.argtypes = [vp, C.POINTER(Stats)]
+    lib.xdpgpu_queue_stats.argtypes = [u32, C.POINTER(Stats)]
     lib.xdpgpu_stats_reset.argtypes = [vp]
     lib.xdpgpu_jhash_dev.argtypes = [vp, vp, u32, u32, u32, u32, vp, vp]
+    lib.xdpgpu_jhash2_dev.argtypes = [vp, vp, u32, u32, u32, u32, vp, vp]
+    lib.xdpgpu_jhash_nwords_dev.argtypes = [vp, vp, u32, u32, u32, u32, vp, vp]
     lib.xdpgpu_ip_fast_csum_dev.argtypes = [vp, vp, u32, u32, vp, vp]
     lib.xdpgpu_hints_dev.argtypes = [vp, vp, u64, vp, u32, u32, u32, vp, vp]
     lib.xdpgpu_sync.argtypes = [vp, vp]
@@ -246,6 +250,17 @@ class HostBuffer:
             pass
 
 
+def queue_stats(queue_id: int) -> dict:
+    """Counters of RX queue queue_id: every context of this process made
+    with that queue_id, live or closed (xdpgpu_queue_stats)."""
+    lib = load_library()
+    s = Stats()
+    rc = lib.xdpgpu_queue_stats(queue_id, C.byref(s))
+    if rc:
+        raise XdpGpuError(f"xdpgpu_queue_stats: {os.strerror(-rc)} ({rc})")
+    return s.as_dict()
+
+
 def device_count() -> int:
     return load_library().xdpgpu_device_count()
 
@@ -255,11 +270,12 @@ class XdpGpu:
 
     def __init__(self, device: int = 0, flags: int = CFG_DEFAULT,
                  initval: int = 0, tuple_fmt: int = TUPLE_V4,
-                 window: int = 64, max_batch: int = 0, tune: int = 0):
+                 window: int = 64, max_batch: int = 0, tune: int = 0,
+                 queue_id: int = 0):
         self.lib = load_library()
         cfg = Cfg(device=device, flags=flags, max_batch=max_batch,
                   jhash_initval=initval & 0xffffffff, tuple_fmt=tuple_fmt,
-                  window=window, tune=tune)
+                  window=window, tune=tune, queue_id=queue_id)
         h = C.c_void_p()
         rc = self.lib.xdpgpu_init(C.byref(cfg), C.byref(h))
         if rc:
@@ -361,6 +377,20 @@ class XdpGpu:
         self._check(self.lib.xdpgpu_jhash_dev(
             self.h, _ptr(keys), key_len, key_stride, n, initval & 0xffffffff,
             _ptr(out), _stream_handle(stream)), "xdpgpu_jhash_dev")
+
+    def jhash2_dev(self, words, nwords: int, word_stride: int, n: int,
+                   initval: int, out, stream=None) -> None:
+        """jhash2 (include/jhash.h:114) over n keys of nwords u32."""
+        self._check(self.lib.xdpgpu_jhash2_dev(
+            self.h, _ptr(words), nwords, word_stride, n, initval & 0xffffffff,
+            _ptr(out), _stream_handle(stream)), "xdpgpu_jhash2_dev")
+
+    def jhash_nwords_dev(self, words, nwords: int, word_stride: int, n: int,
+                         initval: int, out, stream=None) -> None:
+        """jhash_1word / 2words / 3words (include/jhash.h:157-170)."""
+        self._check(self.lib.xdpgpu_jhash_nwords_dev(
+            self.h, _ptr(words), nwords, word_stride, n, initval & 0xffffffff,
+            _ptr(out), _stream_handle(stream)), "xdpgpu_jhash_nwords_dev")
 
     def ip_fast_csum_dev(self, hdrs, stride: int, n: int, out,
                          stream=None) -> None:

@@ -143,7 +143,10 @@ struct xdpgpu_cfg {
 				 * host path without the mapped UMEM (span
 				 * copies, compact echo records);
 				 * 0 = default */
-	uint32_t rsvd;
+	uint32_t queue_id;      /* the RX queue this context serves (the XDP
+				 * program's ctx->rx_queue_index): its
+				 * counters add into that queue's
+				 * (xdpgpu_queue_stats)                      */
 };
 
 /* UMEM registration flags (headers/linux/if_xdp.h:31) */
@@ -225,12 +228,30 @@ int xdpgpu_process_dev(struct xdpgpu_ctx *ctx, void *d_umem,
 int xdpgpu_stats(struct xdpgpu_ctx *ctx, struct xdpgpu_stats *out);
 int xdpgpu_stats_reset(struct xdpgpu_ctx *ctx);
 
+/* Per-queue counters (AF_XDP-interaction/af_xdp_kern.c:19-24 xdp_stats_map,
+ * indexed by rx_queue_index, :157-160): the sum of the counters of every
+ * context of this process with cfg.queue_id == queue_id, live or finished
+ * (a finished context's counters are kept).  frames is the map's packet
+ * count; the other fields split it as xdpgpu_stats does. */
+int xdpgpu_queue_stats(uint32_t queue_id, struct xdpgpu_stats *out);
+
 /* Device primitives, one lane per item (device pointers, stream as above).
  * jhash over n keys of key_len bytes at key_stride   (include/jhash.h:68-105)
  * ip_fast_csum over n IPv4 headers at hdr_stride      (lib_checksum.h:103-106) */
 int xdpgpu_jhash_dev(struct xdpgpu_ctx *ctx, const void *d_keys,
 		     uint32_t key_len, uint32_t key_stride, uint32_t n,
 		     uint32_t initval, uint32_t *d_out, void *stream);
+/* jhash2 over n keys of nwords u32 at word_stride words
+ *   (include/jhash.h:114-142: jhash2(k, length, initval));
+ * jhash_1word / jhash_2words / jhash_3words for nwords = 1..3 over n items
+ *   of nwords u32 at word_stride words (jhash.h:157-170; the flow-key
+ *   hash of the IPv4 fast variant, jhash_3words(saddr, daddr, ports, iv)). */
+int xdpgpu_jhash2_dev(struct xdpgpu_ctx *ctx, const uint32_t *d_words,
+		      uint32_t nwords, uint32_t word_stride, uint32_t n,
+		      uint32_t initval, uint32_t *d_out, void *stream);
+int xdpgpu_jhash_nwords_dev(struct xdpgpu_ctx *ctx, const uint32_t *d_words,
+			    uint32_t nwords, uint32_t word_stride, uint32_t n,
+			    uint32_t initval, uint32_t *d_out, void *stream);
 int xdpgpu_ip_fast_csum_dev(struct xdpgpu_ctx *ctx, const void *d_hdrs,
 			    uint32_t hdr_stride, uint32_t n, uint16_t *d_out,
 			    void *stream);

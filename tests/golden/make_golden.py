@@ -442,9 +442,13 @@ def random_vectors():
     w3 = rng.integers(0, 2 ** 32, (500, 3), dtype=np.uint64).astype(np.uint32)
     j3 = np.array([r.ref_jhash_3words(int(a), int(b), int(c), int(v))
                    for (a, b, c), v in zip(w3, iv[:500])], np.uint32)
+    j2 = np.array([r.ref_jhash_2words(int(a), int(b), int(v))
+                   for (a, b, _), v in zip(w3, iv[:500])], np.uint32)
+    j1 = np.array([r.ref_jhash_1word(int(a), int(v))
+                   for (a, _, _), v in zip(w3, iv[:500])], np.uint32)
     np.savez_compressed(os.path.join(HERE, "jhash_vectors.npz"), klen=klen, keys=keys,
                         initval=iv, jhash=jh, wlen=wl, jhash2=jh2, words3=w3,
-                        jhash_3words=j3)
+                        jhash_3words=j3, jhash_2words=j2, jhash_1word=j1)
 
 
 def main():

@@ -275,6 +275,40 @@ def test_jhash_primitive_vectors(dev):
     ctx.close()
 
 
+def test_jhash_word_primitive_vectors(dev):
+    """jhash2 over 0..16 words with per-key initvals, and jhash_1word /
+    2words / 3words: reference-generated vectors (make_golden.py)."""
+    import os
+    vec = np.load(os.path.join(os.path.dirname(__file__), "golden", "jhash_vectors.npz"))
+    keys = np.ascontiguousarray(vec["keys"][:500]).view(np.uint32)      # 16 words each
+    wl, iv = vec["wlen"], vec["initval"][:500]
+    ctx = xdpgpu.XdpGpu(0)
+    d_keys = to_dev(keys)
+    out = torch.zeros(500, dtype=torch.int32, device="cuda:0")
+    for k in range(500):
+        ctx.jhash2_dev(d_keys.data_ptr() + 64 * k, int(wl[k]), 16, 1, int(iv[k]),
+                       out.data_ptr() + 4 * k)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), vec["jhash2"])
+    # one launch of 500 keys of one length: stride and batch indexing
+    for L in (0, 1, 11, 16):
+        ctx.jhash2_dev(d_keys, L, 16, 500, 0x9E3779B9, out)
+        torch.cuda.synchronize()
+        want = [oracle.lib().oracle_jhash2(keys[k].tobytes(), L, 0x9E3779B9)
+                for k in range(500)]
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32),
+                                      np.array(want, np.uint32))
+    w3 = np.ascontiguousarray(vec["words3"])
+    d_w3 = to_dev(w3)
+    for nw, key in ((3, "jhash_3words"), (2, "jhash_2words"), (1, "jhash_1word")):
+        for k in range(500):
+            ctx.jhash_nwords_dev(d_w3.data_ptr() + 12 * k, nw, 3, 1, int(iv[k]),
+                                 out.data_ptr() + 4 * k)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), vec[key], err_msg=key)
+    ctx.close()
+
+
 def test_ip_fast_csum_primitive_vectors(dev):
     import os
     vec = np.load(os.path.join(os.path.dirname(__file__), "golden", "csum_vectors.npz"))

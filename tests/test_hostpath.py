@@ -217,3 +217,36 @@ def test_process_dev_two_streams():
             np.testing.assert_array_equal(dv.cpu().numpy(), wv)
             np.testing.assert_array_equal(dr.cpu().numpy(), wres.view(np.uint8).reshape(-1))
             np.testing.assert_array_equal(dt.cpu().numpy(), wtup)
+
+
+def test_queue_stats():
+    """Per-queue counters (af_xdp_kern.c:19-24, :157-160): contexts of one
+    RX queue add up, a closed context's counters are kept, other queues
+    are apart."""
+    from test_gpu_parity import to_dev
+    qa, qb = 1000 + np.random.randint(1 << 20), 2000 + np.random.randint(1 << 20)
+    pools = [xdpgpu.pool_generate(n, xdpgpu.POOL_IMIX, 64, s) for n, s in ((30000, 51),
+                                                                           (20000, 52))]
+    want = [oracle.process(u.copy(), d, 0x5, 0, 1)[3] for u, d, _ in pools]
+    ctxs = [xdpgpu.XdpGpu(0, 0x5, 0, 1, queue_id=q) for q in (qa, qa, qb)]
+    keep = []      # the device buffers live until the launches are done
+    for c, (u, d, _) in zip(ctxs, (pools[0], pools[1], pools[0])):
+        n = len(d)
+        bufs = (to_dev(u), to_dev(d, 16), torch.empty(n, dtype=torch.uint8, device="cuda:0"),
+                torch.empty(n * 16, dtype=torch.uint8, device="cuda:0"),
+                torch.empty(n * 16, dtype=torch.uint8, device="cuda:0"))
+        keep.append(bufs)
+        c.process_dev(bufs[0], u.nbytes, bufs[1], n, *bufs[2:])
+    torch.cuda.synchronize()
+    a = xdpgpu.queue_stats(qa)
+    assert a["frames"] == want[0]["frames"] + want[1]["frames"]
+    assert [a["verdict"][x] for x in xdpgpu.VERDICT_NAMES] == \
+        [p + q for p, q in zip(want[0]["verdict"], want[1]["verdict"])]
+    b = xdpgpu.queue_stats(qb)
+    assert b["frames"] == want[0]["frames"] and b["bytes"] == want[0]["bytes"]
+    ctxs[1].close()
+    assert xdpgpu.queue_stats(qa)["frames"] == a["frames"]      # kept after close
+    for c in ctxs:
+        c.close()
+    assert xdpgpu.queue_stats(qa) == a
+    assert xdpgpu.queue_stats(qb) == b

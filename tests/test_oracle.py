@@ -41,6 +41,11 @@ def test_jhash_vectors(o):
     for k in range(len(v["words3"])):
         a, b, c = (int(x) for x in v["words3"][k])
         assert o.oracle_jhash_3words(a, b, c, int(v["initval"][k])) == v["jhash_3words"][k]
+        # jhash_2words(a, b, iv) = jhash_3words(a, b, 0, iv - 4), jhash_1word
+        # likewise (jhash.h:157-170: initval + JHASH_INITVAL + 4 nwords)
+        iv = int(v["initval"][k])
+        assert o.oracle_jhash_3words(a, b, 0, (iv - 4) & 0xffffffff) == v["jhash_2words"][k]
+        assert o.oracle_jhash_3words(a, 0, 0, (iv - 8) & 0xffffffff) == v["jhash_1word"][k]
 
 
 def test_csum_vectors(o):

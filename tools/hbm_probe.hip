@@ -397,10 +397,79 @@ static int bulk_main()
 	return 0;
 }
 
+/* "stride": the first CH chunks of 16 B of each 128-B frame, read (R),
+ * written (W) or both in place, as the nat64 header rewrite touches them */
+template <int CH, bool R, bool W, bool NT>
+__global__ __launch_bounds__(256) void k_stride(uint4 *p, size_t nframes, uint32_t *out)
+{
+	uint32_t x = 0;
+	const size_t n = nframes * CH;
+	for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+		uint4 *q = p + (i / CH) * 8 + (i % CH);
+		uint4 v = make_uint4((uint32_t)i, 1, 2, 3);
+		if (R)
+			v = NT ? ntl(q) : *q;
+		if (W) {
+			v.x += 1;
+			if (NT)
+				nts(v, q);
+			else
+				*q = v;
+		} else {
+			x ^= v.x ^ v.y ^ v.z ^ v.w;
+		}
+	}
+	if (x == 0x12345678u)
+		out[0] = x;
+}
+
+static int stride_main()
+{
+	const size_t frames = 16ull << 20;
+	uint4 *p;
+	uint32_t *o;
+	CK(hipMalloc(&p, frames * 128));
+	CK(hipMalloc(&o, 64));
+	CK(hipMemset(p, 1, frames * 128));
+	hipEvent_t e0, e1;
+	CK(hipEventCreate(&e0));
+	CK(hipEventCreate(&e1));
+	struct V { const char *name; void (*k)(uint4 *, size_t, uint32_t *); double bytes; };
+	const V vs[] = {
+		{"read64   ", k_stride<4, true, false, false>, 64.0},
+		{"write64  ", k_stride<4, false, true, false>, 64.0},
+		{"write64nt", k_stride<4, false, true, true>, 64.0},
+		{"rw64     ", k_stride<4, true, true, false>, 128.0},
+		{"rw64nt   ", k_stride<4, true, true, true>, 128.0},
+		{"read128  ", k_stride<8, true, false, false>, 128.0},
+		{"write128 ", k_stride<8, false, true, false>, 128.0},
+		{"rw128    ", k_stride<8, true, true, false>, 256.0},
+	};
+	for (int rep = 0; rep < 2; rep++)
+		for (const V &v : vs)
+			for (int grid : {2048, 8192}) {
+				for (int w = 0; w < 2; w++)
+					hipLaunchKernelGGL(v.k, dim3(grid), dim3(256), 0, 0, p, frames, o);
+				CK(hipEventRecord(e0, 0));
+				for (int r = 0; r < 10; r++)
+					hipLaunchKernelGGL(v.k, dim3(grid), dim3(256), 0, 0, p, frames, o);
+				CK(hipEventRecord(e1, 0));
+				CK(hipEventSynchronize(e1));
+				float ms;
+				CK(hipEventElapsedTime(&ms, e0, e1));
+				ms /= 10;
+				printf("stride %s grid %5d  %.4f ms  %7.1f GB/s of bytes touched\n", v.name,
+				       grid, ms, frames * v.bytes / ms / 1e6);
+			}
+	return 0;
+}
+
 int main(int argc, char **argv)
 {
 	if (argc > 1 && !strcmp(argv[1], "bulk"))
 		return bulk_main();
+	if (argc > 1 && !strcmp(argv[1], "stride"))
+		return stride_main();
 	const bool pair_only = argc > 1 && !strcmp(argv[1], "pair");
 	const size_t frames = 16ull << 20;
 	C.frames = frames;
