@@ -16,6 +16,11 @@
 #include <time.h>
 
 #include "rxapp.h"
+#include "xsk.h"
+
+#include <pthread.h>
+#include <unistd.h>
+#include <linux/if_link.h>
 
 static volatile sig_atomic_t rx_done;
 
@@ -416,6 +421,24 @@ int rx_run(const struct rx_source *src, const struct rx_opts *o,
 	memset(slot, 0, sizeof(slot));
 	if (!o->batch || !src->n)
 		return -EINVAL;
+	if (o->frags) {
+		/* a batch ends on a packet's last fragment: every packet must
+		 * fit one batch */
+		uint32_t run = 0, most = 0;
+		for (uint32_t i = 0; i < src->n; i++) {
+			run++;
+			if (!(src->descs[i].options & XDPGPU_PKT_CONTD)) {
+				most = run > most ? run : most;
+				run = 0;
+			}
+		}
+		most = run > most ? run : most;
+		if (most > o->batch) {
+			fprintf(stderr, "%s: a packet of %u fragments does not fit a batch of %u "
+				"(-b)\n", o->prog, most, o->batch);
+			return -EINVAL;
+		}
+	}
 	rc = xdpgpu_init(&cfg, &ctx);
 	if (rc) {
 		fprintf(stderr, "%s: xdpgpu_init: %s%s\n", o->prog, strerror(-rc),
@@ -430,9 +453,10 @@ int rx_run(const struct rx_source *src, const struct rx_opts *o,
 		xdpgpu_fini(ctx);
 		return rc;
 	}
+	/* page-locked batch arrays: xdpgpu_submit copies them unstaged */
 	for (int k = 0; k < 2; k++) {
-		slot[k].d = malloc((size_t)o->batch * sizeof(*slot[k].d));
-		slot[k].v = malloc(o->batch);
+		slot[k].d = xdpgpu_host_alloc((uint64_t)o->batch * sizeof(*slot[k].d));
+		slot[k].v = xdpgpu_host_alloc(o->batch);
 		if (!slot[k].d || !slot[k].v)
 			rc = -ENOMEM;
 	}
@@ -544,10 +568,308 @@ int rx_run(const struct rx_source *src, const struct rx_opts *o,
 		fflush(stdout);
 	}
 	for (int j = 0; j < 2; j++) {
-		free(slot[j].d);
-		free(slot[j].v);
+		xdpgpu_host_free(slot[j].d);
+		xdpgpu_host_free(slot[j].v);
 	}
 	free(first_pass);
 	xdpgpu_fini(ctx);
+	return rc;
+}
+
+/* ------------------------------------------------------------------ */
+/* live mode                                                            */
+
+struct injector {
+	const struct rx_live *lv;
+	const char *ifname;
+	volatile uint64_t received;  /* frames the RX loop has taken */
+	volatile uint64_t sent;
+	volatile int stop;
+	int rc;
+};
+
+/* Sends the source's frames into the peer, cycling it, keeping at most
+ * ring_size / 2 frames ahead of the receiver (no RX-ring overflow: every
+ * frame sent is received, so verdicts line up with the source). */
+static void *inject_main(void *arg)
+{
+	struct injector *in = arg;
+	const struct rx_source *src = in->lv->inject;
+	const uint64_t window = in->lv->ring_size / 2;
+	uint64_t k = 0;
+
+	while (!in->stop && k < in->lv->inject_count) {
+		uint64_t m = in->lv->inject_count - k;
+		const uint64_t room = window - (k - in->received);
+		if (k - in->received >= window) {
+			usleep(20);
+			continue;
+		}
+		m = m < room ? m : room;
+		m = m < 256 ? m : 256;
+		const uint32_t at = (uint32_t)(k % src->n);
+		if (m > src->n - at)
+			m = src->n - at;
+		const int r = xsk_inject(in->ifname, src->umem,
+					 (const struct xdp_desc *)(src->descs + at), (uint32_t)m);
+		if (r < 0) {
+			in->rc = r;
+			break;
+		}
+		k += (uint64_t)r;
+		in->sent = k;
+	}
+	return NULL;
+}
+
+int rx_run_live(const struct rx_live *lv, const struct rx_opts *o, struct rx_totals *out)
+{
+	struct xdpgpu_cfg cfg = {
+		.device = o->device,
+		.flags = o->cfg_flags,
+		.max_batch = o->batch,
+		.jhash_initval = o->initval,
+		.tuple_fmt = o->tuple_fmt,
+		.window = 64,
+		.queue_id = lv->queue,
+	};
+	struct xdpgpu_ctx *ctx = NULL;
+	struct rx_slot slot[2];
+	struct xsk_sock x;
+	struct injector in;
+	pthread_t th;
+	bool th_up = false, veth = false;
+	uint8_t *verdicts = NULL;
+	uint64_t *fill = NULL;
+	struct xdp_desc *txd = NULL;
+	int rc;
+
+	memset(out, 0, sizeof(*out));
+	memset(slot, 0, sizeof(slot));
+	memset(&in, 0, sizeof(in));
+	memset(&x, 0, sizeof(x));
+	x.fd = x.map_fd = x.prog_fd = x.link_fd = -1;
+	if (!o->batch || o->batch > lv->ring_size || lv->nframes < 2 * lv->ring_size)
+		return -EINVAL;
+	if (lv->veth_peer) {
+		(void)xsk_link_delete(lv->ifname);
+		rc = xsk_veth_create(lv->ifname, lv->veth_peer);
+		if (rc) {
+			fprintf(stderr, "%s: veth %s <-> %s: %s\n", o->prog, lv->ifname,
+				lv->veth_peer, strerror(-rc));
+			return rc == -EPERM || rc == -EACCES ? 1 : rc;
+		}
+		veth = true;
+	}
+	const struct xsk_cfg xc = {
+		.ifname = lv->ifname, .queue = lv->queue, .nframes = lv->nframes,
+		.frame_size = lv->frame_size, .headroom = 0, .ring_size = lv->ring_size,
+		.bind_flags = lv->bind_flags, .xdp_flags = lv->xdp_flags, .attach_prog = true,
+	};
+	rc = xsk_open(&x, &xc);
+	if (rc) {
+		fprintf(stderr, "%s: AF_XDP on %s:%u: %s\n", o->prog, lv->ifname, lv->queue, x.err);
+		rc = (rc == -EPERM || rc == -EACCES || rc == -EAFNOSUPPORT) ? 1 : rc;
+		goto out;
+	}
+	rc = xdpgpu_init(&cfg, &ctx);
+	if (rc) {
+		fprintf(stderr, "%s: xdpgpu_init: %s%s\n", o->prog, strerror(-rc),
+			rc == -ENODEV ? " (no GPU: this build has no CPU fallback)" : "");
+		goto out;
+	}
+	rc = xdpgpu_register_umem(ctx, x.umem, x.umem_size, lv->frame_size, 0, 0);
+	if (rc) {
+		fprintf(stderr, "%s: xdpgpu_register_umem: %s %s\n", o->prog, strerror(-rc),
+			xdpgpu_last_error(ctx));
+		goto out;
+	}
+	for (int k = 0; k < 2; k++) {
+		slot[k].d = xdpgpu_host_alloc((uint64_t)o->batch * sizeof(*slot[k].d));
+		slot[k].v = xdpgpu_host_alloc(o->batch);
+		if (!slot[k].d || !slot[k].v)
+			rc = -ENOMEM;
+	}
+	fill = malloc((size_t)lv->nframes * sizeof(*fill));
+	txd = malloc((size_t)o->batch * sizeof(*txd));
+	if (o->verdict_out && o->count)
+		verdicts = calloc(o->count, 1);
+	if (rc || !fill || !txd || (o->verdict_out && o->count && !verdicts)) {
+		rc = -ENOMEM;
+		goto out;
+	}
+	/* the fill ring takes the first ring_size frames, the rest wait in a
+	 * free list (xsk_populate_fill_ring, xdpsock.c:1081-1098) */
+	uint32_t nfree = 0;
+	for (uint32_t i = 0; i < lv->nframes; i++)
+		fill[nfree++] = (uint64_t)i * lv->frame_size;
+	nfree -= lv->ring_size;
+	rc = xsk_fill(&x, fill + nfree, lv->ring_size);
+	if (rc)
+		goto out;
+
+	if (lv->inject) {
+		in.lv = lv;
+		in.ifname = lv->veth_peer ? lv->veth_peer : lv->ifname;
+		if (pthread_create(&th, NULL, inject_main, &in)) {
+			rc = -errno;
+			goto out;
+		}
+		th_up = true;
+	}
+
+	rx_done = 0;
+	signal(SIGINT, on_signal);
+	signal(SIGTERM, on_signal);
+	setlocale(LC_NUMERIC, "en_US");
+	const uint64_t t0 = now_ns();
+	struct rx_stats_state st = { .t_prev = t0 };
+	const char *label = o->label ? o->label : o->prog;
+	uint64_t seen = 0;
+	uint32_t k = 0, idle = 0;
+
+	while (!rc) {
+		struct rx_slot *s = &slot[k & 1];
+		const bool stop = rx_done || (o->count && seen >= o->count) ||
+				  (o->duration_ns && now_ns() - t0 >= o->duration_ns) ||
+				  (lv->inject && !o->count && !o->duration_ns &&
+				   seen >= lv->inject_count);
+		s->n = 0;
+		if (!stop) {
+			uint32_t want = o->batch;
+			if (o->count && o->count - seen < want)
+				want = (uint32_t)(o->count - seen);
+			s->n = xsk_rx(&x, (struct xdp_desc *)s->d, want);
+			if (s->n) {
+				rc = xdpgpu_submit(ctx, k & 1, s->d, s->n, s->v, NULL, NULL);
+				if (rc)
+					break;
+				s->busy = true;
+				s->first = seen;
+				seen += s->n;
+				in.received = seen;
+			}
+		}
+		/* the previous batch: wait, apply its verdicts to the rings */
+		struct rx_slot *p = &slot[(k + 1) & 1];
+		if (p->busy) {
+			rc = xdpgpu_wait(ctx, (k + 1) & 1);
+			if (rc)
+				break;
+			p->busy = false;
+			uint32_t ntx = 0, nfill = 0;
+			for (uint32_t i = 0; i < p->n; i++) {
+				const uint8_t v = p->v[i];
+				const uint64_t a = p->d[i].addr;
+				bool tx = false;
+
+				out->rx_frags++;
+				out->rx_pkts++;
+				out->rx_bytes += p->d[i].len;
+				if (v < XDPGPU_NUM_VERDICTS)
+					out->verdict[v]++;
+				if (verdicts && p->first + i < o->count)
+					verdicts[p->first + i] = v;
+				if (o->mode == RX_MODE_L2FWD && v == XDPGPU_REDIRECT) {
+					swap_macs(x.umem + a);
+					tx = true;
+				} else if (v == XDPGPU_TX && o->mode != RX_MODE_DROP) {
+					tx = true;     /* the reply the GPU wrote */
+				}
+				if (tx) {
+					txd[ntx].addr = a;
+					txd[ntx].len = p->d[i].len;
+					txd[ntx].options = 0;
+					ntx++;
+					out->tx_pkts++;
+					out->tx_frags++;
+					out->tx_bytes += p->d[i].len;
+				} else {
+					fill[nfree + nfill++] = a - a % lv->frame_size;
+				}
+			}
+			if (ntx)
+				rc = xsk_tx(&x, txd, ntx);
+			if (!rc && nfill)
+				rc = xsk_fill(&x, fill + nfree, nfill);
+			out->batches++;
+		}
+		/* sent frames back to the fill ring (complete_tx_l2fwd) */
+		if (!rc) {
+			uint32_t c = xsk_complete(&x, fill + nfree, lv->ring_size);
+			if (c)
+				rc = xsk_fill(&x, fill + nfree, c);
+			else if (x.tx.cached_prod != x.tx.cached_cons)
+				(void)xsk_kick_tx(&x);
+		}
+		if (stop && !slot[0].busy && !slot[1].busy)
+			break;
+		if (!s->n && !p->n) {
+			if (++idle > 64)
+				xsk_wakeup_rx(&x, 1);
+		} else {
+			idle = 0;
+		}
+		p->n = 0;
+		k++;
+		if (o->interval_s && !o->quiet) {
+			const uint64_t t = now_ns();
+			if (t - st.t_prev >= (uint64_t)o->interval_s * 1000000000ull)
+				print_stats(o, out, &st, label, t);
+		}
+	}
+	for (int j = 0; j < 2; j++)
+		if (slot[j].busy)
+			(void)xdpgpu_wait(ctx, j);
+	const uint64_t t1 = now_ns();
+	out->seconds = (double)(t1 - t0) / 1e9;
+	if (rc)
+		fprintf(stderr, "%s: live RX failed: %s %s\n", o->prog, strerror(-rc),
+			xdpgpu_last_error(ctx));
+	else if (!o->quiet)
+		print_stats(o, out, &st, label, t1);
+	if (!rc && verdicts) {
+		FILE *f = fopen(o->verdict_out, "wb");
+		const size_t nv = seen < o->count ? (size_t)seen : (size_t)o->count;
+		if (!f || fwrite(verdicts, 1, nv, f) != nv)
+			rc = -EIO;
+		if (f && fclose(f))
+			rc = -EIO;
+	}
+	if (!rc && o->json) {
+		const double mpps = out->seconds > 0 ? out->rx_pkts / out->seconds / 1e6 : 0;
+		printf("{\"prog\": \"%s\", \"live\": \"%s:%u\", \"frames\": %llu, \"seconds\": %.6f, "
+		       "\"mpps\": %.3f, \"rx_pkts\": %llu, \"rx_bytes\": %llu, \"tx_pkts\": %llu, "
+		       "\"injected\": %llu, \"batch\": %u, \"batches\": %llu, "
+		       "\"verdict\": {\"ABORTED\": %llu, \"DROP\": %llu, \"PASS\": %llu, "
+		       "\"TX\": %llu, \"REDIRECT\": %llu}}\n",
+		       o->prog, lv->ifname, lv->queue, (unsigned long long)out->rx_pkts,
+		       out->seconds, mpps, (unsigned long long)out->rx_pkts,
+		       (unsigned long long)out->rx_bytes, (unsigned long long)out->tx_pkts,
+		       (unsigned long long)in.sent, o->batch, (unsigned long long)out->batches,
+		       (unsigned long long)out->verdict[0], (unsigned long long)out->verdict[1],
+		       (unsigned long long)out->verdict[2], (unsigned long long)out->verdict[3],
+		       (unsigned long long)out->verdict[4]);
+		fflush(stdout);
+	}
+out:
+	if (th_up) {
+		in.stop = 1;
+		pthread_join(th, NULL);
+		if (!rc && in.rc)
+			rc = in.rc;
+	}
+	for (int j = 0; j < 2; j++) {
+		xdpgpu_host_free(slot[j].d);
+		xdpgpu_host_free(slot[j].v);
+	}
+	free(fill);
+	free(txd);
+	free(verdicts);
+	if (ctx)
+		xdpgpu_fini(ctx);
+	xsk_close(&x);
+	if (veth)
+		(void)xsk_link_delete(lv->ifname);
 	return rc;
 }

@@ -104,6 +104,31 @@ struct rx_totals {
 int rx_run(const struct rx_source *src, const struct rx_opts *opts,
 	   struct rx_totals *out);
 
+/* Live mode: an AF_XDP socket on ifname:queue
+ * (apps/xsk.c), its RX ring feeding the GPU batches, the verdicts applied
+ * to the fill and TX rings as the reference loops do (rx_drop / l2fwd,
+ * xdpsock.c:1462-1506, 1718-1784; af_xdp_user.c:1042-1113).  With
+ * veth_peer the program makes the veth pair ifname <-> veth_peer and
+ * removes it at the end (testenv.sh:214-307); with inject, a thread sends
+ * the source's frames into the peer (cycling it, inject_count frames,
+ * paced so that the RX ring never overflows). */
+struct rx_live {
+	const char *ifname;
+	uint32_t queue;
+	uint32_t frame_size;     /* chunk size (XSK_UMEM__DEFAULT_FRAME_SIZE) */
+	uint32_t nframes;        /* UMEM frames (NUM_FRAMES)                  */
+	uint32_t ring_size;      /* each ring (XSK_RING_*__DEFAULT_NUM_DESCS)  */
+	uint32_t bind_flags;     /* XDP_COPY / XDP_ZEROCOPY | NEED_WAKEUP      */
+	uint32_t xdp_flags;      /* XDP_FLAGS_SKB_MODE / DRV_MODE              */
+	const char *veth_peer;
+	const struct rx_source *inject;
+	uint64_t inject_count;
+};
+
+/* 0, -errno, or 1 when the host refuses AF_XDP / bpf / netlink (printed). */
+int rx_run_live(const struct rx_live *lv, const struct rx_opts *opts,
+		struct rx_totals *out);
+
 /* Parse "aa:bb:cc:dd:ee:ff". */
 bool rx_parse_mac(const char *s, uint8_t mac[6]);
 

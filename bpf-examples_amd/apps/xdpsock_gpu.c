@@ -14,12 +14,16 @@
  * (--frags) splits pcap records longer than a chunk into multi-buffer
  * packets (XDPGPU_CFG_FRAGS) and counts packets and fragments.  Frames
  * come from a UMEM this program fills, either a synthetic pool (--pool N)
- * or a pcap file (--pcap FILE).  Live AF_XDP sockets are not part of this
- * build.
+ * or a pcap file (--pcap FILE), or, with -i IF and neither, from a live
+ * AF_XDP socket on IF:queue (apps/xsk.c; -S generic / -N native XDP, -c
+ * copy / -z zero-copy, -m no need_wakeup, -f chunk size): config 1.
  *
  * Added options: --gpu N, --pool N, --pool-kind xdpsock|udp4|imix|afxdp,
  * --seed S, --pcap FILE, --no-verify, --initval N, --json, --verdicts FILE,
- * --tx-pcap FILE, --dry-run.  Exit status: 0, 1 on a failure, 2 on a bad
+ * --tx-pcap FILE, --dry-run; live mode: --veth PEER (make the veth pair
+ * IF <-> PEER, as testenv.sh does), --inject N (send N frames of the pool
+ * the pool options describe into PEER), --inject-pcap FILE.  Exit status:
+ * 0, 1 on a failure (live: also when the host refuses AF_XDP), 2 on a bad
  * option (xdpsock's usage() exits with EXIT_FAILURE).
  */
 #define _GNU_SOURCE
@@ -30,7 +34,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <linux/if_link.h>
+
 #include "rxapp.h"
+#include "xsk.h"
 
 #define MIN_PKT_SIZE 64            /* xdpsock.c:65 */
 #define MAX_PKT_SIZE 9728          /* xdpsock.c:66 */
@@ -40,6 +47,7 @@
 enum {
 	OPT_GPU = 256, OPT_POOL, OPT_POOL_KIND, OPT_SEED, OPT_PCAP, OPT_NO_VERIFY,
 	OPT_INITVAL, OPT_JSON, OPT_VERDICTS, OPT_TX_PCAP, OPT_DRY_RUN, OPT_HELP,
+	OPT_VETH, OPT_INJECT, OPT_INJECT_PCAP,
 };
 
 static struct option long_options[] = {
@@ -93,6 +101,9 @@ static struct option long_options[] = {
 	{ "verdicts", required_argument, 0, OPT_VERDICTS },
 	{ "tx-pcap", required_argument, 0, OPT_TX_PCAP },
 	{ "dry-run", no_argument, 0, OPT_DRY_RUN },
+	{ "veth", required_argument, 0, OPT_VETH },
+	{ "inject", required_argument, 0, OPT_INJECT },
+	{ "inject-pcap", required_argument, 0, OPT_INJECT_PCAP },
 	{ "help", no_argument, 0, OPT_HELP },
 	{ 0, 0, 0, 0 }
 };
@@ -105,8 +116,13 @@ static void usage(const char *prog)
 		"  -r, --rxdrop		Discard all incoming packets (default)\n"
 		"  -l, --l2fwd		MAC swap L2 forwarding\n"
 		"  -t, --txonly		(not available: no receive path)\n"
-		"  -i, --interface=n	Label the statistics with interface n\n"
-		"  -q, --queue=n	Queue label (default 0)\n"
+		"  -i, --interface=n	Live AF_XDP socket on n (no --pool/--pcap), else a label\n"
+		"  -q, --queue=n	Queue (default 0)\n"
+		"  -S, --xdp-skb	Generic XDP (live; the default on veth)\n"
+		"  -N, --xdp-native	Native XDP (live)\n"
+		"  -c, --copy		Copy mode (live, default)\n"
+		"  -z, --zero-copy	Zero-copy mode (live)\n"
+		"  -m, --no-need-wakeup	No need_wakeup flag (live)\n"
 		"  -n, --interval=n	Statistics update interval (default 1 sec)\n"
 		"  -f, --frame-size=n   UMEM chunk size for --pcap (power of two unless -u, default %d)\n"
 		"  -u, --unaligned	Unaligned (packed) chunk placement\n"
@@ -124,7 +140,7 @@ static void usage(const char *prog)
 		"  -Q, --quiet          Do not display any stats\n"
 		"  -F, --frags          Multi-buffer packets: pcap records longer than a chunk span\n"
 		"                       several chunks (XDP_PKT_CONTD); packets and frags counted\n"
-		"  -p -S -N -z -c -m -M -B -R -w -W -U -I -O -T -y -a: accepted, no effect\n"
+		"  -p -M -B -R -w -W -U -I -O -T -y -a: accepted, no effect\n"
 		"  Options (this build):\n"
 		"      --gpu=n          HIP device (default 0)\n"
 		"      --pool=n         Synthetic UMEM pool of n frames\n"
@@ -136,7 +152,10 @@ static void usage(const char *prog)
 		"      --json           One JSON summary line at the end\n"
 		"      --verdicts=file  Per-frame verdicts (u8, enum xdp_action) of the first pass\n"
 		"      --tx-pcap=file   The frames sent (l2fwd) in the first pass, as pcap\n"
-		"      --dry-run        Build the UMEM, describe it, no GPU\n",
+		"      --dry-run        Build the UMEM, describe it, no GPU\n"
+		"      --veth=peer      Live: make the veth pair IF <-> peer (removed at exit)\n"
+		"      --inject=n       Live: send n frames of the pool (pool options) into peer\n"
+		"      --inject-pcap=f  Live: send the frames of a pcap file into peer\n",
 		prog, DEFAULT_FRAME_SIZE, 64, MIN_PKT_SIZE, MAX_PKT_SIZE, MIN_PKT_SIZE,
 		DEFAULT_PATTERN);
 	exit(2);
@@ -155,6 +174,54 @@ static int pool_kind(const char *s)
 	return -1;
 }
 
+/* config 1: a live socket, frames from the wire (or the injected source) */
+static int run_live(const char *prog, const char *ifname, uint32_t queue, struct rx_opts *o,
+		    uint32_t frame_size, bool skb, bool zerocopy, bool no_wakeup,
+		    const char *veth, uint64_t inject_n, const char *inject_pcap, int kind,
+		    uint32_t pkt_size, uint64_t seed)
+{
+	struct rx_source inj;
+	bool have_inj = false;
+	int rc;
+
+	if (inject_n || inject_pcap) {
+		if (inject_pcap) {
+			rc = rx_source_pcap(&inj, inject_pcap, 2048, 0, true, false, 0);
+		} else {
+			struct xdpgpu_pool_spec spec;
+			xdpgpu_pool_spec_default(&spec, (uint32_t)kind, pkt_size, seed);
+			rc = rx_source_pool(&inj, &spec,
+					    (uint32_t)(inject_n < 1048576 ? inject_n : 1048576));
+		}
+		if (rc) {
+			fprintf(stderr, "%s: inject source: %s\n", prog, strerror(-rc));
+			return 1;
+		}
+		have_inj = true;
+		if (!inject_n)
+			inject_n = inj.n;
+	}
+	/* xdpsock's defaults: NUM_FRAMES 4096, 2048-entry rings
+	 * (XSK_RING_*__DEFAULT_NUM_DESCS), 4096-byte frames */
+	struct rx_live lv = {
+		.ifname = ifname, .queue = queue, .frame_size = frame_size,
+		.nframes = 4096, .ring_size = 2048,
+		.bind_flags = (zerocopy ? XDP_ZEROCOPY : XDP_COPY) |
+			      (no_wakeup ? 0 : XDP_USE_NEED_WAKEUP),
+		.xdp_flags = skb ? XDP_FLAGS_SKB_MODE : XDP_FLAGS_DRV_MODE,
+		.veth_peer = veth, .inject = have_inj ? &inj : NULL, .inject_count = inject_n,
+	};
+	char label[128];
+	snprintf(label, sizeof(label), "%s:%u %s %s", ifname, queue,
+		 o->mode == RX_MODE_L2FWD ? "l2fwd" : "rxdrop", skb ? "xdp-skb" : "xdp-drv");
+	o->label = label;
+	struct rx_totals t;
+	rc = rx_run_live(&lv, o, &t);
+	if (have_inj)
+		rx_source_free(&inj);
+	return rc ? 1 : 0;
+}
+
 int main(int argc, char **argv)
 {
 	const char *prog = basename(argv[0]);
@@ -162,7 +229,9 @@ int main(int argc, char **argv)
 	int queue = 0, kind = XDPGPU_POOL_XDPSOCK, vlan = 0, dry = 0, extra = 0;
 	uint32_t pool_n = 0, pkt_size = MIN_PKT_SIZE, frame_size = DEFAULT_FRAME_SIZE;
 	uint32_t pattern = DEFAULT_PATTERN, vlan_id = 1, vlan_pri = 0, unaligned = 0;
-	uint64_t seed = 0x5EED0002;
+	uint64_t seed = 0x5EED0002, inject_n = 0;
+	const char *veth = NULL, *inject_pcap = NULL;
+	bool live_native = false, zerocopy = false, no_wakeup = false, iface_set = false;
 	uint8_t dmac[6], smac[6];
 	bool have_dmac = false, have_smac = false, have_pattern = false, skb = false;
 	struct rx_opts o = {
@@ -187,9 +256,13 @@ int main(int argc, char **argv)
 			fprintf(stderr, "%s: -t/--txonly has no receive path; use xdpsock\n",
 				prog);
 			return 2;
-		case 'i': ifname = optarg; break;
+		case 'i': ifname = optarg; iface_set = true; break;
 		case 'q': queue = atoi(optarg); break;
 		case 'S': skb = true; break;
+		case 'N': live_native = true; break;
+		case 'z': zerocopy = true; break;
+		case 'c': zerocopy = false; break;
+		case 'm': no_wakeup = true; break;
 		case 'n': o.interval_s = (uint32_t)atoi(optarg); break;
 		case 'f': frame_size = (uint32_t)atoi(optarg); break;
 		case 'u': unaligned = 1; break;
@@ -226,10 +299,10 @@ int main(int argc, char **argv)
 			break;
 		case 'x': extra = 1; break;
 		case 'Q': o.quiet = true; break;
-		case 'p': case 'N': case 'w': case 'O': case 'c': case 'z': case 'm':
+		case 'p': case 'w': case 'O':
 		case 'M': case 'T': case 'y': case 'W': case 'U': case 'a': case 'I':
 		case 'B': case 'R':
-			break;    /* socket / scheduling options: no socket here */
+			break;    /* scheduling options: no effect */
 		case 'F':
 			/* opt_frags (xdpsock.c:1349): multi-buffer packets */
 			o.frags = true;
@@ -252,15 +325,22 @@ int main(int argc, char **argv)
 		case OPT_VERDICTS: o.verdict_out = optarg; break;
 		case OPT_TX_PCAP: o.tx_pcap = optarg; break;
 		case OPT_DRY_RUN: dry = 1; break;
+		case OPT_VETH: veth = optarg; break;
+		case OPT_INJECT: inject_n = strtoull(optarg, NULL, 0); break;
+		case OPT_INJECT_PCAP: inject_pcap = optarg; break;
 		default:
 			usage(prog);
 		}
 	}
 	if (optind < argc)
 		usage(prog);
-	if (!pool_n && !pcap) {
-		fprintf(stderr, "%s: live AF_XDP sockets are not part of this build; "
-			"give --pool N or --pcap FILE\n", prog);
+	const bool live = !pool_n && !pcap;
+	if (live && !iface_set) {
+		fprintf(stderr, "%s: give -i IF (live AF_XDP), --pool N or --pcap FILE\n", prog);
+		usage(prog);
+	}
+	if (!live && (veth || inject_n || inject_pcap)) {
+		fprintf(stderr, "%s: --veth / --inject are live-mode options (-i IF)\n", prog);
 		usage(prog);
 	}
 	if (pool_n && pcap) {
@@ -278,6 +358,10 @@ int main(int argc, char **argv)
 	}
 	if (!extra)
 		o.cfg_flags &= ~XDPGPU_CFG_STATS;
+	if (live)
+		return run_live(prog, ifname, (uint32_t)queue, &o, frame_size, skb || !live_native,
+				zerocopy, no_wakeup, veth, inject_n, inject_pcap, kind, pkt_size,
+				seed);
 
 	struct rx_source src;
 	int rc;

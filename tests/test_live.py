@@ -1,0 +1,124 @@
+# SPDX-License-Identifier: GPL-2.0
+"""Live AF_XDP.
+
+CPU: the socket plumbing of bpf-examples_amd/apps/xsk.c (UMEM, fill / RX /
+TX / completion rings, the XSKMAP redirect program, a veth pair) moves
+frames byte for byte, where the host allows AF_XDP (skipped where it
+refuses; DESIGN.md records which hosts do).
+
+GPU: the frames a live socket received here (tests/golden/live_capture.npz,
+tools/live_capture.py: the RX ring's chunk addresses and bytes, chunks
+recycled through the fill ring) replayed through the host path as the live
+loop drives it (two slots in flight, batches of 64, each batch's frames
+written into their chunks first): verdicts, records and the echo replies
+written back, bit-exact with the oracle."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+import xdpgpu
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+APPS = os.path.join(ROOT, "bpf-examples_amd", "apps")
+FIXTURE = os.path.join(ROOT, "tests", "golden", "live_capture.npz")
+
+
+def _probe():
+    exe = os.path.join(APPS, "xsk_probe")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", APPS, "xsk_probe"], check=True)
+    return exe
+
+
+def test_xsk_plumbing_live():
+    r = subprocess.run([_probe(), "--frames", "3000", "--size", "256", "--ifa", "xgta0",
+                        "--ifb", "xgtb0"], capture_output=True, text=True, timeout=120)
+    if r.returncode == 2:
+        pytest.skip(f"host refuses live AF_XDP: {r.stdout.strip()}")
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert '"ok": true' in r.stdout
+
+
+def test_live_fixture_is_the_pool_frames():
+    """The captured frames are the generator's frames, in the order sent."""
+    fx = np.load(FIXTURE)
+    lens, frames = fx["lens"], fx["frames"]
+    descs = fx["descs"].view(xdpgpu.DESC_DTYPE)
+    assert len(descs) == len(lens) and int(lens.sum()) == len(frames)
+    assert np.array_equal(descs["len"], lens)
+    # each frame inside its chunk (copy mode puts it XDP_PACKET_HEADROOM in)
+    chunk = int(fx["chunk"])
+    assert np.all(descs["addr"] % chunk + descs["len"] <= chunk)
+    # the first pool (xdpsock shape, 1024 frames of 64 B) leads the capture
+    u, d, _ = xdpgpu.pool_generate(1024, xdpgpu.POOL_XDPSOCK, 64, 0x5EED0051)
+    eff = (d["addr"] & ((1 << 48) - 1)) + (d["addr"] >> 48)
+    off = np.concatenate([[0], np.cumsum(lens.astype(np.int64))])
+    k = 0
+    for i in range(1024):
+        ln = int(d["len"][i])
+        if 14 <= ln <= 1514:
+            assert frames[off[k]:off[k + 1]].tobytes() == u[int(eff[i]):int(eff[i]) + ln].tobytes()
+            k += 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("flags", [xdpgpu.CFG_DEFAULT,
+                                   xdpgpu.CFG_DEFAULT | xdpgpu.CFG_ICMP6_ECHO],
+                         ids=["verify", "echo"])
+def test_live_capture_vs_oracle(flags):
+    pytest.importorskip("torch")
+    fx = np.load(FIXTURE)
+    descs = fx["descs"].view(xdpgpu.DESC_DTYPE).copy()
+    lens, frames = fx["lens"], fx["frames"]
+    chunk = int(fx["chunk"])
+    off = np.concatenate([[0], np.cumsum(lens.astype(np.int64))])
+    nchunks = int(descs["addr"].max()) // chunk + 1
+    umem = np.zeros(nchunks * chunk, np.uint8)          # the socket's UMEM
+    ou = umem.copy()                                     # the oracle's
+    B = 64
+    n = len(descs)
+    with xdpgpu.XdpGpu(0, flags, 0x9E3779B9, xdpgpu.TUPLE_V4, max_batch=B) as ctx:
+        ctx.register_umem(umem)
+        bufs = [(xdpgpu.HostBuffer(B, xdpgpu.DESC_DTYPE), xdpgpu.HostBuffer(B, np.uint8),
+                 xdpgpu.HostBuffer(B, xdpgpu.RESULT_DTYPE),
+                 xdpgpu.HostBuffer(B * 16, np.uint8)) for _ in range(2)]
+        pending = [None, None]
+
+        def collect(slot):
+            lo, hi = pending[slot]
+            ctx.wait(slot)
+            d, v, r, t = bufs[slot]
+            m = hi - lo
+            ov, ores, otup, _ = oracle.process(ou, descs[lo:hi], flags, 0x9E3779B9, 1)
+            np.testing.assert_array_equal(v.array[:m], ov, err_msg=f"frames {lo}..{hi}")
+            assert r.array[:m].tobytes() == ores.tobytes(), f"records {lo}..{hi}"
+            assert t.array[: 16 * m].tobytes() == otup.tobytes(), f"tuples {lo}..{hi}"
+            for i in range(lo, hi):      # the chunk's bytes after the batch
+                a, ln = int(descs["addr"][i]), int(descs["len"][i])
+                assert umem[a:a + ln].tobytes() == ou[a:a + ln].tobytes(), f"frame {i}"
+            pending[slot] = None
+
+        for k, lo in enumerate(range(0, n, B)):
+            slot = k & 1
+            if pending[slot] is not None:
+                collect(slot)
+            hi = min(n, lo + B)
+            # the kernel wrote the batch's frames into their chunks
+            for i in range(lo, hi):
+                a = int(descs["addr"][i])
+                umem[a:a + int(lens[i])] = frames[off[i]:off[i + 1]]
+                ou[a:a + int(lens[i])] = frames[off[i]:off[i + 1]]
+            d, v, r, t = bufs[slot]
+            d.array[: hi - lo] = descs[lo:hi]
+            ctx.submit(slot, d.array[: hi - lo], v.array[: hi - lo], r.array[: hi - lo],
+                       t.array[: 16 * (hi - lo)])
+            pending[slot] = (lo, hi)
+        for slot in range(2):
+            if pending[slot] is not None:
+                collect(slot)
+        for b in bufs:
+            for x in b:
+                x.close()
