@@ -117,17 +117,28 @@ def cpu_baseline(umem, descs, flags, fmt, budget_s: float = 10.0):
     import oracle
     oracle.lib()
     try:
-        cores = len(os.sched_getaffinity(0))
+        affinity = len(os.sched_getaffinity(0))
     except AttributeError:
-        cores = os.cpu_count() or 1
+        affinity = os.cpu_count() or 1
+    # the cgroup's CPU quota, when it is below the affinity set (a GPU box's
+    # share of its host): more threads than that only time-slice
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    cores = min(affinity, quota) if quota else affinity
     sample = descs[: 1 << 21]
     one = sample[: 1 << 19]
     t1, _ = oracle.leg_bench(umem, one, 1, 1, True, flags, 0, fmt)
     reps1 = max(1, int(3.0 / max(t1, 1e-3)))
     t1, _ = oracle.leg_bench(umem, one, 1, reps1, True, flags, 0, fmt)
     st_mpps = len(one) * reps1 / t1 / 1e6
-    dt, _ = oracle.leg_bench(umem, sample, cores, 1, True, flags, 0, fmt)
-    reps = max(1, int(budget_s / max(dt, 1e-3)))
+    dt, _ = oracle.leg_bench(umem, sample, cores, 2, True, flags, 0, fmt)
+    reps = max(1, int(2 * budget_s / max(dt, 1e-3)))
     dt, (v, res, tup) = oracle.leg_bench(umem, sample, cores, reps, True, flags, 0, fmt)
     mpps = len(sample) * reps / dt / 1e6
     k = 1 << 16
@@ -142,6 +153,7 @@ def cpu_baseline(umem, descs, flags, fmt, budget_s: float = 10.0):
     if ref:
         cal["leg_over_reference"] = round(ref / mine, 3)
     return {"value": round(mpps, 2), "unit": "Mpps", "cores": cores,
+            "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
             "kind": "port", "cpu_model": cpu_model(),
             "gbps": round(mpps * 1e6 * BYTES_PER_FRAME / 1e9, 2),
             "single_thread_mpps": round(st_mpps, 2),

@@ -13,10 +13,13 @@
  * by default (--verify turns the DROP verdict on).  The reference's
  * options are parsed with its short-option string; the ones that act on a
  * kernel socket or XDP program (-S -N -A -F -c -z -Q -p -w -s -U -B
- * --filename --progsec --offload-mode) have no effect here, -d labels the
- * statistics, --src-ip/--dst-ip/-G/-H set the generated frames
- * (gen_base_pkt, af_xdp_user.c:688-700).  Frames come from --pool N or
- * --pcap FILE; live AF_XDP sockets are not part of this build.
+ * --filename --progsec --offload-mode) have no effect on a pool or pcap
+ * source, -d labels the statistics, --src-ip/--dst-ip/-G/-H set the
+ * generated frames (gen_base_pkt, af_xdp_user.c:688-700).  Frames come from
+ * --pool N or --pcap FILE, or, with -d IF and neither, from a live AF_XDP
+ * socket on IF (apps/xsk.c; -S / -N, -c / -z, -Q queue as the reference
+ * uses them; --veth PEER, --inject N, --inject-pcap FILE as xdpsock-gpu's),
+ * the echo replies sent on its TX ring.
  *
  * Exit status as common_defines.h:50-54: 0, 1 (EXIT_FAIL), 2
  * (EXIT_FAIL_OPTION).
@@ -30,7 +33,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <linux/if_link.h>
+
 #include "rxapp.h"
+#include "xsk.h"
 
 #define EXIT_OK 0
 #define EXIT_FAIL 1
@@ -39,7 +45,7 @@
 enum {
 	OPT_GPU = 256, OPT_POOL, OPT_POOL_KIND, OPT_SEED, OPT_PCAP, OPT_VERIFY,
 	OPT_COUNT, OPT_DURATION, OPT_JSON, OPT_VERDICTS, OPT_TX_PCAP, OPT_DRY_RUN,
-	OPT_ECHO_PPM, OPT_SIZE, OPT_BATCH,
+	OPT_ECHO_PPM, OPT_SIZE, OPT_BATCH, OPT_VETH, OPT_INJECT, OPT_INJECT_PCAP,
 };
 
 struct opt_help {
@@ -51,14 +57,14 @@ struct opt_help {
 /* af_xdp_user.c:225-309, plus this build's options */
 static const struct opt_help opts[] = {
 	{ { "help", no_argument, NULL, 'h' }, "Show help", NULL },
-	{ { "dev", required_argument, NULL, 'd' }, "Label the statistics with <ifname>", "<ifname>" },
-	{ { "skb-mode", no_argument, NULL, 'S' }, "(no effect: no XDP program here)", NULL },
-	{ { "native-mode", no_argument, NULL, 'N' }, "(no effect)", NULL },
+	{ { "dev", required_argument, NULL, 'd' }, "Live AF_XDP on <ifname> (no --pool/--pcap), else a label", "<ifname>" },
+	{ { "skb-mode", no_argument, NULL, 'S' }, "Generic XDP (live; default)", NULL },
+	{ { "native-mode", no_argument, NULL, 'N' }, "Native XDP (live)", NULL },
 	{ { "auto-mode", no_argument, NULL, 'A' }, "(no effect)", NULL },
 	{ { "force", no_argument, NULL, 'F' }, "(no effect)", NULL },
-	{ { "copy", no_argument, NULL, 'c' }, "(no effect)", NULL },
-	{ { "zero-copy", no_argument, NULL, 'z' }, "(no effect)", NULL },
-	{ { "queue", required_argument, NULL, 'Q' }, "Receive queue label", NULL },
+	{ { "copy", no_argument, NULL, 'c' }, "Copy mode (live; default)", NULL },
+	{ { "zero-copy", no_argument, NULL, 'z' }, "Zero-copy mode (live)", NULL },
+	{ { "queue", required_argument, NULL, 'Q' }, "Receive queue", NULL },
 	{ { "priority", required_argument, NULL, 'p' }, "(no effect)", NULL },
 	{ { "wakeup-mode", no_argument, NULL, 'w' }, "(no effect)", NULL },
 	{ { "spin-mode", no_argument, NULL, 's' }, "(no effect)", NULL },
@@ -92,6 +98,9 @@ static const struct opt_help opts[] = {
 	{ { "verdicts", required_argument, NULL, OPT_VERDICTS }, "Per-frame verdicts of the first pass", "<file>" },
 	{ { "tx-pcap", required_argument, NULL, OPT_TX_PCAP }, "The echo replies of the first pass, as pcap", "<file>" },
 	{ { "dry-run", no_argument, NULL, OPT_DRY_RUN }, "Build the UMEM, describe it, no GPU", NULL },
+	{ { "veth", required_argument, NULL, OPT_VETH }, "Live: make the veth pair <ifname> <-> <peer>", "<peer>" },
+	{ { "inject", required_argument, NULL, OPT_INJECT }, "Live: send <n> frames of the pool into the peer", "<n>" },
+	{ { "inject-pcap", required_argument, NULL, OPT_INJECT_PCAP }, "Live: send a pcap file's frames into the peer", "<file>" },
 	{ { NULL, 0, NULL, 0 }, NULL, NULL },
 };
 
@@ -142,8 +151,10 @@ static int pool_kind(const char *s)
 int main(int argc, char **argv)
 {
 	const char *prog = basename(argv[0]);
-	const char *ifname = "pool", *pcap = NULL;
+	const char *ifname = "pool", *pcap = NULL, *veth = NULL, *inject_pcap = NULL;
 	int queue = 0, kind = XDPGPU_POOL_AFXDP_USER, dry = 0;
+	bool dev_set = false, native = false, zerocopy = false;
+	uint64_t inject_n = 0;
 	uint32_t pool_n = 0, size = 64, echo_ppm = 0, saddr = 0, daddr = 0;
 	bool have_echo = false, have_dmac = false, have_smac = false;
 	uint64_t seed = 0x5EED0003;
@@ -172,6 +183,7 @@ int main(int argc, char **argv)
 				return opt_error(prog);
 			}
 			ifname = optarg;
+			dev_set = true;
 			break;
 		case 'Q': queue = atoi(optarg); break;
 		case 'q': o.quiet = true; break;
@@ -204,8 +216,15 @@ int main(int argc, char **argv)
 				daddr = a;
 			break;
 		}
-		case 'r': case 'L': case 'R': case 'B': case 'A': case 'S': case 'N':
-		case 'F': case 'U': case 'M': case 'c': case 'z': case 'p': case 't':
+		case 'N': native = true; break;
+		case 'S': native = false; break;
+		case 'z': zerocopy = true; break;
+		case 'c': zerocopy = false; break;
+		case OPT_VETH: veth = optarg; break;
+		case OPT_INJECT: inject_n = strtoull(optarg, NULL, 0); break;
+		case OPT_INJECT_PCAP: inject_pcap = optarg; break;
+		case 'r': case 'L': case 'R': case 'B': case 'A':
+		case 'F': case 'U': case 'M': case 'p': case 't':
 		case 'i': case 'w': case 's': case 'P': case 'm': case 'D':
 		case 1: case 2: case 3:
 			break;    /* kernel socket / XDP program / debug options */
@@ -241,9 +260,13 @@ int main(int argc, char **argv)
 	}
 	if (optind < argc)
 		return opt_error(prog);
-	if (!pool_n == !pcap) {
-		fprintf(stderr, "ERR: give one of --pool N or --pcap FILE "
-			"(live AF_XDP sockets are not part of this build)\n");
+	const bool live = !pool_n && !pcap && dev_set;
+	if (!live && !pool_n == !pcap) {
+		fprintf(stderr, "ERR: give one of -d IF (live AF_XDP), --pool N or --pcap FILE\n");
+		return opt_error(prog);
+	}
+	if (!live && (veth || inject_n || inject_pcap)) {
+		fprintf(stderr, "ERR: --veth / --inject need a live socket (-d IF)\n");
 		return opt_error(prog);
 	}
 	if (!o.batch) {
@@ -253,6 +276,47 @@ int main(int argc, char **argv)
 
 	struct rx_source src;
 	int rc;
+	if (live) {
+		/* af_xdp_user's geometry: NUM_FRAMES 4096 of FRAME_SIZE,
+		 * af_xdp_user.c:55-56; default rings */
+		struct rx_source inj;
+		bool have_inj = false;
+		if (inject_n || inject_pcap) {
+			if (inject_pcap) {
+				rc = rx_source_pcap(&inj, inject_pcap, 2048, 0, true, false, 0);
+			} else {
+				struct xdpgpu_pool_spec spec;
+				xdpgpu_pool_spec_default(&spec, (uint32_t)kind, size, seed);
+				if (have_echo)
+					spec.ppm_echo6 = echo_ppm;
+				rc = rx_source_pool(&inj, &spec,
+						    (uint32_t)(inject_n < 1048576 ? inject_n : 1048576));
+			}
+			if (rc) {
+				fprintf(stderr, "ERR: inject source: %s\n", strerror(-rc));
+				return EXIT_FAIL;
+			}
+			have_inj = true;
+			if (!inject_n)
+				inject_n = inj.n;
+		}
+		struct rx_live lv = {
+			.ifname = ifname, .queue = (uint32_t)queue, .frame_size = 4096,
+			.nframes = 4096, .ring_size = 2048,
+			.bind_flags = (zerocopy ? XDP_ZEROCOPY : XDP_COPY) | XDP_USE_NEED_WAKEUP,
+			.xdp_flags = native ? XDP_FLAGS_DRV_MODE : XDP_FLAGS_SKB_MODE,
+			.veth_peer = veth, .inject = have_inj ? &inj : NULL,
+			.inject_count = inject_n,
+		};
+		char label[64];
+		snprintf(label, sizeof(label), "%s:%d", ifname, queue);
+		o.label = label;
+		struct rx_totals t;
+		rc = rx_run_live(&lv, &o, &t);
+		if (have_inj)
+			rx_source_free(&inj);
+		return rc ? EXIT_FAIL : EXIT_OK;
+	}
 	if (pcap) {
 		/* af_xdp_user's UMEM: FRAME_SIZE chunks, af_xdp_user.c:56 */
 		rc = rx_source_pcap(&src, pcap, 4096, 0, false, false, 0);

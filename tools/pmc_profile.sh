@@ -8,7 +8,8 @@ VARIANT=${VARIANT:-64:0}
 DEST=${DEST:-}
 mkdir -p $OUT
 export TMPDIR=/tmp
-CMD="python3 tools/tune_rx.py --variants $VARIANT --rounds 1 --reps 3"
+ARGS=${PMC_ARGS:-}
+CMD="python3 tools/tune_rx.py --variants $VARIANT --rounds 1 --reps 3 $ARGS"
 i=0
 for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
 	   "SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE" \

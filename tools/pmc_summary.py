@@ -12,10 +12,10 @@ import sys
 from collections import defaultdict
 
 
-RX = ("xdp_rx_kernel", "xdp_rx_bulk_kernel", "xdp_rx_generic_kernel")
+RX = ("xdp_rx_db_kernel", "xdp_rx_kernel", "xdp_rx_bulk_kernel", "xdp_rx_generic_kernel")
 
 
-def main(out, dest=None, frames=16 << 20, size=64):
+def main(out, dest=None, frames=16 << 20, size=64, label=None):
     acc = defaultdict(lambda: defaultdict(list))
     for f in glob.glob(os.path.join(out, "p*", "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
@@ -45,8 +45,8 @@ def main(out, dest=None, frames=16 << 20, size=64):
     rx = {k: v for k, v in summary.items()
           if any(k.split("<")[0].split("(")[0].endswith(r) for r in RX)}
     tot = sum(v.get("hbm_bytes_per_launch", 0.0) for v in rx.values())
-    doc = {"workload": f"config2 pool: {frames} x {size} B IPv4/UDP "
-                       "(tools/tune_rx.py, V4 tuples)",
+    doc = {"workload": label or (f"config2 pool: {frames} x {size} B IPv4/UDP "
+                                 "(tools/tune_rx.py, V4 tuples)"),
            "frames": frames, "frame_size": size,
            "method": "rocprofv3 --pmc, one counter group per pass; "
                      "bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 "
@@ -60,4 +60,6 @@ def main(out, dest=None, frames=16 << 20, size=64):
 
 if __name__ == "__main__":
     main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc",
-         sys.argv[2] if len(sys.argv) > 2 else None)
+         sys.argv[2] if len(sys.argv) > 2 else None,
+         int(os.environ.get("FRAMES", 16 << 20)), int(os.environ.get("SIZE", 64)),
+         os.environ.get("LABEL"))
