@@ -300,35 +300,50 @@ __device__ __forceinline__ bool v4pos(uint32_t plen, int (&pos)[4], int &pref_en
 }
 
 struct Tables {
-	const Nat64V6Bucket *v6map;
+	Nat64V6Bucket *v6map;
 	uint32_t v6nb;
 	const Nat64V4Bucket *v4map;
 	uint32_t v4nb;
+	uint32_t dyn;              /* Nat64Args.dyn, .now, .thr */
+	unsigned long long now, thr;
 };
 
-/* v6_state_map lookup: v4 (host order) or 0.  One 128-byte bucket per
- * probe: the four keys and the value word are 16-byte loads of one line. */
+/* v6_state_map lookup (nat64_handle_v6, nat64_kern.c:809-828): the IPv4
+ * address (host order) of the source's entry, one 128-byte bucket per
+ * probe.  With dynamic state a hit stamps last_seen with the batch clock
+ * (nat64_kern.c:821-823), and an entry that has timed out (last_seen <
+ * now - timeout_ns, not static: check_item, :543-561) counts as a miss:
+ * an earlier frame of the batch may reclaim it, which only the host's
+ * in-order commit can tell. */
 __device__ uint32_t lookup_v6(const Tables &T, const uint32_t (&w)[4], bool &found)
 {
 	uint32_t b = nat64_home(slot_hash(w[0], w[1], w[2], w[3]), T.v6nb);
 	for (uint32_t probe = 0; probe < T.v6nb; probe++) {
-		const Nat64V6Bucket *B = T.v6map + b;
-		uint4 k[4];
-#pragma unroll
-		for (int j = 0; j < 4; j++)
-			k[j] = B->key[j];
-		const uint4 v = *reinterpret_cast<const uint4 *>(B->val);
-		const uint32_t cnt = B->n;
-		const uint32_t vals[4] = {v.x, v.y, v.z, v.w};
+		Nat64V6Bucket *B = T.v6map + b;
+		const uint32_t meta = B->meta;
+		uint32_t hit = 0;
 #pragma unroll
 		for (int j = 0; j < 4; j++) {
-			if ((uint32_t)j < cnt && k[j].x == w[0] && k[j].y == w[1] &&
-			    k[j].z == w[2] && k[j].w == w[3]) {
-				found = true;
-				return vals[j];
-			}
+			const uint4 k = B->key[j];
+			hit |= ((k.x == w[0]) & (k.y == w[1]) & (k.z == w[2]) & (k.w == w[3]))
+				       ? 1u << j : 0u;
 		}
-		if (cnt < 4)
+		hit &= meta;
+		if (hit) {
+			const uint32_t j = (uint32_t)__builtin_ctz(hit);
+			if (T.dyn) {
+				const unsigned long long ls = B->last_seen[j];
+				if (!((meta >> (8 + j)) & 1) && ls < T.thr) {
+					found = false;
+					return 0;
+				}
+				if (ls != T.now)
+					B->last_seen[j] = T.now;
+			}
+			found = true;
+			return B->val[j];
+		}
+		if (!(meta & kNat64Ovf))
 			break;
 		b = b + 1 == T.v6nb ? 0 : b + 1;
 	}
@@ -342,24 +357,42 @@ __device__ bool lookup_v4(const Tables &T, uint32_t v4, uint32_t (&w)[4])
 	for (uint32_t probe = 0; probe < T.v4nb; probe++) {
 		const Nat64V4Bucket *B = T.v4map + b;
 		const uint4 k = *reinterpret_cast<const uint4 *>(B->key);
-		const uint32_t cnt = B->n;
-		const uint32_t keys[4] = {k.x, k.y, k.z, k.w};
-#pragma unroll
-		for (int j = 0; j < 4; j++) {
-			if ((uint32_t)j < cnt && keys[j] == v4) {
-				const uint4 v = B->val[j];
-				w[0] = v.x;
-				w[1] = v.y;
-				w[2] = v.z;
-				w[3] = v.w;
-				return true;
-			}
+		const uint32_t hit = B->meta & ((k.x == v4 ? 1u : 0u) | (k.y == v4 ? 2u : 0u) |
+						(k.z == v4 ? 4u : 0u) | (k.w == v4 ? 8u : 0u));
+		if (hit) {
+			const uint4 v = B->val[__builtin_ctz(hit)];
+			w[0] = v.x;
+			w[1] = v.y;
+			w[2] = v.z;
+			w[3] = v.w;
+			return true;
 		}
-		if (cnt < 4)
+		if (!(B->meta & kNat64Ovf))
 			break;
 		b = b + 1 == T.v4nb ? 0 : b + 1;
 	}
 	return false;
+}
+
+/* List the wave's frames that need the host's commit (dynamic state):
+ * one atomic per wave on the list length. */
+__device__ __forceinline__ void miss_append(const Nat64Args &a, bool miss, uint32_t i,
+					    uint4 src, int lane)
+{
+	const uint64_t m = __ballot(miss);
+	if (!m)
+		return;
+	const int lead = __builtin_ffsll((long long)m) - 1;
+	uint32_t base = 0;
+	if (lane == lead)
+		base = atomicAdd(a.miss_cnt, (uint32_t)__popcll(m));
+	base = __shfl(base, lead);
+	const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+							__builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+	if (miss) {
+		a.miss_idx[base + rank] = i;
+		a.miss_src[base + rank] = src;
+	}
 }
 
 struct Plan {
@@ -370,7 +403,7 @@ struct Plan {
 /* nat64_handle_v6 (nat64_kern.c:741-873) */
 __device__ uint32_t handle_v6(const Row &R, uint32_t len, int l3,
 			      const Nat64Args &a, const Tables &T, Plan &P,
-			      int64_t &shift)
+			      int64_t &shift, uint32_t ovv, uint4 &srcw)
 {
 	if ((uint32_t)l3 + 40 > len || (R.b(l3) >> 4) != 6)
 		return XDPGPU_TC_ACT_OK;          /* parse_ip6hdr */
@@ -431,10 +464,20 @@ __device__ uint32_t handle_v6(const Row &R, uint32_t len, int l3,
 	for (int k = 0; k < 4; k++)
 		w[k] = R.b(l3 + 8 + 4 * k) | R.b(l3 + 9 + 4 * k) << 8 |
 		       R.b(l3 + 10 + 4 * k) << 16 | R.b(l3 + 11 + 4 * k) << 24;
-	bool found;
-	const uint32_t src = lookup_v6(T, w, found);
-	if (!found)
-		return XDPGPU_NAT64_NO_STATE;
+	/* the state: from the table, or (commit pass) the host's decision */
+	uint32_t src;
+	if (a.ov) {
+		if (!ovv)
+			return XDPGPU_TC_ACT_SHOT;    /* alloc_new_state failed */
+		src = ovv;
+	} else {
+		bool found;
+		src = lookup_v6(T, w, found);
+		if (!found) {
+			srcw = make_uint4(w[0], w[1], w[2], w[3]);
+			return XDPGPU_NAT64_NO_STATE;
+		}
+	}
 
 	/* the original IPv6 header, kept for the checksum updates */
 	uint8_t v6[40];
@@ -602,7 +645,7 @@ __global__ __launch_bounds__(kBlockN) void xdp_nat64_kernel(Nat64Args a)
 	uint32_t *rows = rows_all + wid * kWaveN * kRowDw;
 	uint64_t *dtab = dtab_all + wid * kWaveN;
 	uint8_t *rb = reinterpret_cast<uint8_t *>(rows + lane * kRowDw);
-	const Tables T = {a.v6map, a.v6nb, a.v4map, a.v4nb};
+	const Tables T = {a.v6map, a.v6nb, a.v4map, a.v4nb, a.dyn, a.now, a.thr};
 	const uint64_t us16 = (a.usize + 15) & ~15ull;
 
 	/* work: every frame (a.xlist null) or the fast kernel's slow-frame
@@ -613,6 +656,7 @@ __global__ __launch_bounds__(kBlockN) void xdp_nat64_kernel(Nat64Args a)
 	for (uint64_t t = (uint64_t)blockIdx.x * kWavesN + wid; t < nitems; t += nwaves) {
 		uint64_t i;
 		bool active;
+		uint32_t ovv = 0;
 		if (a.xlist) {
 			const uint32_t r = (uint32_t)(t % a.nregions);
 			const uint32_t b = (uint32_t)(t / a.nregions) * kWaveN;
@@ -620,7 +664,10 @@ __global__ __launch_bounds__(kBlockN) void xdp_nat64_kernel(Nat64Args a)
 			if (b >= cnt)
 				continue;
 			active = b + lane < cnt;
-			i = active ? a.xlist[(uint64_t)r * a.xregion + b + lane] : 0;
+			const uint64_t li = (uint64_t)r * a.xregion + b + lane;
+			i = active ? a.xlist[li] : 0;
+			if (a.ov && active)
+				ovv = a.ov[li];
 		} else {
 			i = t * kWaveN + lane;
 			active = i < a.n;
@@ -665,6 +712,7 @@ __global__ __launch_bounds__(kBlockN) void xdp_nat64_kernel(Nat64Args a)
 		uint32_t act = valid ? XDPGPU_TC_ACT_OK : XDPGPU_TC_ACT_SHOT;
 		Plan P = {0, 0, -1};
 		int64_t shift = 0;
+		uint4 srcw = make_uint4(0, 0, 0, 0);
 		if (valid && len >= 14) {
 			/* parse_ethhdr (parsing_helpers.h:86-137) */
 			int l3 = 14;
@@ -680,8 +728,11 @@ __global__ __launch_bounds__(kBlockN) void xdp_nat64_kernel(Nat64Args a)
 			if (a.cfg.direction == XDPGPU_NAT64_EGRESS && proto == 0x0800)
 				act = handle_v4(R, len, l3, eff, a, T, P, shift);
 			else if (a.cfg.direction == XDPGPU_NAT64_INGRESS && proto == 0x86DD)
-				act = handle_v6(R, len, l3, a, T, P, shift);
+				act = handle_v6(R, len, l3, a, T, P, shift, ovv, srcw);
 		}
+		if (a.dyn && !a.ov)
+			miss_append(a, active && act == XDPGPU_NAT64_NO_STATE, (uint32_t)i, srcw,
+				    lane);
 
 		/* write back the rewritten span [P.lo, P.hi) of the row (the
 		 * translated frame ends where the original did) and the TCP
@@ -748,7 +799,7 @@ __device__ __forceinline__ void ingress_tile(const Nat64Args &a, const Tables &T
 					     const uint32_t (&F)[16], uint64_t eff,
 					     uint32_t len, bool valid, bool staged,
 					     uint4 *obuf, uint64_t *otab, int lane,
-					     uint32_t &act, bool &slow, bool &xlate)
+					     uint32_t &act, bool &slow, bool &xlate, uint4 &srcw)
 {
 	const int osw = (lane >> 2) & 3;
 	/* classification (nat64_handler, nat64_handle_v6 order) */
@@ -819,6 +870,7 @@ __device__ __forceinline__ void ingress_tile(const Nat64Args &a, const Tables &T
 		if (!found) {
 			xlate = false;
 			act = XDPGPU_NAT64_NO_STATE;
+			srcw = make_uint4(s[0], s[1], s[2], s[3]);
 		} else {
 			act = XDPGPU_TC_ACT_REDIRECT;
 		}
@@ -1064,7 +1116,7 @@ __global__ __launch_bounds__(kCuBlockN, 1) void xdp_nat64_fast_kernel(Nat64Args 
 	uint32_t *xq = xq_all + wid * 2 * kWaveN;
 	uint4 *obuf = obuf_all + wid * 4 * kWaveN;
 	uint64_t *otab = otab_all + wid * kWaveN;
-	const Tables T = {a.v6map, a.v6nb, a.v4map, a.v4nb};
+	const Tables T = {a.v6map, a.v6nb, a.v4map, a.v4nb, a.dyn, a.now, a.thr};
 
 	if (threadIdx.x == 0)
 		ctl[0] = ctl[1] = 0;
@@ -1150,12 +1202,17 @@ __global__ __launch_bounds__(kCuBlockN, 1) void xdp_nat64_fast_kernel(Nat64Args 
 
 		uint32_t act;
 		bool slow, xlate;
-		if constexpr (EG)
+		if constexpr (EG) {
 			egress_tile(a, T, F, eff, len, valid, staged, obuf, otab, lane, act,
 				    slow, xlate);
-		else
+		} else {
+			uint4 srcw = make_uint4(0, 0, 0, 0);
 			ingress_tile(a, T, F, eff, len, valid, staged, obuf, otab, lane, act,
-				     slow, xlate);
+				     slow, xlate, srcw);
+			if (a.dyn)
+				miss_append(a, active && !slow && act == XDPGPU_NAT64_NO_STATE,
+					    (uint32_t)i, srcw, lane);
+		}
 
 		/* slow frames to the block's list */
 		{
@@ -1239,6 +1296,18 @@ uint32_t nat64_grid(uint32_t n, uint32_t max_blocks)
 hipError_t launch_nat64(const Nat64Args &a0, uint32_t max_blocks, hipStream_t stream)
 {
 	Nat64Args a = a0;
+	if (a.ov) {
+		/* the commit pass: the general kernel over the listed frames
+		 * (xlist, one region of xregion entries, its count in xcount) */
+		uint32_t sb = resident_n<xdp_nat64_kernel>();
+		if (sb > max_blocks)
+			sb = max_blocks;
+		const uint32_t need = (a.xregion / kWaveN + kWavesN - 1) / kWavesN;
+		if (sb > need)
+			sb = need ? need : 1u;
+		hipLaunchKernelGGL(xdp_nat64_kernel, dim3(sb), dim3(kBlockN), 0, stream, a);
+		return hipGetLastError();
+	}
 	if (a.fast) {
 		const uint32_t blocks = nat64_grid(a.n, max_blocks);
 		/* one slow-list region per block: its share of the tiles */
@@ -1269,6 +1338,43 @@ hipError_t launch_nat64(const Nat64Args &a0, uint32_t max_blocks, hipStream_t st
 		return hipSuccess;
 	hipLaunchKernelGGL(xdp_nat64_kernel, dim3((uint32_t)blocks), dim3(kBlockN), 0,
 			   stream, a);
+	return hipGetLastError();
+}
+
+/* The host's dynamic-state commit: changed slots and their buckets' meta
+ * words (all patches of one bucket carry its final meta). */
+__global__ void nat64_patch_kernel(Nat64V6Bucket *v6map, Nat64V4Bucket *v4map,
+				   const Nat64Patch *p, uint32_t np)
+{
+	const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+	if (k >= np)
+		return;
+	const Nat64Patch q = p[k];
+	if (q.table == 0) {
+		Nat64V6Bucket *B = v6map + q.bucket;
+		if (q.slot < 4) {
+			B->key[q.slot] = q.k6;
+			B->val[q.slot] = q.v4;
+			B->last_seen[q.slot] = q.last_seen;
+		}
+		B->meta = q.meta;
+	} else {
+		Nat64V4Bucket *B = v4map + q.bucket;
+		if (q.slot < 4) {
+			B->key[q.slot] = q.v4;
+			B->val[q.slot] = q.k6;
+		}
+		B->meta = q.meta;
+	}
+}
+
+hipError_t launch_nat64_patch(Nat64V6Bucket *v6map, Nat64V4Bucket *v4map,
+			      const Nat64Patch *p, uint32_t np, hipStream_t stream)
+{
+	if (!np)
+		return hipSuccess;
+	hipLaunchKernelGGL(nat64_patch_kernel, dim3((np + 255) / 256), dim3(256), 0, stream,
+			   v6map, v4map, p, np);
 	return hipGetLastError();
 }
 

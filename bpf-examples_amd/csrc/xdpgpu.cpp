@@ -25,6 +25,9 @@
 
 #include "xdpgpu.h"
 #include "xdpgpu_internal.h"
+#include "nat64_state.h"
+
+#include <time.h>
 
 using namespace xdpgpu;
 
@@ -96,7 +99,19 @@ struct xdpgpu_ctx {
 	xdpgpu_nat64_cfg ncfg;
 	Nat64V6Bucket *d_v6map = nullptr;
 	Nat64V4Bucket *d_v4map = nullptr;
-	uint32_t nb = 0;           /* buckets of each table */
+	uint32_t nb = 0;           /* buckets of each table (device copy) */
+	std::vector<xdpgpu_nat64_map> nstat;   /* the static entries */
+	Nat64State nst;            /* host copy and the dynamic allocator */
+	bool ndyn = false;         /* xdpgpu_nat64_dynamic */
+	uint64_t nclock = 0;       /* batch clock, 0: CLOCK_MONOTONIC */
+	/* dynamic state: the frames a batch lists, and the commit pass */
+	uint32_t *d_midx = nullptr;
+	uint4 *d_msrc = nullptr;
+	uint32_t *d_mcnt = nullptr;            /* [0] listed, [1] committed */
+	uint32_t *d_mov = nullptr;             /* [cap] order, then [cap] v4 */
+	uint64_t mcap = 0;
+	Nat64Patch *d_patch = nullptr;
+	uint64_t pcap = 0;
 	uint32_t tn = 0;
 	char err[256];
 };
@@ -254,6 +269,10 @@ void xdpgpu_fini(xdpgpu_ctx *ctx)
 		(void)hipFree(ctx->d_v6map);
 	if (ctx->d_v4map)
 		(void)hipFree(ctx->d_v4map);
+	for (void *p : {(void *)ctx->d_midx, (void *)ctx->d_msrc, (void *)ctx->d_mcnt,
+			(void *)ctx->d_mov, (void *)ctx->d_patch})
+		if (p)
+			(void)hipFree(p);
 	if (ctx->pinned)
 		(void)hipHostUnregister(ctx->h_umem);
 	delete ctx;
@@ -664,6 +683,31 @@ static uint32_t nat64_buckets(uint32_t n)
 	return n < 3 ? 1u : (n + 2) / 3;
 }
 
+/* (re)allocate the device tables for the host copy's size and upload it */
+static int nat64_upload(xdpgpu_ctx *ctx)
+{
+	const uint32_t nb = ctx->nst.buckets();
+	HIP_TRY(ctx, hipSetDevice(ctx->cfg.device));
+	if (nb != ctx->nb || !ctx->d_v6map) {
+		if (ctx->d_v6map)
+			(void)hipFree(ctx->d_v6map);
+		if (ctx->d_v4map)
+			(void)hipFree(ctx->d_v4map);
+		ctx->d_v6map = nullptr;
+		ctx->d_v4map = nullptr;
+		ctx->nb = 0;
+		if (hipMalloc(&ctx->d_v6map, (size_t)nb * sizeof(Nat64V6Bucket)) != hipSuccess ||
+		    hipMalloc(&ctx->d_v4map, (size_t)nb * sizeof(Nat64V4Bucket)) != hipSuccess)
+			return set_err(ctx, -ENOMEM, "nat64 tables of %u buckets", nb);
+		ctx->nb = nb;
+	}
+	HIP_TRY(ctx, hipMemcpy(ctx->d_v6map, ctx->nst.v6().data(),
+			       (size_t)nb * sizeof(Nat64V6Bucket), hipMemcpyHostToDevice));
+	HIP_TRY(ctx, hipMemcpy(ctx->d_v4map, ctx->nst.v4().data(),
+			       (size_t)nb * sizeof(Nat64V4Bucket), hipMemcpyHostToDevice));
+	return 0;
+}
+
 int xdpgpu_nat64_setup(xdpgpu_ctx *ctx, const xdpgpu_nat64_cfg *cfg,
 		       const xdpgpu_nat64_map *map, uint32_t nmap)
 {
@@ -675,63 +719,171 @@ int xdpgpu_nat64_setup(xdpgpu_ctx *ctx, const xdpgpu_nat64_cfg *cfg,
 	if (cfg->direction > XDPGPU_NAT64_EGRESS || cfg->allow_plen > 128 ||
 	    (cfg->v4_prefix & ~cfg->v4_mask) || nmap > (1u << 30))
 		return -EINVAL;
-	const uint32_t nb = nat64_buckets(nmap);
-	std::vector<Nat64V6Bucket> v6t(nb);
-	std::vector<Nat64V4Bucket> v4t(nb);
-	memset(v6t.data(), 0, nb * sizeof(Nat64V6Bucket));
-	memset(v4t.data(), 0, nb * sizeof(Nat64V4Bucket));
-	for (uint32_t e = 0; e < nmap; e++) {
-		uint32_t w[4];
-		memcpy(w, map[e].v6, 16);
-		/* a repeated key keeps the last value, as a map update would */
-		uint32_t b = nat64_home(nat64_slot_hash(w[0], w[1], w[2], w[3]), nb);
-		for (;;) {
-			Nat64V6Bucket &B = v6t[b];
-			uint32_t j = 0;
-			while (j < B.n && !(B.key[j].x == w[0] && B.key[j].y == w[1] &&
-					    B.key[j].z == w[2] && B.key[j].w == w[3]))
-				j++;
-			if (j < 4) {
-				B.key[j] = make_uint4(w[0], w[1], w[2], w[3]);
-				B.val[j] = map[e].v4;
-				B.n = std::max(B.n, j + 1);
-				break;
-			}
-			b = b + 1 == nb ? 0 : b + 1;
-		}
-		b = nat64_home(nat64_slot_hash(map[e].v4, 0, 0, 0), nb);
-		for (;;) {
-			Nat64V4Bucket &B = v4t[b];
-			uint32_t j = 0;
-			while (j < B.n && B.key[j] != map[e].v4)
-				j++;
-			if (j < 4) {
-				B.key[j] = map[e].v4;
-				B.val[j] = make_uint4(w[0], w[1], w[2], w[3]);
-				B.n = std::max(B.n, j + 1);
-				break;
-			}
-			b = b + 1 == nb ? 0 : b + 1;
-		}
-	}
-	HIP_TRY(ctx, hipSetDevice(ctx->cfg.device));
-	if (ctx->d_v6map)
-		(void)hipFree(ctx->d_v6map);
-	if (ctx->d_v4map)
-		(void)hipFree(ctx->d_v4map);
-	ctx->d_v6map = nullptr;
-	ctx->d_v4map = nullptr;
 	ctx->nat64 = false;
-	if (hipMalloc(&ctx->d_v6map, nb * sizeof(Nat64V6Bucket)) != hipSuccess ||
-	    hipMalloc(&ctx->d_v4map, nb * sizeof(Nat64V4Bucket)) != hipSuccess)
-		return set_err(ctx, -ENOMEM, "nat64 tables of %u buckets", nb);
-	HIP_TRY(ctx, hipMemcpy(ctx->d_v6map, v6t.data(), nb * sizeof(Nat64V6Bucket),
-			       hipMemcpyHostToDevice));
-	HIP_TRY(ctx, hipMemcpy(ctx->d_v4map, v4t.data(), nb * sizeof(Nat64V4Bucket),
-			       hipMemcpyHostToDevice));
-	ctx->nb = nb;
+	ctx->ndyn = false;
+	ctx->nstat.assign(map, map + nmap);
+	ctx->nst.v4_prefix = cfg->v4_prefix;
+	ctx->nst.v4_mask = cfg->v4_mask;
+	ctx->nst.cap = 0;
+	ctx->nst.build(ctx->nstat, nat64_buckets(nmap));
+	const int rc = nat64_upload(ctx);
+	if (rc)
+		return rc;
 	ctx->ncfg = *cfg;
 	ctx->nat64 = true;
+	return 0;
+}
+
+int xdpgpu_nat64_dynamic(xdpgpu_ctx *ctx, const xdpgpu_nat64_dyn *dyn)
+{
+	if (!ctx)
+		return -EINVAL;
+	if (!ctx->nat64)
+		return set_err(ctx, -EINVAL, "xdpgpu_nat64_setup not called");
+	uint32_t cap = 0;
+	if (dyn) {
+		/* num_addr (nat64.c:396), the size of all three maps */
+		const uint32_t top = ctx->ncfg.v4_prefix | ~ctx->ncfg.v4_mask;
+		if (~ctx->ncfg.v4_mask < 3)
+			return set_err(ctx, -EINVAL, "v4 pool %#x/%#x has no dynamic addresses",
+				       ctx->ncfg.v4_prefix, ctx->ncfg.v4_mask);
+		cap = top - ctx->ncfg.v4_prefix - 2;
+		if (cap > (1u << 26))
+			return set_err(ctx, -E2BIG, "v4 pool of %u addresses", cap);
+	}
+	ctx->nat64 = false;
+	ctx->nst.cap = cap;
+	ctx->nst.timeout_ns = dyn ? dyn->timeout_ns : 0;
+	ctx->nst.next_addr = dyn ? dyn->next_addr : 1;
+	ctx->nclock = dyn ? dyn->now_ns : 0;
+	const uint32_t nmap = (uint32_t)ctx->nstat.size();
+	ctx->nst.build(ctx->nstat, nat64_buckets(std::max(nmap, cap)));
+	const int rc = nat64_upload(ctx);
+	if (rc)
+		return rc;
+	ctx->ndyn = dyn != nullptr;
+	ctx->nat64 = true;
+	return 0;
+}
+
+int xdpgpu_nat64_clock(xdpgpu_ctx *ctx, uint64_t now_ns)
+{
+	if (!ctx)
+		return -EINVAL;
+	ctx->nclock = now_ns;
+	return 0;
+}
+
+int xdpgpu_nat64_direction(xdpgpu_ctx *ctx, uint32_t direction)
+{
+	if (!ctx || direction > XDPGPU_NAT64_EGRESS)
+		return -EINVAL;
+	if (!ctx->nat64)
+		return set_err(ctx, -EINVAL, "xdpgpu_nat64_setup not called");
+	ctx->ncfg.direction = direction;
+	return 0;
+}
+
+static int nat64_devtab(xdpgpu_ctx *ctx, std::vector<Nat64V6Bucket> &out)
+{
+	out.resize(ctx->nb);
+	HIP_TRY(ctx, hipMemcpy(out.data(), ctx->d_v6map, (size_t)ctx->nb * sizeof(Nat64V6Bucket),
+			       hipMemcpyDeviceToHost));
+	return 0;
+}
+
+int xdpgpu_nat64_state(xdpgpu_ctx *ctx, xdpgpu_nat64_entry *out, uint32_t max, uint32_t *n,
+		       xdpgpu_nat64_dyn *dyn, uint32_t *queue, uint32_t qmax, uint32_t *nq)
+{
+	if (!ctx || (max && !out) || (qmax && !queue))
+		return -EINVAL;
+	if (!ctx->nat64)
+		return set_err(ctx, -EINVAL, "xdpgpu_nat64_setup not called");
+	HIP_TRY(ctx, hipSetDevice(ctx->cfg.device));
+	for (uint32_t i = 0; i < kSlots; i++)
+		HIP_TRY(ctx, hipStreamSynchronize(ctx->slot[i].stream));
+	std::vector<Nat64V6Bucket> dev;
+	int rc = nat64_devtab(ctx, dev);
+	if (rc)
+		return rc;
+	std::vector<xdpgpu_nat64_entry> all;
+	ctx->nst.entries(all, &dev);
+	if (n)
+		*n = (uint32_t)all.size();
+	for (uint32_t k = 0; k < max && k < all.size(); k++)
+		out[k] = all[k];
+	if (dyn) {
+		memset(dyn, 0, sizeof(*dyn));
+		dyn->timeout_ns = ctx->nst.timeout_ns;
+		dyn->next_addr = ctx->nst.next_addr;
+		dyn->now_ns = ctx->nclock;
+	}
+	const std::deque<uint32_t> &q = ctx->nst.queue();
+	if (nq)
+		*nq = (uint32_t)q.size();
+	for (uint32_t k = 0; k < qmax && k < q.size(); k++)
+		queue[k] = q[k];
+	return 0;
+}
+
+/* the dynamic-state commit of one ingress batch (see xdpgpu.h): the
+ * frames the kernels listed, in frame order through alloc_new_state on the
+ * host, the changed table slots to the device, then the listed frames
+ * again through the general kernel with their addresses */
+static int nat64_commit(xdpgpu_ctx *ctx, Nat64Args a, uint64_t now, hipStream_t st)
+{
+	uint32_t m = 0;
+	HIP_TRY(ctx, hipMemcpyAsync(&m, ctx->d_mcnt, 4, hipMemcpyDeviceToHost, st));
+	HIP_TRY(ctx, hipStreamSynchronize(st));
+	if (!m)
+		return 0;
+	if (m > a.n)
+		return set_err(ctx, -EIO, "nat64: %u listed frames in a batch of %u", m, a.n);
+	std::vector<uint32_t> idx(m);
+	std::vector<uint4> src(m);
+	HIP_TRY(ctx, hipMemcpyAsync(idx.data(), ctx->d_midx, (size_t)m * 4,
+				    hipMemcpyDeviceToHost, st));
+	HIP_TRY(ctx, hipMemcpyAsync(src.data(), ctx->d_msrc, (size_t)m * 16,
+				    hipMemcpyDeviceToHost, st));
+	HIP_TRY(ctx, hipStreamSynchronize(st));
+	std::vector<uint32_t> sidx, ov;
+	std::vector<Nat64Patch> patches;
+	int err = 0;
+	ctx->nst.commit(idx.data(), src.data(), m, now,
+			[ctx](std::vector<Nat64V6Bucket> &t) { return nat64_devtab(ctx, t); },
+			sidx, ov, patches, err);
+	if (err)
+		return err;
+	if (patches.size() > ctx->pcap) {
+		if (ctx->d_patch)
+			(void)hipFree(ctx->d_patch);
+		ctx->d_patch = nullptr;
+		ctx->pcap = 0;
+		if (hipMalloc(&ctx->d_patch, patches.size() * sizeof(Nat64Patch)) != hipSuccess)
+			return set_err(ctx, -ENOMEM, "nat64 patches");
+		ctx->pcap = patches.size();
+	}
+	const uint32_t reg = (m + 63) & ~63u;
+	/* stream-ordered; the host vectors live until the final synchronize */
+	if (!patches.empty())
+		HIP_TRY(ctx, hipMemcpyAsync(ctx->d_patch, patches.data(),
+					    patches.size() * sizeof(Nat64Patch),
+					    hipMemcpyHostToDevice, st));
+	HIP_TRY(ctx, hipMemcpyAsync(ctx->d_mov, sidx.data(), (size_t)m * 4,
+				    hipMemcpyHostToDevice, st));
+	HIP_TRY(ctx, hipMemcpyAsync(ctx->d_mov + ctx->mcap, ov.data(), (size_t)m * 4,
+				    hipMemcpyHostToDevice, st));
+	HIP_TRY(ctx, hipMemcpyAsync(ctx->d_mcnt + 1, &m, 4, hipMemcpyHostToDevice, st));
+	HIP_TRY(ctx, launch_nat64_patch(ctx->d_v6map, ctx->d_v4map, ctx->d_patch,
+					(uint32_t)patches.size(), st));
+	a.fast = 0;
+	a.xlist = ctx->d_mov;
+	a.xcount = ctx->d_mcnt + 1;
+	a.nregions = 1;
+	a.xregion = reg;
+	a.ov = ctx->d_mov + ctx->mcap;
+	HIP_TRY(ctx, launch_nat64(a, ctx->max_blocks, st));
+	HIP_TRY(ctx, hipStreamSynchronize(st));
 	return 0;
 }
 
@@ -756,6 +908,41 @@ int xdpgpu_nat64_dev(xdpgpu_ctx *ctx, void *d_umem, uint64_t umem_size,
 	a.cfg = ctx->ncfg;
 	a.v6map = ctx->d_v6map;
 	a.v6nb = ctx->nb;
+	const bool dyn = ctx->ndyn && ctx->ncfg.direction == XDPGPU_NAT64_INGRESS;
+	uint64_t now = 0;
+	if (dyn) {
+		/* one instant per batch (bpf_ktime_get_ns, CLOCK_MONOTONIC) */
+		now = ctx->nclock;
+		if (!now) {
+			struct timespec ts;
+			clock_gettime(CLOCK_MONOTONIC, &ts);
+			now = (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+		}
+		if (n > ctx->mcap) {
+			for (void *p : {(void *)ctx->d_midx, (void *)ctx->d_msrc,
+					(void *)ctx->d_mov})
+				if (p)
+					(void)hipFree(p);
+			ctx->d_midx = nullptr;
+			ctx->d_msrc = nullptr;
+			ctx->d_mov = nullptr;
+			ctx->mcap = 0;
+			const uint64_t cap = ((uint64_t)n + 63) & ~63ull;
+			if (hipMalloc(&ctx->d_midx, cap * 4) != hipSuccess ||
+			    hipMalloc(&ctx->d_msrc, cap * 16) != hipSuccess ||
+			    hipMalloc(&ctx->d_mov, cap * 8) != hipSuccess)
+				return set_err(ctx, -ENOMEM, "nat64 miss lists of %u", n);
+			ctx->mcap = cap;
+		}
+		if (!ctx->d_mcnt && hipMalloc(&ctx->d_mcnt, 16) != hipSuccess)
+			return set_err(ctx, -ENOMEM, "nat64 miss count");
+		a.dyn = 1;
+		a.now = now;
+		a.thr = now - ctx->nst.timeout_ns;
+		a.miss_idx = ctx->d_midx;
+		a.miss_src = ctx->d_msrc;
+		a.miss_cnt = ctx->d_mcnt;
+	}
 	a.v4map = ctx->d_v4map;
 	a.v4nb = ctx->nb;
 	/* the fast kernels cover both directions under a /96 prefix; they
@@ -784,15 +971,20 @@ int xdpgpu_nat64_dev(xdpgpu_ctx *ctx, void *d_umem, uint64_t umem_size,
 		memcpy(a.pref_w, ctx->ncfg.v6_prefix, 12);
 	}
 	hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
+	if (dyn)
+		HIP_TRY(ctx, hipMemsetAsync(ctx->d_mcnt, 0, 16, st));
 	if (!a.fast) {
 		HIP_TRY(ctx, launch_nat64(a, ctx->max_blocks, st));
-		return 0;
+		return dyn ? nat64_commit(ctx, a, now, st) : 0;
 	}
 	int rc = scratch_enter(ctx, ctx->slot[0], st);
 	if (rc)
 		return rc;
 	HIP_TRY(ctx, launch_nat64(a, ctx->max_blocks, st));
-	return scratch_leave(ctx, ctx->slot[0], st);
+	rc = scratch_leave(ctx, ctx->slot[0], st);
+	if (rc)
+		return rc;
+	return dyn ? nat64_commit(ctx, a, now, st) : 0;
 }
 
 int xdpgpu_ceiling_dev(xdpgpu_ctx *ctx, const void *d_umem, uint64_t umem_size,

@@ -208,19 +208,24 @@ struct EchoArgs {
 };
 hipError_t launch_echo_writeback(const EchoArgs &a, hipStream_t stream);
 
-/* nat64 static tables (v6_state_map and v4_reversemap, nat64_kern.c:17-46):
+/* nat64 state tables (v6_state_map and v4_reversemap, nat64_kern.c:17-46):
  * 4-way buckets of one 128-byte line, so a lookup touches one line; the
  * home bucket is fastrange(nat64_slot_hash(key), nbuckets), a full bucket
- * overflows into the next (linear probing over buckets). */
+ * overflows into the next (linear probing over buckets).  `meta`: bits 0-3
+ * the slots in use, bit 4 an entry of an earlier home bucket lies further
+ * on (probing continues past this bucket), bits 8-11 static_conf of the
+ * slots (v6 table).  Deleting an entry clears its use bit only. */
+constexpr uint32_t kNat64Ovf = 0x10;
 struct Nat64V6Bucket {
 	uint4 key[4];              /* IPv6 address words as stored          */
 	uint32_t val[4];           /* IPv4 address, host order              */
-	uint32_t n;                /* slots used (0..4)                     */
-	uint32_t pad[11];
+	uint32_t meta;
+	uint32_t pad[3];
+	unsigned long long last_seen[4];  /* v6_addr_state.last_seen (ns)   */
 };
 struct Nat64V4Bucket {
 	uint32_t key[4];           /* IPv4 address, host order              */
-	uint32_t n;
+	uint32_t meta;
 	uint32_t pad[3];
 	uint4 val[4];              /* IPv6 address words                    */
 	uint4 pad2[2];
@@ -233,6 +238,18 @@ __host__ __device__ inline uint32_t nat64_home(uint32_t h, uint32_t nbuckets)
 	return (uint32_t)(((uint64_t)h * nbuckets) >> 32);
 }
 
+/* One slot of a table written by the host after a dynamic-state commit
+ * (nat64_patch_kernel): table 0 v6 (key k6, value v4, last_seen), 1 v4
+ * (key v4, value k6); the bucket's meta word in both. */
+struct Nat64Patch {
+	uint32_t table, bucket, slot, meta;
+	uint4 k6;
+	uint32_t v4, pad;
+	unsigned long long last_seen;
+	uint4 pad2;
+};
+static_assert(sizeof(Nat64Patch) == 64, "patch record");
+
 struct Nat64Args {
 	uint8_t *umem;
 	uint64_t usize;
@@ -241,7 +258,7 @@ struct Nat64Args {
 	uint8_t *action;
 	xdpgpu_desc *out;
 	xdpgpu_nat64_cfg cfg;
-	const Nat64V6Bucket *v6map;
+	Nat64V6Bucket *v6map;
 	uint32_t v6nb;             /* buckets */
 	const Nat64V4Bucket *v4map;
 	uint32_t v4nb;
@@ -254,10 +271,24 @@ struct Nat64Args {
 	uint32_t *xlist;           /* slow frames, xregion per fast wave    */
 	uint32_t *xcount;
 	uint32_t xregion, nregions;
+	/* dynamic state (xdpgpu_nat64_dynamic): a hit stamps last_seen with
+	 * the batch clock `now`; a miss, or a hit on an entry that timed out
+	 * (last_seen < thr, not static), is left untouched and listed for the
+	 * host's in-order commit (miss_idx / miss_src, count in miss_cnt) */
+	uint32_t dyn;
+	unsigned long long now, thr;
+	uint32_t *miss_idx;
+	uint4 *miss_src;
+	uint32_t *miss_cnt;
+	/* the commit's second pass: xlist is the listed frames in order, ov
+	 * the IPv4 address each was given (0: SHOT), no table lookup */
+	const uint32_t *ov;
 };
 
 hipError_t launch_nat64(const Nat64Args &a, uint32_t max_blocks,
 			hipStream_t stream);
+hipError_t launch_nat64_patch(Nat64V6Bucket *v6map, Nat64V4Bucket *v4map,
+			      const Nat64Patch *p, uint32_t np, hipStream_t stream);
 uint32_t nat64_slot_hash(uint32_t a, uint32_t b, uint32_t c, uint32_t d);
 
 hipError_t launch_hints(const uint8_t *umem, uint64_t usize,

@@ -59,6 +59,8 @@ NAT64_INGRESS, NAT64_EGRESS = 0, 1
 TC_ACT_OK, TC_ACT_SHOT, TC_ACT_REDIRECT = 0, 2, 7
 NAT64_NO_STATE = 0x80
 NAT64_MAP_DTYPE = np.dtype([("v6", "u1", (16,)), ("v4", "<u4"), ("rsvd", "<u4")])
+NAT64_ENTRY_DTYPE = np.dtype([("v6", "u1", (16,)), ("v4", "<u4"), ("static_conf", "<u4"),
+                              ("last_seen", "<u8")])
 UMEM_UNALIGNED_CHUNK_FLAG = 1
 
 DESC_DTYPE = np.dtype([("addr", "<u8"), ("len", "<u4"), ("options", "<u4")])
@@ -129,6 +131,12 @@ class Nat64Cfg(C.Structure):
                 ("direction", C.c_uint32), ("rsvd", C.c_uint32 * 3)]
 
 
+class Nat64Dyn(C.Structure):
+    """struct xdpgpu_nat64_dyn"""
+    _fields_ = [("timeout_ns", C.c_uint64), ("next_addr", C.c_uint64),
+                ("now_ns", C.c_uint64), ("rsvd", C.c_uint64)]
+
+
 class XdpGpuError(RuntimeError):
     pass
 
@@ -146,7 +154,8 @@ EXPORTS = (
     "xdpgpu_abi_version", "xdpgpu_pool_size", "xdpgpu_pool_generate",
     "xdpgpu_pool_spec_default", "xdpgpu_hints_dev", "xdpgpu_host_alloc",
     "xdpgpu_host_free", "xdpgpu_jhash2_dev", "xdpgpu_jhash_nwords_dev",
-    "xdpgpu_queue_stats",
+    "xdpgpu_queue_stats", "xdpgpu_nat64_dynamic", "xdpgpu_nat64_clock",
+    "xdpgpu_nat64_state", "xdpgpu_nat64_direction",
 )
 
 # struct xdpgpu_hints (XDP hints in front of a frame)
@@ -185,6 +194,11 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.xdpgpu_nat64_setup.argtypes = [vp, C.POINTER(Nat64Cfg), vp, u32]
     lib.xdpgpu_nat64_dev.argtypes = [vp, vp, u64, vp, u32, vp, vp, vp]
     lib.xdpgpu_nat64_pool_config.argtypes = [u32, C.POINTER(Nat64Cfg), vp, u32]
+    lib.xdpgpu_nat64_dynamic.argtypes = [vp, C.POINTER(Nat64Dyn)]
+    lib.xdpgpu_nat64_clock.argtypes = [vp, u64]
+    lib.xdpgpu_nat64_direction.argtypes = [vp, u32]
+    lib.xdpgpu_nat64_state.argtypes = [vp, vp, u32, C.POINTER(u32), C.POINTER(Nat64Dyn),
+                                       vp, u32, C.POINTER(u32)]
     lib.xdpgpu_device_count.argtypes = []
     lib.xdpgpu_last_error.argtypes = [vp]
     lib.xdpgpu_last_error.restype = C.c_char_p
@@ -364,6 +378,36 @@ class XdpGpu:
         self._check(self.lib.xdpgpu_nat64_dev(
             self.h, _ptr(umem), umem_size, _ptr(descs), n, _ptr(action),
             _ptr(out), _stream_handle(stream)), "xdpgpu_nat64_dev")
+
+    def nat64_dynamic(self, timeout_ns: Optional[int] = None, next_addr: int = 1,
+                      now_ns: int = 0) -> None:
+        """Dynamic state on (alloc_new_state) or, with timeout_ns None, off."""
+        if timeout_ns is None:
+            self._check(self.lib.xdpgpu_nat64_dynamic(self.h, None), "xdpgpu_nat64_dynamic")
+            return
+        d = Nat64Dyn(timeout_ns, next_addr, now_ns, 0)
+        self._check(self.lib.xdpgpu_nat64_dynamic(self.h, C.byref(d)), "xdpgpu_nat64_dynamic")
+
+    def nat64_clock(self, now_ns: int) -> None:
+        self._check(self.lib.xdpgpu_nat64_clock(self.h, now_ns), "xdpgpu_nat64_clock")
+
+    def nat64_direction(self, direction: int) -> None:
+        self._check(self.lib.xdpgpu_nat64_direction(self.h, direction),
+                    "xdpgpu_nat64_direction")
+
+    def nat64_state(self):
+        """(entries in insertion order as NAT64_ENTRY_DTYPE, next_addr,
+        reclaim queue oldest first)."""
+        n, nq = C.c_uint32(0), C.c_uint32(0)
+        d = Nat64Dyn()
+        self._check(self.lib.xdpgpu_nat64_state(self.h, None, 0, C.byref(n), C.byref(d),
+                                                None, 0, C.byref(nq)), "xdpgpu_nat64_state")
+        ent = np.zeros(n.value, NAT64_ENTRY_DTYPE)
+        q = np.zeros(nq.value, np.uint32)
+        self._check(self.lib.xdpgpu_nat64_state(
+            self.h, ent.ctypes.data if n.value else None, n.value, C.byref(n), C.byref(d),
+            q.ctypes.data if nq.value else None, nq.value, C.byref(nq)), "xdpgpu_nat64_state")
+        return ent, int(d.next_addr), q
 
     def ceiling_dev(self, umem, umem_size: int, descs, n: int, verdict, res,
                     tup, stream=None) -> None:

@@ -319,9 +319,9 @@ int xdpgpu_abi_version(void);
 #define XDPGPU_TC_ACT_OK       0  /* not for the translator: untouched   */
 #define XDPGPU_TC_ACT_SHOT     2  /* in the prefix but not translatable  */
 #define XDPGPU_TC_ACT_REDIRECT 7  /* translated                          */
-/* An allowed IPv6 source with no mapping in the static table.  The
- * reference allocates one (alloc_new_state, nat64_kern.c:576-622); that
- * order-dependent allocation stays with the host: the frame is untouched. */
+/* An allowed IPv6 source with no mapping in the state table, when dynamic
+ * state is off (the frame is untouched; xdpgpu_nat64_dynamic turns on the
+ * reference's allocation, alloc_new_state, nat64_kern.c:576-622). */
 #define XDPGPU_NAT64_NO_STATE  0x80
 
 /* struct nat64_config (nat64.h:6-12) plus the allowed_v6_src entry. */
@@ -361,6 +361,52 @@ int xdpgpu_nat64_setup(struct xdpgpu_ctx *ctx,
 int xdpgpu_nat64_dev(struct xdpgpu_ctx *ctx, void *d_umem, uint64_t umem_size,
 		     const struct xdpgpu_desc *d_descs, uint32_t n,
 		     uint8_t *d_action, struct xdpgpu_desc *d_out, void *stream);
+
+/* Dynamic state: v6_state_map entries made on first sight of an allowed
+ * source (alloc_new_state, nat64_kern.c:576-622): the next address of the
+ * v4 pool (config.next_addr) while prefix + next_addr < (prefix | ~mask) - 1,
+ * then reclaimed addresses (reclaim_v4_addr, :563-574: the reclaimed_addrs
+ * queue, else one entry whose last_seen is older than now - timeout_ns and
+ * not static, found in insertion order), within num_addr = (prefix | ~mask)
+ * - prefix - 2 entries (nat64.c:396-401); a hit refreshes last_seen
+ * (:821-823).  A failed allocation is TC_ACT_SHOT.  Frames are taken in
+ * descriptor order, one batch at one instant: `now_ns`, or CLOCK_MONOTONIC
+ * read once per xdpgpu_nat64_dev call when 0 (bpf_ktime_get_ns()).  With
+ * dynamic state xdpgpu_nat64_dev returns after the batch has completed: the
+ * frames that need a new or timed-out entry are committed in order on the
+ * host and translated in a second pass. */
+struct xdpgpu_nat64_dyn {
+	uint64_t timeout_ns;       /* config.timeout_ns; nat64.c: 7200 s     */
+	uint64_t next_addr;        /* config.next_addr; nat64.c: 1           */
+	uint64_t now_ns;           /* the batch clock, 0: CLOCK_MONOTONIC    */
+	uint64_t rsvd;
+};
+
+/* One v6_state_map entry (struct v6_addr_state, nat64.h:15-19, with its key). */
+struct xdpgpu_nat64_entry {
+	uint8_t  v6[16];
+	uint32_t v4;               /* host byte order                        */
+	uint32_t static_conf;
+	uint64_t last_seen;
+};
+
+/* Turn dynamic state on (dyn) or off (NULL), after xdpgpu_nat64_setup: the
+ * tables are rebuilt from the static entries, sized for num_addr entries,
+ * and the reclaim queue is emptied. */
+int xdpgpu_nat64_dynamic(struct xdpgpu_ctx *ctx, const struct xdpgpu_nat64_dyn *dyn);
+/* Set the batch clock for the following calls (0: CLOCK_MONOTONIC). */
+int xdpgpu_nat64_clock(struct xdpgpu_ctx *ctx, uint64_t now_ns);
+/* Switch the direction of the following calls, keeping the tables: the
+ * reference's nat64_ingress and nat64_egress programs share their maps
+ * (nat64_kern.c:875-902); egress reads v4_reversemap only. */
+int xdpgpu_nat64_direction(struct xdpgpu_ctx *ctx, uint32_t direction);
+/* Read the state: up to max entries in insertion order (*n: how many there
+ * are), the dynamic configuration with the current next_addr (dyn, may be
+ * NULL) and up to qmax reclaim-queue addresses, oldest first (*nq: how
+ * many there are; queue may be NULL). */
+int xdpgpu_nat64_state(struct xdpgpu_ctx *ctx, struct xdpgpu_nat64_entry *out,
+		       uint32_t max, uint32_t *n, struct xdpgpu_nat64_dyn *dyn,
+		       uint32_t *queue, uint32_t qmax, uint32_t *nq);
 
 /* ------------------------------------------------------------------ */
 /* Synthetic UMEM pool generator (host).  Replaces the reference's packet

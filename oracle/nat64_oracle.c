@@ -25,6 +25,7 @@
  * kernel-helper boundary).
  */
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "oracle.h"
@@ -131,6 +132,276 @@ static const struct xdpgpu_nat64_map *find_v4(const struct xdpgpu_nat64_map *map
 }
 
 /* allowed_v6_src: an LPM trie with the one configured entry */
+/* ------------------------------------------------------------------ */
+/* Dynamic state (nat64_kern.c:543-622): v6_state_map, v4_reversemap and
+ * reclaimed_addrs as plain arrays, searched linearly (test sizes).  The
+ * reference walks v6_state_map in its kernel hash order when it reclaims;
+ * this restatement (and the build) walk insertion order. */
+struct ent6 {
+	uint8_t v6[16];
+	uint32_t v4, static_conf, alive;
+	uint64_t last_seen;
+};
+struct ent4 {
+	uint32_t v4, alive;
+	uint8_t v6[16];
+};
+struct oracle_nat64_state {
+	uint64_t timeout_ns, next_addr;
+	uint32_t v4_prefix, v4_mask, cap;
+	uint32_t n6, n4, max6, max4, count;   /* count: live v6 entries */
+	struct ent6 *e6;
+	struct ent4 *e4;
+	uint32_t *queue, qhead, qlen;          /* ring of cap entries */
+};
+
+static struct ent6 *st_find6(struct oracle_nat64_state *st, const uint8_t *v6)
+{
+	for (uint32_t i = 0; i < st->n6; i++)
+		if (st->e6[i].alive && !memcmp(st->e6[i].v6, v6, 16))
+			return &st->e6[i];
+	return NULL;
+}
+
+static struct ent4 *st_find4(struct oracle_nat64_state *st, uint32_t v4)
+{
+	for (uint32_t i = 0; i < st->n4; i++)
+		if (st->e4[i].alive && st->e4[i].v4 == v4)
+			return &st->e4[i];
+	return NULL;
+}
+
+static int st_grow(void **p, uint32_t *max, uint32_t need, size_t sz)
+{
+	if (need <= *max)
+		return 0;
+	uint32_t m = *max ? *max : 64;
+	while (m < need)
+		m *= 2;
+	void *q = realloc(*p, (size_t)m * sz);
+	if (!q)
+		return -1;
+	*p = q;
+	*max = m;
+	return 0;
+}
+
+/* a map update: an existing key keeps its place and takes the value */
+static struct ent6 *st_put6(struct oracle_nat64_state *st, const uint8_t *v6, uint32_t v4,
+			    uint32_t stat, uint64_t ls)
+{
+	struct ent6 *e = st_find6(st, v6);
+	if (!e) {
+		if (st_grow((void **)&st->e6, &st->max6, st->n6 + 1, sizeof(*e)))
+			return NULL;
+		e = &st->e6[st->n6++];
+		memcpy(e->v6, v6, 16);
+		e->alive = 1;
+		st->count++;
+	}
+	e->v4 = v4;
+	e->static_conf = stat;
+	e->last_seen = ls;
+	return e;
+}
+
+static void st_put4(struct oracle_nat64_state *st, uint32_t v4, const uint8_t *v6)
+{
+	struct ent4 *e = st_find4(st, v4);
+	if (!e) {
+		if (st_grow((void **)&st->e4, &st->max4, st->n4 + 1, sizeof(*e)))
+			return;
+		e = &st->e4[st->n4++];
+		e->v4 = v4;
+		e->alive = 1;
+	}
+	memcpy(e->v6, v6, 16);
+}
+
+static void st_del6(struct oracle_nat64_state *st, struct ent6 *e)
+{
+	e->alive = 0;
+	st->count--;
+}
+
+/* bpf_map_push_elem / pop_elem on the BPF_MAP_TYPE_QUEUE of num_addr */
+static void st_push(struct oracle_nat64_state *st, uint32_t v4)
+{
+	if (st->qlen < st->cap)
+		st->queue[(st->qhead + st->qlen++) % st->cap] = v4;
+}
+
+static int st_pop(struct oracle_nat64_state *st, uint32_t *v4)
+{
+	if (!st->qlen)
+		return -1;
+	*v4 = st->queue[st->qhead];
+	st->qhead = (st->qhead + 1) % st->cap;
+	st->qlen--;
+	return 0;
+}
+
+/* reclaim_v4_addr + check_item (nat64_kern.c:543-574) */
+static uint32_t st_reclaim(struct oracle_nat64_state *st, uint64_t now)
+{
+	const uint64_t timeout = now - st->timeout_ns;
+	uint32_t v4;
+
+	if (st_pop(st, &v4) == 0)
+		return v4;
+	for (uint32_t i = 0; i < st->n6; i++) {
+		struct ent6 *e = &st->e6[i];
+		if (e->alive && e->last_seen < timeout && !e->static_conf) {
+			const uint32_t a = e->v4;
+			struct ent4 *r = st_find4(st, a);
+			st_del6(st, e);
+			if (r)
+				r->alive = 0;
+			st_push(st, a);
+			break;          /* one address at a time */
+		}
+	}
+	return st_pop(st, &v4) ? 0 : v4;
+}
+
+/* alloc_new_state (nat64_kern.c:576-622), one thread: the CAS loop's first
+ * round decides */
+static struct ent6 *st_alloc(struct oracle_nat64_state *st, const uint8_t *v6, uint64_t now)
+{
+	const uint32_t max_v4 = (st->v4_prefix | ~st->v4_mask) - 1;
+	const uint32_t next_v4 = st->v4_prefix + (uint32_t)st->next_addr;
+	uint32_t src_v4;
+
+	if (next_v4 >= max_v4) {
+		src_v4 = st_reclaim(st, now);
+	} else {
+		st->next_addr++;
+		src_v4 = next_v4;
+	}
+	if (!src_v4)
+		return NULL;
+	if (st->count >= st->cap) {          /* v6_state_map full: -E2BIG */
+		st_push(st, src_v4);
+		return NULL;
+	}
+	struct ent6 *e = st_put6(st, v6, src_v4, 0, now);
+	if (!e)
+		return NULL;
+	if (st_find4(st, src_v4)) {          /* v4_reversemap NOEXIST fails */
+		st_del6(st, e);
+		st_push(st, src_v4);
+		return NULL;
+	}
+	st_put4(st, src_v4, v6);
+	return e;
+}
+
+struct oracle_nat64_state *oracle_nat64_state_new(const struct xdpgpu_nat64_cfg *cfg,
+						  const struct xdpgpu_nat64_map *map,
+						  uint32_t nmap, uint64_t timeout_ns,
+						  uint64_t next_addr)
+{
+	struct oracle_nat64_state *st = calloc(1, sizeof(*st));
+	if (!st)
+		return NULL;
+	st->timeout_ns = timeout_ns;
+	st->next_addr = next_addr;
+	st->v4_prefix = cfg->v4_prefix;
+	st->v4_mask = cfg->v4_mask;
+	/* num_addr (nat64.c:396) */
+	st->cap = (cfg->v4_prefix | ~cfg->v4_mask) - cfg->v4_prefix - 2;
+	st->queue = calloc(st->cap ? st->cap : 1, sizeof(uint32_t));
+	for (uint32_t i = 0; i < nmap; i++) {
+		st_put6(st, map[i].v6, map[i].v4, 1, 0);
+		st_put4(st, map[i].v4, map[i].v6);
+	}
+	return st;
+}
+
+void oracle_nat64_state_free(struct oracle_nat64_state *st)
+{
+	if (!st)
+		return;
+	free(st->e6);
+	free(st->e4);
+	free(st->queue);
+	free(st);
+}
+
+int oracle_nat64_state_read(const struct oracle_nat64_state *st,
+			    struct xdpgpu_nat64_entry *out, uint32_t max, uint32_t *n,
+			    uint64_t *next_addr, uint32_t *queue, uint32_t qmax, uint32_t *nq)
+{
+	uint32_t k = 0;
+	for (uint32_t i = 0; i < st->n6; i++) {
+		const struct ent6 *e = &st->e6[i];
+		if (!e->alive)
+			continue;
+		if (k < max) {
+			memset(&out[k], 0, sizeof(out[k]));
+			memcpy(out[k].v6, e->v6, 16);
+			out[k].v4 = e->v4;
+			out[k].static_conf = e->static_conf;
+			out[k].last_seen = e->last_seen;
+		}
+		k++;
+	}
+	*n = k;
+	*next_addr = st->next_addr;
+	for (uint32_t i = 0; i < st->qlen && i < qmax; i++)
+		queue[i] = st->queue[(st->qhead + i) % st->cap];
+	*nq = st->qlen;
+	return 0;
+}
+
+/* the tables one call sees: the static map, or the dynamic state */
+struct tabs {
+	const struct xdpgpu_nat64_map *map;
+	uint32_t nmap;
+	struct oracle_nat64_state *st;
+	uint64_t now;
+};
+
+/* v6_state_map for nat64_handle_v6 (:809-828): 1 and the address, 0 no
+ * entry (static tables: NO_STATE), -1 allocation failed */
+static int tab_v6(const struct tabs *T, const uint8_t *v6, uint32_t *v4)
+{
+	if (!T->st) {
+		const struct xdpgpu_nat64_map *m = find_v6(T->map, T->nmap, v6);
+		if (!m)
+			return 0;
+		*v4 = m->v4;
+		return 1;
+	}
+	struct ent6 *e = st_find6(T->st, v6);
+	if (e) {
+		e->last_seen = T->now;
+	} else {
+		e = st_alloc(T->st, v6, T->now);
+		if (!e)
+			return -1;
+	}
+	*v4 = e->v4;
+	return 1;
+}
+
+/* v4_reversemap for nat64_handle_v4 (:491) */
+static int tab_v4(const struct tabs *T, uint32_t v4, uint8_t v6[16])
+{
+	if (!T->st) {
+		const struct xdpgpu_nat64_map *m = find_v4(T->map, T->nmap, v4);
+		if (!m)
+			return 0;
+		memcpy(v6, m->v6, 16);
+		return 1;
+	}
+	const struct ent4 *r = st_find4(T->st, v4);
+	if (!r)
+		return 0;
+	memcpy(v6, r->v6, 16);
+	return 1;
+}
+
 static int lpm_match(const uint8_t *addr, const uint8_t *pref, uint32_t plen)
 {
 	if (!plen)
@@ -319,8 +590,7 @@ static void l4_addr_update(uint8_t *c, int proto, const uint8_t *from, int fn,
 
 /* nat64_handle_v6 (nat64_kern.c:741-873) on one frame */
 static int handle_v6(uint8_t *umem, uint64_t eff, uint32_t len, uint32_t l3,
-		     const struct xdpgpu_nat64_cfg *cfg,
-		     const struct xdpgpu_nat64_map *map, uint32_t nmap,
+		     const struct xdpgpu_nat64_cfg *cfg, const struct tabs *T,
 		     struct xdpgpu_desc *out)
 {
 	uint8_t *p = umem + eff;
@@ -343,9 +613,12 @@ static int handle_v6(uint8_t *umem, uint64_t eff, uint32_t len, uint32_t l3,
 		return XDPGPU_TC_ACT_SHOT;
 	if (!lpm_match(p + l3 + 8, cfg->allow_prefix, cfg->allow_plen))
 		return XDPGPU_TC_ACT_SHOT;
-	const struct xdpgpu_nat64_map *st = find_v6(map, nmap, p + l3 + 8);
-	if (!st)
+	uint32_t src4 = 0;
+	const int got = tab_v6(T, p + l3 + 8, &src4);
+	if (got == 0)
 		return XDPGPU_NAT64_NO_STATE;
+	if (got < 0)
+		return XDPGPU_TC_ACT_SHOT;     /* alloc_new_state failed */
 
 	/* the new IPv4 header */
 	uint8_t h4[20];
@@ -356,7 +629,7 @@ static int handle_v6(uint8_t *umem, uint64_t eff, uint32_t len, uint32_t l3,
 	put_be16(h4 + 6, 0x4000);
 	h4[8] = p[l3 + 7];
 	h4[9] = (uint8_t)nexthdr;
-	put_be32(h4 + 12, st->v4);
+	put_be32(h4 + 12, src4);
 	memcpy(h4 + 16, a4, 4);
 
 	const uint32_t l4 = l3 + 40;
@@ -406,8 +679,7 @@ static int handle_v6(uint8_t *umem, uint64_t eff, uint32_t len, uint32_t l3,
 
 /* nat64_handle_v4 (nat64_kern.c:443-541) on one frame */
 static int handle_v4(uint8_t *umem, uint64_t eff, uint32_t len, uint32_t l3,
-		     const struct xdpgpu_nat64_cfg *cfg,
-		     const struct xdpgpu_nat64_map *map, uint32_t nmap,
+		     const struct xdpgpu_nat64_cfg *cfg, const struct tabs *T,
 		     struct xdpgpu_desc *out)
 {
 	uint8_t *p = umem + eff;
@@ -421,14 +693,14 @@ static int handle_v4(uint8_t *umem, uint64_t eff, uint32_t len, uint32_t l3,
 		return XDPGPU_TC_ACT_OK;
 	if (ihl != 20 || (be16(p + l3 + 6) & ~0x4000u))
 		return XDPGPU_TC_ACT_SHOT;
-	const struct xdpgpu_nat64_map *st = find_v4(map, nmap, d4);
-	if (!st)
+	uint8_t dst6[16];
+	if (!tab_v4(T, d4, dst6))
 		return XDPGPU_TC_ACT_SHOT;
 	uint8_t h6[40];
 	memset(h6, 0, 40);
 	if (!oracle_v4addr_to_v6(p + l3 + 12, h6 + 8, cfg->v6_prefix, (int)cfg->v6_plen))
 		return XDPGPU_TC_ACT_SHOT;
-	memcpy(h6 + 24, st->v6, 16);
+	memcpy(h6 + 24, dst6, 16);
 	const uint8_t tos = p[l3 + 1], proto = p[l3 + 9];
 	/* struct ipv6hdr on little-endian: priority:4 is the low nibble */
 	h6[0] = (uint8_t)(6 << 4 | ((tos & 0x70) >> 4));
@@ -468,10 +740,9 @@ static int handle_v4(uint8_t *umem, uint64_t eff, uint32_t len, uint32_t l3,
 }
 
 /* nat64_handler (nat64_kern.c:875-890) over a batch */
-int oracle_nat64(uint8_t *umem, uint64_t umem_size, const struct xdpgpu_desc *descs,
-		 uint32_t n, const struct xdpgpu_nat64_cfg *cfg,
-		 const struct xdpgpu_nat64_map *map, uint32_t nmap,
-		 uint8_t *action, struct xdpgpu_desc *out)
+static int run_batch(uint8_t *umem, uint64_t umem_size, const struct xdpgpu_desc *descs,
+		     uint32_t n, const struct xdpgpu_nat64_cfg *cfg, const struct tabs *T,
+		     uint8_t *action, struct xdpgpu_desc *out)
 {
 	for (uint32_t i = 0; i < n; i++) {
 		const uint64_t addr = descs[i].addr;
@@ -486,12 +757,30 @@ int oracle_nat64(uint8_t *umem, uint64_t umem_size, const struct xdpgpu_desc *de
 		const int et = eth_type(umem + eff, len, &l3);
 		int act = XDPGPU_TC_ACT_OK;
 		if (cfg->direction == XDPGPU_NAT64_EGRESS && et == 0x0800)
-			act = handle_v4(umem, eff, len, l3, cfg, map, nmap, &out[i]);
+			act = handle_v4(umem, eff, len, l3, cfg, T, &out[i]);
 		else if (cfg->direction == XDPGPU_NAT64_INGRESS && et == 0x86DD)
-			act = handle_v6(umem, eff, len, l3, cfg, map, nmap, &out[i]);
+			act = handle_v6(umem, eff, len, l3, cfg, T, &out[i]);
 		if (act == XDPGPU_TC_ACT_REDIRECT)
 			out[i].options = descs[i].options;
 		action[i] = (uint8_t)act;
 	}
 	return 0;
+}
+
+int oracle_nat64(uint8_t *umem, uint64_t umem_size, const struct xdpgpu_desc *descs,
+		 uint32_t n, const struct xdpgpu_nat64_cfg *cfg,
+		 const struct xdpgpu_nat64_map *map, uint32_t nmap,
+		 uint8_t *action, struct xdpgpu_desc *out)
+{
+	const struct tabs T = {map, nmap, NULL, 0};
+	return run_batch(umem, umem_size, descs, n, cfg, &T, action, out);
+}
+
+int oracle_nat64_dyn(uint8_t *umem, uint64_t umem_size, const struct xdpgpu_desc *descs,
+		     uint32_t n, const struct xdpgpu_nat64_cfg *cfg,
+		     struct oracle_nat64_state *st, uint64_t now, uint8_t *action,
+		     struct xdpgpu_desc *out)
+{
+	const struct tabs T = {NULL, 0, st, now};
+	return run_batch(umem, umem_size, descs, n, cfg, &T, action, out);
 }

@@ -53,6 +53,24 @@ int oracle_nat64(uint8_t *umem, uint64_t umem_size,
 		 const struct xdpgpu_nat64_cfg *cfg,
 		 const struct xdpgpu_nat64_map *map, uint32_t nmap,
 		 uint8_t *action, struct xdpgpu_desc *out);
+/* nat64 with dynamic state (alloc_new_state): the tables live in an opaque
+ * object made from the configuration and the static entries; one call is
+ * one batch at time `now`, frames in order. */
+struct oracle_nat64_state;
+struct oracle_nat64_state *oracle_nat64_state_new(const struct xdpgpu_nat64_cfg *cfg,
+						  const struct xdpgpu_nat64_map *map,
+						  uint32_t nmap, uint64_t timeout_ns,
+						  uint64_t next_addr);
+void oracle_nat64_state_free(struct oracle_nat64_state *st);
+int oracle_nat64_dyn(uint8_t *umem, uint64_t umem_size,
+		     const struct xdpgpu_desc *descs, uint32_t n,
+		     const struct xdpgpu_nat64_cfg *cfg, struct oracle_nat64_state *st,
+		     uint64_t now, uint8_t *action, struct xdpgpu_desc *out);
+/* entries in insertion order, next_addr, reclaim queue oldest first (the
+ * counts are returned whatever max / qmax allow to be copied) */
+int oracle_nat64_state_read(const struct oracle_nat64_state *st,
+			    struct xdpgpu_nat64_entry *out, uint32_t max, uint32_t *n,
+			    uint64_t *next_addr, uint32_t *queue, uint32_t qmax, uint32_t *nq);
 int oracle_v4addr_to_v6(const uint8_t a4[4], uint8_t a6[16],
 			const uint8_t pref[16], int plen);
 int oracle_v6addr_to_v4(const uint8_t a6[16], int plen, uint8_t a4[4],

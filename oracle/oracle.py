@@ -89,6 +89,14 @@ def lib() -> C.CDLL:
         o.oracle_bench.restype = C.c_double
         o.oracle_nat64.argtypes = [vp, u64, vp, u32, C.POINTER(Nat64Cfg), vp, u32,
                                    vp, vp]
+        o.oracle_nat64_state_new.argtypes = [C.POINTER(Nat64Cfg), vp, u32, u64, u64]
+        o.oracle_nat64_state_new.restype = vp
+        o.oracle_nat64_state_free.argtypes = [vp]
+        o.oracle_nat64_state_free.restype = None
+        o.oracle_nat64_dyn.argtypes = [vp, u64, vp, u32, C.POINTER(Nat64Cfg), vp, u64,
+                                       vp, vp]
+        o.oracle_nat64_state_read.argtypes = [vp, vp, u32, C.POINTER(u32),
+                                              C.POINTER(u64), vp, u32, C.POINTER(u32)]
         o.oracle_hints.argtypes = [vp, u64, vp, u32, u32, u32, vp]
         o.oracle_v4addr_to_v6.argtypes = [vp, vp, vp, C.c_int]
         o.oracle_v6addr_to_v4.argtypes = [vp, C.c_int, vp, vp]
@@ -195,6 +203,55 @@ def nat64(umem: np.ndarray, descs: np.ndarray, cfg: "Nat64Cfg", smap: np.ndarray
                    smap.ctypes.data if len(smap) else None, len(smap),
                    action.ctypes.data, out.ctypes.data)
     return action, out
+
+
+NAT64_ENTRY_DTYPE = np.dtype([("v6", "u1", (16,)), ("v4", "<u4"), ("static_conf", "<u4"),
+                              ("last_seen", "<u8")])
+
+
+class Nat64State:
+    """The nat64 state tables with dynamic allocation (oracle_nat64_state):
+    one `run` is one batch at time `now`, frames in order."""
+
+    def __init__(self, cfg: "Nat64Cfg", smap: np.ndarray, timeout_ns: int,
+                 next_addr: int = 1):
+        self.o = lib()
+        self.cfg = cfg
+        smap = np.ascontiguousarray(smap, NAT64_MAP_DTYPE)
+        self.h = self.o.oracle_nat64_state_new(C.byref(cfg),
+                                               smap.ctypes.data if len(smap) else None,
+                                               len(smap), timeout_ns, next_addr)
+        if not self.h:
+            raise MemoryError("oracle_nat64_state_new")
+
+    def run(self, umem: np.ndarray, descs: np.ndarray, now: int):
+        descs = np.ascontiguousarray(descs, DESC_DTYPE)
+        n = len(descs)
+        action = np.zeros(n, np.uint8)
+        out = np.zeros(n, DESC_DTYPE)
+        self.o.oracle_nat64_dyn(umem.ctypes.data, umem.nbytes, descs.ctypes.data, n,
+                                C.byref(self.cfg), self.h, now, action.ctypes.data,
+                                out.ctypes.data)
+        return action, out
+
+    def state(self):
+        """(entries in insertion order, next_addr, reclaim queue)"""
+        n, nq, na = C.c_uint32(0), C.c_uint32(0), C.c_uint64(0)
+        self.o.oracle_nat64_state_read(self.h, None, 0, C.byref(n), C.byref(na), None, 0,
+                                       C.byref(nq))
+        ent = np.zeros(n.value, NAT64_ENTRY_DTYPE)
+        q = np.zeros(nq.value, np.uint32)
+        self.o.oracle_nat64_state_read(self.h, ent.ctypes.data, n.value, C.byref(n),
+                                       C.byref(na), q.ctypes.data, nq.value, C.byref(nq))
+        return ent, int(na.value), q
+
+    def close(self):
+        if self.h:
+            self.o.oracle_nat64_state_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
 
 
 def hints(umem: np.ndarray, descs: np.ndarray, rx_time_id: int, mark_id: int):
