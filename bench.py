@@ -168,7 +168,9 @@ def pmc_traffic(n: int, size: int):
     (profiles/*_pmc.json, tools/pmc_profile.sh + tools/pmc_summary.py), if it
     was taken on this workload; else None."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
+    # the config-2 summaries only (r<NN>_pmc.json; the other workloads'
+    # are r<NN>_pmc_<workload>.json)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc.json")))
     if not files:
         return None
     try:
@@ -247,6 +249,35 @@ def nat64_run(dev, stream, n, steps, local):
             if k >= 2:
                 ms.append(e0.elapsed_time(e1))
     ok = bool(np.array_equal(d_act.cpu().numpy(), ex))
+    # dynamic state (alloc_new_state) in steady state: the 65533 static
+    # mappings, the v4 pool widened to 10.98.0.0/15 so that the pool's 1000
+    # unmapped sources get addresses from next_addr 1 (10.98.0.x) in the
+    # untimed first launches; then every launch is a hit per frame (the
+    # last_seen stamps, the listed-frame count read back)
+    dms = []
+    dcfg = xdpgpu.Nat64Cfg.from_buffer_copy(bytes(cfg))
+    dcfg.v4_prefix, dcfg.v4_mask = 0x0A620000, 0xFFFE0000
+    with xdpgpu.XdpGpu(local) as g:
+        g.nat64_setup(dcfg, smap)
+        g.nat64_dynamic(7200 * 10**9, 1)
+        for k in range(steps + 2):
+            g.nat64_clock(10**13 + k)
+            with torch.cuda.stream(stream):
+                work.copy_(pristine, non_blocking=True)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            g.nat64_dev(work, u.nbytes, d_desc, n, d_act, d_out, stream)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            if k >= 2:
+                dms.append(e0.elapsed_time(e1))
+        nent = len(g.nat64_state()[0])
+    exd = ex.copy()
+    exd[exd == xdpgpu.NAT64_NO_STATE] = xdpgpu.TC_ACT_REDIRECT
+    dyn = {"workload": "the same pool, dynamic state: 65533 static entries + those allocated for "
+                       "its unmapped sources (v4 pool 10.98.0.0/15), steady state",
+           "ms_per_launch": round(float(np.mean(dms)), 4),
+           "entries": nent, "actions_ok": bool(np.array_equal(d_act.cpu().numpy(), exd))}
     t = float(np.mean(ms))
     algo = n * 149
     out = {"workload": f"config4: {n} x 128B IPv6 frames, nat64 ingress (64:ff9b::/96, "
@@ -255,7 +286,7 @@ def nat64_run(dev, stream, n, steps, local):
            "algorithmic_bytes_per_launch": algo,
            "gbps": round(algo / t / 1e6, 1),
            "roofline_frac": round(algo / t / 1e6 / HBM_PEAK_GBS, 4),
-           "actions_ok": ok}
+           "actions_ok": ok, "dynamic_state": dyn}
     del pristine, work, d_desc, d_act, d_out
     torch.cuda.empty_cache()
     return out

@@ -35,6 +35,7 @@ void Nat64State::build(const std::vector<xdpgpu_nat64_map> &statics, uint32_t nb
 	seq_.assign((size_t)nb_ * 4, 0);
 	touched_.assign((size_t)nb_ * 4, 0);
 	order_.clear();
+	dorder_.clear();
 	queue_.clear();
 	count_ = 0;
 	next_seq_ = 0;
@@ -100,6 +101,10 @@ bool Nat64State::put6(const uint32_t (&w)[4], uint32_t v4, bool stat, uint64_t l
 		B.val[slot & 3] = v4;
 		B.last_seen[slot & 3] = ls;
 		B.meta = (B.meta & ~(1u << (8 + (slot & 3)))) | (stat ? 1u << (8 + (slot & 3)) : 0);
+		if (stat)
+			dorder_.erase(seq_[slot]);
+		else
+			dorder_[seq_[slot]] = slot;
 		touch(0, slot >> 2, slot & 3);
 		return true;
 	}
@@ -117,6 +122,8 @@ bool Nat64State::put6(const uint32_t (&w)[4], uint32_t v4, bool stat, uint64_t l
 				B.meta |= 1u << (8 + j);
 			slot = b * 4 + j;
 			seq_[slot] = next_seq_;
+			if (!stat)
+				dorder_[next_seq_] = slot;
 			order_[next_seq_++] = slot;
 			count_++;
 			touch(0, b, j);
@@ -165,6 +172,7 @@ void Nat64State::erase6(uint32_t slot)
 	const uint32_t j = slot & 3;
 	B.meta &= ~(1u << j | 1u << (8 + j));
 	order_.erase(seq_[slot]);
+	dorder_.erase(seq_[slot]);
 	count_--;
 	touch(0, slot >> 2, j);
 }
@@ -195,11 +203,14 @@ uint32_t Nat64State::reclaim(uint64_t now,
 		queue_.pop_front();
 		return v;
 	}
+	/* static entries are never reclaimed: the walk covers the dynamic
+	 * ones, from the commit's cursor (the entries before it were seen
+	 * not timed out at this `now`, and an entry only leaves that state
+	 * by a later batch) */
 	const uint64_t thr = now - timeout_ns;   /* u64, as the reference */
-	for (auto it = order_.begin(); it != order_.end(); ++it) {
+	for (auto it = dorder_.lower_bound(cursor_); it != dorder_.end(); ++it) {
 		const uint32_t slot = it->second, b = slot >> 2, j = slot & 3;
-		if ((v6_[b].meta >> (8 + j)) & 1)
-			continue;
+		cursor_ = it->first;
 		uint64_t ls;
 		if (touched_[slot] == epoch_) {
 			ls = v6_[b].last_seen[j];
@@ -242,6 +253,7 @@ void Nat64State::commit(const uint32_t *idx, const uint4 *src, uint32_t m, uint6
 		epoch_ = 1;
 	}
 	have_dev_ = false;
+	cursor_ = 0;
 	pmap_.clear();
 	std::vector<std::pair<uint32_t, uint32_t>> ord(m);
 	for (uint32_t k = 0; k < m; k++)

@@ -73,6 +73,9 @@ private:
 	std::vector<Nat64V4Bucket> v4_;
 	uint32_t count_ = 0;              /* v6 entries */
 	std::map<uint64_t, uint32_t> order_;   /* insertion seq -> v6 slot */
+	std::map<uint64_t, uint32_t> dorder_;  /* the same, dynamic entries */
+	uint64_t cursor_ = 0;   /* per commit: the dynamic entries before this
+				 * seq were seen not timed out (they stay so) */
 	std::vector<uint64_t> seq_;            /* v6 slot -> insertion seq */
 	uint64_t next_seq_ = 0;
 	std::deque<uint32_t> queue_;           /* reclaimed_addrs, FIFO */

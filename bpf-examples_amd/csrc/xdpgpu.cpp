@@ -849,9 +849,20 @@ static int nat64_commit(xdpgpu_ctx *ctx, Nat64Args a, uint64_t now, hipStream_t 
 	std::vector<uint32_t> sidx, ov;
 	std::vector<Nat64Patch> patches;
 	int err = 0;
+	struct timespec t0, t1;
+	clock_gettime(CLOCK_MONOTONIC, &t0);
 	ctx->nst.commit(idx.data(), src.data(), m, now,
 			[ctx](std::vector<Nat64V6Bucket> &t) { return nat64_devtab(ctx, t); },
 			sidx, ov, patches, err);
+	clock_gettime(CLOCK_MONOTONIC, &t1);
+	if (getenv("XDPGPU_NAT64_TRACE")) {
+		uint32_t shot = 0;
+		for (uint32_t v : ov)
+			shot += !v;
+		fprintf(stderr, "nat64 commit: %u listed, %u failed, %zu patches, %.3f ms\n", m,
+			shot, patches.size(),
+			(t1.tv_sec - t0.tv_sec) * 1e3 + (t1.tv_nsec - t0.tv_nsec) / 1e6);
+	}
 	if (err)
 		return err;
 	if (patches.size() > ctx->pcap) {

@@ -12,7 +12,8 @@ import sys
 from collections import defaultdict
 
 
-RX = ("xdp_rx_db_kernel", "xdp_rx_kernel", "xdp_rx_bulk_kernel", "xdp_rx_generic_kernel")
+RX = ("xdp_rx_db_kernel", "xdp_rx_kernel", "xdp_rx_bulk_kernel", "xdp_rx_generic_kernel",
+      "xdp_nat64_fast_kernel", "xdp_nat64_kernel")
 
 
 def main(out, dest=None, frames=16 << 20, size=64, label=None):
@@ -41,7 +42,7 @@ def main(out, dest=None, frames=16 << 20, size=64, label=None):
     print(json.dumps(summary, indent=1))
     with open(os.path.join(out, "summary.json"), "w") as fh:
         json.dump(summary, fh, indent=1)
-    # bench.py form: HBM bytes per RX launch = sum over the three kernels
+    # bench.py form: HBM bytes per launch = sum over the launch's kernels
     rx = {k: v for k, v in summary.items()
           if any(k.split("<")[0].split("(")[0].endswith(r) for r in RX)}
     tot = sum(v.get("hbm_bytes_per_launch", 0.0) for v in rx.values())
