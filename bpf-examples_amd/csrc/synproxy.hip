@@ -1,0 +1,463 @@
+// SPDX-License-Identifier: GPL-2.0
+/*
+ * synproxy.hip - the SYN proxy transform (xdpgpu_synproxy_dev): the XDP
+ * program of xdp-synproxy/xdp_synproxy_kern.c (syncookie_xdp, :803-819)
+ * over a batch of UMEM frames, one lane per frame.
+ *
+ * A lane stages its frame's first kRow bytes in an LDS row (16-byte loads
+ * for 16-byte aligned frames, bytes otherwise), runs the program on the row
+ * (TCP option bytes past the row are read from the UMEM, bytes past the
+ * frame's end as the zeros bpf_xdp_adjust_tail grows it with), and writes
+ * back what changed: the SYN-ACK's headers (at most 14 + 40 + 40 bytes, all
+ * in the row) or the zeroed growth of a frame the program grew and then
+ * passed or dropped.  HBM-bound on the frame's first line and a few stores;
+ * the byte-wise parse runs in LDS.  Semantics and what lies outside the
+ * transform (conntrack, the kernel's cookie): include/xdpgpu.h.
+ */
+#include <hip/hip_runtime.h>
+
+#include "xdpgpu.h"
+#include "xdpgpu_internal.h"
+
+namespace xdpgpu {
+namespace {
+
+constexpr int kRow = 144;                 /* staged bytes per frame */
+constexpr int kRowDw = kRow / 4 + 1;      /* odd dword stride: no bank conflicts */
+constexpr int kBlockS = 256;
+
+enum { SP_ABORTED = 0, SP_DROP = 1, SP_PASS = 2, SP_TX = 3 };
+
+struct Frame {
+	uint8_t *row;              /* LDS: bytes [0, kRow) */
+	const uint8_t *g;          /* the frame in the UMEM */
+	uint32_t len0;             /* the frame's length before any growth */
+	/* the row holds the frame's bytes and zeros past its end (what the
+	 * program writes goes to the row); past the row, the UMEM up to the
+	 * frame's end, then the zeros of its growth */
+	__device__ uint32_t b(uint32_t i) const
+	{
+		if (i < (uint32_t)kRow)
+			return row[i];
+		return i < len0 ? g[i] : 0u;
+	}
+	__device__ void put(uint32_t i, uint32_t v) const { row[i] = (uint8_t)v; }
+	__device__ uint32_t be16(uint32_t i) const { return b(i) << 8 | b(i + 1); }
+	__device__ uint32_t be32(uint32_t i) const { return be16(i) << 16 | be16(i + 2); }
+	__device__ uint32_t le32(uint32_t i) const
+	{
+		return b(i) | b(i + 1) << 8 | b(i + 2) << 16 | b(i + 3) << 24;
+	}
+	__device__ void put_be16(uint32_t i, uint32_t v) const
+	{
+		put(i, v >> 8);
+		put(i + 1, v);
+	}
+	__device__ void put_be32(uint32_t i, uint32_t v) const
+	{
+		put_be16(i, v >> 16);
+		put_be16(i + 2, v & 0xffff);
+	}
+};
+
+/* bpf_csum_diff(0, 0, p, n, 0): LE words, 64-bit accumulation */
+__device__ uint64_t sum32(const Frame &F, uint32_t at, uint32_t n)
+{
+	uint64_t s = 0;
+	for (uint32_t i = 0; i + 4 <= n; i += 4)
+		s += F.le32(at + i);
+	return s;
+}
+
+/* csum_fold (xdp_synproxy_kern.c:121-126) of a 64-bit sum */
+__device__ uint32_t fold(uint64_t s)
+{
+	s = (s & 0xffffffffu) + (s >> 32);
+	s = (s & 0xffffffffu) + (s >> 32);
+	uint32_t c = (uint32_t)s;
+	c = (c & 0xffff) + (c >> 16);
+	c = (c & 0xffff) + (c >> 16);
+	return ~c & 0xffff;
+}
+
+/* csum_tcpudp_magic (:128-147, little-endian) / csum_ipv6_magic (:149-172) */
+__device__ uint32_t l4_magic(const Frame &F, uint32_t ip, bool v6, uint32_t len,
+			     uint64_t body)
+{
+	uint64_t s = body;
+	if (v6) {
+		for (int i = 0; i < 8; i++)
+			s += F.le32(ip + 8 + 4 * i);
+		s += __builtin_bswap32(len);
+		s += __builtin_bswap32(6u);
+	} else {
+		s += F.le32(ip + 12);
+		s += F.le32(ip + 16);
+		s += (uint64_t)(6 + len) << 8;
+	}
+	return fold(s);
+}
+
+/* the build-defined cookie (include/xdpgpu.h) */
+__device__ uint32_t cookie_hash(const Frame &F, uint32_t ip, bool v6, uint32_t tcp,
+				uint32_t key, uint32_t count)
+{
+	uint32_t w[9];
+	for (int i = 0; i < 9; i++)
+		w[i] = 0;
+	if (v6) {
+		for (int i = 0; i < 4; i++) {
+			w[i] = F.le32(ip + 8 + 4 * i);
+			w[4 + i] = F.le32(ip + 24 + 4 * i);
+		}
+	} else {
+		w[0] = F.le32(ip + 12);
+		w[4] = F.le32(ip + 16);
+	}
+	w[8] = F.be16(tcp) << 16 | F.be16(tcp + 2);
+	return jhash2_dev(w, 9, key + count);
+}
+
+struct Opt {
+	uint32_t off, end;
+	uint32_t wscale, ts, sack, tsecr;   /* tsecr: the 4 bytes, LE word */
+};
+
+/* next() (:199-215) */
+__device__ bool next(Opt &c, uint32_t sz, uint32_t &at)
+{
+	if (c.off > 0xffffu - sz || c.off + sz >= c.end)
+		return false;
+	at = c.off;
+	c.off += sz;
+	return true;
+}
+
+/* tscookie_tcpopt_parse (:217-262): true ends the walk */
+__device__ bool opt_parse(Opt &c, const Frame &F)
+{
+	const uint32_t off = c.off;
+	uint32_t op, sz, v;
+	if (!next(c, 1, op))
+		return true;
+	const uint32_t code = F.b(op);
+	if (code == 0)
+		return true;
+	if (code == 1)
+		return false;
+	if (!next(c, 1, sz))
+		return true;
+	const uint32_t osz = F.b(sz);
+	if (osz < 2)
+		return true;
+	if (code == 3) {
+		if (!next(c, 1, v))
+			return true;
+		if (osz == 3)
+			c.wscale = F.b(v) < 14 ? F.b(v) : 14;
+	} else if (code == 8) {
+		if (!next(c, 4, v))
+			return true;
+		if (osz == 10) {
+			c.ts = 1;
+			c.tsecr = F.le32(v);
+		}
+	} else if (code == 4) {
+		if (osz == 2)
+			c.sack = 1;
+	}
+	c.off = off + osz;
+	return false;
+}
+
+/* syncookie_handle_syn (:577-715); len is the grown length */
+__device__ uint32_t handle_syn(const Frame &F, uint32_t &len, uint32_t ip, bool v6,
+			       uint32_t tcp, const xdpgpu_synproxy_cfg &cfg, bool &synack)
+{
+	uint32_t tcp_len = (F.b(tcp + 12) >> 4) * 4;
+	const uint32_t fl = F.b(tcp + 13);
+	if (fl & 0x05)
+		return SP_DROP;
+	if (!v6 && fold(sum32(F, ip, (F.b(ip) & 15) * 4)) != 0)
+		return SP_DROP;
+	if (l4_magic(F, ip, v6, tcp_len, sum32(F, tcp, tcp_len)) != 0)
+		return SP_DROP;
+	const uint32_t ip_len = v6 ? 40 : 20;
+	const uint32_t count = (uint32_t)(cfg.now_ns / 60000000000ull);
+	const uint32_t cookie = cookie_hash(F, ip, v6, tcp, cfg.cookie_key, count) +
+				F.be32(tcp + 4);
+	/* tscookie_init (:274-308) */
+	Opt oc = {tcp + 20, len, 0xf, 0, 0, 0};
+	for (int i = 0; i < 42; i++)
+		if (opt_parse(oc, F))
+			break;
+	uint32_t tsval = 0;        /* the TS option's first word, host order */
+	if (oc.ts) {
+		tsval = (uint32_t)(cfg.now_ns / 1000000ull) & ~0x3fu;
+		tsval |= oc.wscale & 0xf;
+		if (oc.sack)
+			tsval |= 1u << 4;
+		if ((fl & 0x40) && (fl & 0x80))
+			tsval |= 1u << 5;
+	}
+	if (14 + ip_len + 60 > len)
+		return SP_ABORTED;
+	if (!v6 && (F.b(ip) & 15) * 4 > 20) {
+		/* the TCP header moves down to the end of a 20-byte IP header */
+		for (uint32_t i = 0; i < 20; i++)
+			F.put(34 + i, F.b(tcp + i));
+		tcp = 34;
+		F.put(ip, (F.b(ip) & 0xf0) | 5);
+	}
+	uint32_t mss, wscale, ttl;
+	if (cfg.values) {
+		mss = v6 ? (uint32_t)(cfg.values >> 32) & 0xffff : (uint32_t)cfg.values & 0xffff;
+		wscale = (uint32_t)(cfg.values >> 16) & 0xf;
+		ttl = (uint32_t)(cfg.values >> 24) & 0xff;
+	} else {
+		mss = v6 ? 1440 : 1460;
+		wscale = 7;
+		ttl = 64;
+	}
+	/* tcpv4/v6_gen_synack (:533-575) */
+	for (uint32_t i = 0; i < 6; i++) {
+		const uint32_t t = F.b(i);
+		F.put(i, F.b(6 + i));
+		F.put(6 + i, t);
+	}
+	const uint32_t sa = v6 ? ip + 8 : ip + 12, da = v6 ? ip + 24 : ip + 16;
+	for (uint32_t i = 0; i < (v6 ? 16u : 4u); i++) {
+		const uint32_t t = F.b(sa + i);
+		F.put(sa + i, F.b(da + i));
+		F.put(da + i, t);
+	}
+	if (!v6) {
+		F.put(ip + 10, 0);
+		F.put(ip + 11, 0);
+		F.put(ip + 1, 0);
+		F.put(ip + 4, 0);
+		F.put(ip + 5, 0);
+		F.put(ip + 8, ttl);
+	} else {
+		F.put_be32(ip, 0x60000000u);
+		F.put(ip + 7, ttl);
+	}
+	/* tcp_gen_synack (:512-531) */
+	const uint32_t seq = F.be32(tcp + 4);
+	F.put(tcp + 12, 0x50);
+	F.put(tcp + 13, 0x12 | ((oc.ts && (tsval & (1u << 5))) ? 0x40 : 0));
+	F.put(tcp + 14, 0);
+	F.put(tcp + 15, 0);
+	const uint32_t sp = F.be16(tcp), dp = F.be16(tcp + 2);
+	F.put_be16(tcp, dp);
+	F.put_be16(tcp + 2, sp);
+	F.put_be32(tcp + 8, seq + 1);
+	F.put_be32(tcp + 4, cookie);
+	for (uint32_t i = 16; i < 20; i++)
+		F.put(tcp + i, 0);
+	/* tcp_mkoptions (:480-510) */
+	uint32_t o = tcp + 20;
+	F.put_be32(o, 2u << 24 | 4u << 16 | (mss & 0xffff));
+	o += 4;
+	if (oc.ts) {
+		F.put_be32(o, (tsval & (1u << 4)) ? (4u << 24 | 2u << 16 | 8u << 8 | 10u)
+						  : (1u << 24 | 1u << 16 | 8u << 8 | 10u));
+		F.put_be32(o + 4, tsval);
+		F.put(o + 8, oc.tsecr);
+		F.put(o + 9, oc.tsecr >> 8);
+		F.put(o + 10, oc.tsecr >> 16);
+		F.put(o + 11, oc.tsecr >> 24);
+		o += 12;
+		if ((tsval & 0xf) != 0xf) {
+			F.put_be32(o, 1u << 24 | 3u << 16 | 3u << 8 | wscale);
+			o += 4;
+		}
+	}
+	tcp_len = o - tcp;
+	F.put(tcp + 12, (tcp_len / 4) << 4);
+	if (!v6)
+		F.put_be16(ip + 2, 20 + tcp_len);
+	else
+		F.put_be16(ip + 4, tcp_len);
+	/* checksums (:679-704), stored as computed (LE u16) */
+	const uint32_t c = l4_magic(F, ip, v6, tcp_len, sum32(F, tcp, tcp_len));
+	F.put(tcp + 16, c);
+	F.put(tcp + 17, c >> 8);
+	if (!v6) {
+		const uint32_t h = fold(sum32(F, ip, 20));
+		F.put(ip + 10, h);
+		F.put(ip + 11, h >> 8);
+	}
+	len = 14 + ip_len + tcp_len;
+	synack = true;
+	return SP_TX;
+}
+
+/* syncookie_handle_ack (:717-734), the build-defined cookie check */
+__device__ uint32_t handle_ack(const Frame &F, uint32_t ip, bool v6, uint32_t tcp,
+			       const xdpgpu_synproxy_cfg &cfg)
+{
+	if (F.b(tcp + 13) & 0x04)
+		return SP_DROP;
+	const uint32_t count = (uint32_t)(cfg.now_ns / 60000000000ull);
+	const uint32_t want = F.be32(tcp + 8) - 1, seq = F.be32(tcp + 4) - 1;
+	for (uint32_t d = 0; d < 2; d++)
+		if (cookie_hash(F, ip, v6, tcp, cfg.cookie_key, count - d) + seq == want)
+			return SP_PASS;
+	return SP_DROP;
+}
+
+/* syncookie_xdp (:803-819): part1 (:736-767), part2 (:769-801) */
+__device__ uint32_t sp_frame(const Frame &F, uint32_t &len, uint64_t room,
+			     const xdpgpu_synproxy_cfg &cfg, bool &synack, uint32_t &grow)
+{
+	grow = 0;
+	if (len < 14)
+		return SP_DROP;
+	const uint32_t proto = F.be16(12), ip = 14;
+	uint32_t tcp;
+	bool v6;
+	if (proto == 0x0800) {
+		v6 = false;
+		if (ip + 20 > len)
+			return SP_DROP;
+		if ((F.b(ip) & 15) * 4 < 20 || (F.b(ip) >> 4) != 4)
+			return SP_DROP;
+		if (F.b(ip + 9) != 6)
+			return SP_PASS;
+		tcp = ip + (F.b(ip) & 15) * 4;
+	} else if (proto == 0x86DD) {
+		v6 = true;
+		if (ip + 40 > len)
+			return SP_DROP;
+		if ((F.b(ip) >> 4) != 6)
+			return SP_DROP;
+		if (F.b(ip + 6) != 6)
+			return SP_PASS;
+		tcp = ip + 40;
+	} else {
+		return SP_PASS;
+	}
+	if (tcp + 20 > len)
+		return SP_DROP;
+	uint32_t tcp_len = (F.b(tcp + 12) >> 4) * 4;
+	if (tcp_len < 20)
+		return SP_DROP;
+	if (!v6 && (F.be16(ip + 6) & 0x7fff) != 0x4000)
+		return SP_DROP;
+	bool allowed = false;
+	const uint32_t port = F.be16(tcp + 2);
+	for (int i = 0; i < 8; i++) {
+		if (cfg.ports[i] == 0)
+			break;
+		if (cfg.ports[i] == port) {
+			allowed = true;
+			break;
+		}
+	}
+	if (!allowed)
+		return SP_PASS;
+	const uint32_t fl = F.b(tcp + 13);
+	const uint32_t syn = (fl >> 1) & 1, ack = (fl >> 4) & 1;
+	if ((syn ^ ack) != 1)
+		return SP_DROP;
+	if (60 - tcp_len > room)
+		return SP_ABORTED;
+	grow = 60 - tcp_len;
+	len += grow;
+	if (!v6 && ip + 60 > len)
+		return SP_ABORTED;
+	if (tcp + 60 > len)
+		return SP_ABORTED;
+	return syn ? handle_syn(F, len, ip, v6, tcp, cfg, synack)
+		   : handle_ack(F, ip, v6, tcp, cfg);
+}
+
+__global__ __launch_bounds__(kBlockS) void synproxy_kernel(uint8_t *umem, uint64_t usize,
+							   const xdpgpu_desc *desc, uint32_t n,
+							   xdpgpu_synproxy_cfg cfg, uint8_t *verdict,
+							   xdpgpu_desc *out,
+							   unsigned long long *synacks)
+{
+	__shared__ uint32_t rows[kBlockS * kRowDw];
+	const uint64_t i = (uint64_t)blockIdx.x * kBlockS + threadIdx.x;
+	const bool active = i < n;
+	uint8_t *row = reinterpret_cast<uint8_t *>(rows + threadIdx.x * kRowDw);
+	const uint4 dv = active ? *reinterpret_cast<const uint4 *>(desc + i)
+				: make_uint4(0, 0, 0, 0);
+	const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
+	uint32_t len = dv.z;
+	const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
+	const bool valid = active && (uint64_t)len <= usize && eff <= usize - len;
+	bool synack = false;
+	if (valid) {
+		uint8_t *g = umem + eff;
+		/* stage [0, kRow): the frame's bytes, zeros past its end */
+		const uint32_t st = len < (uint32_t)kRow ? len : (uint32_t)kRow;
+		if (!(eff & 3)) {
+			for (uint32_t w = 0; w < (uint32_t)kRow / 4; w++) {
+				uint32_t v = 0;
+				if (4 * w < st) {
+					if (4 * w + 4 <= len) {
+						v = *reinterpret_cast<const uint32_t *>(g + 4 * w);
+					} else {
+						for (uint32_t k = 4 * w; k < len; k++)
+							v |= (uint32_t)g[k] << (8 * (k - 4 * w));
+					}
+				}
+				*reinterpret_cast<uint32_t *>(row + 4 * w) = v;
+			}
+		} else {
+			for (uint32_t k = 0; k < (uint32_t)kRow; k++)
+				row[k] = k < st ? g[k] : 0;
+		}
+		const Frame F = {row, g, len};
+		uint64_t room = usize - eff - len;
+		if (room > cfg.tailroom)
+			room = cfg.tailroom;
+		uint32_t grow = 0;
+		const uint32_t len0 = len;
+		const uint32_t act = sp_frame(F, len, room, cfg, synack, grow);
+		if (act == SP_TX) {
+			/* the SYN-ACK, and the rest of the growth as zeros */
+			const uint32_t end = len > len0 + grow ? len : len0 + grow;
+			for (uint32_t k = 0; k < end && k < (uint32_t)kRow; k++)
+				g[k] = row[k];
+			for (uint32_t k = len0 > (uint32_t)kRow ? len0 : (uint32_t)kRow;
+			     k < len0 + grow; k++)
+				g[k] = 0;
+		} else if (grow) {
+			/* grown by bpf_xdp_adjust_tail, then passed or dropped */
+			for (uint32_t k = 0; k < grow; k++)
+				g[len0 + k] = 0;
+		}
+		verdict[i] = (uint8_t)act;
+	} else if (active) {
+		verdict[i] = SP_ABORTED;
+	}
+	if (active) {
+		uint4 od = dv;
+		od.z = len;
+		*reinterpret_cast<uint4 *>(out + i) = od;
+	}
+	/* values[1] (values_inc_synacks, :332-340): one atomic per wave */
+	const uint64_t m = __ballot(synack);
+	if (synacks && m && (threadIdx.x & 63) == (uint32_t)(__builtin_ffsll((long long)m) - 1))
+		atomicAdd(synacks, (unsigned long long)__popcll(m));
+}
+
+} // namespace
+
+hipError_t launch_synproxy(uint8_t *umem, uint64_t usize, const xdpgpu_desc *desc,
+			   uint32_t n, const xdpgpu_synproxy_cfg &cfg, uint8_t *verdict,
+			   xdpgpu_desc *out, unsigned long long *synacks, hipStream_t stream)
+{
+	const uint32_t blocks = (n + kBlockS - 1) / kBlockS;
+	if (!blocks)
+		return hipSuccess;
+	hipLaunchKernelGGL(synproxy_kernel, dim3(blocks), dim3(kBlockS), 0, stream, umem, usize,
+			   desc, n, cfg, verdict, out, synacks);
+	return hipGetLastError();
+}
+
+} // namespace xdpgpu

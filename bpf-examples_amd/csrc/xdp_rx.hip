@@ -58,8 +58,9 @@ __device__ __forceinline__ bool dbg_bad(bool bad, uint32_t code, uint64_t val)
 
 /* Timing builds (-DXDPGPU_STAMPS, tools/dbg_build.sh stamps): each wave of
  * the double-buffered kernel records s_memrealtime (100 MHz) at its start
- * (0), the end of its tile loop (1), its end (2), the ends of its tail's
- * exception (4) and bulk (5) passes; read by xdpgpu_stamps_read. */
+ * (0), the end of its tile loop (1), its end (2), and the time its tail
+ * spends in each kind of batch (4-7, STAMP_ADD); read by
+ * xdpgpu_stamps_read. */
 #ifdef XDPGPU_STAMPS
 constexpr int kStampWaves = 8192;
 __device__ unsigned long long g_stamp[8 * kStampWaves];
@@ -69,13 +70,28 @@ __device__ unsigned long long g_stamp[8 * kStampWaves];
 		if ((lane) == 0 && (wgid) < (uint64_t)kStampWaves) {           \
 			g_stamp[8 * (wgid) + (k)] = __builtin_amdgcn_s_memrealtime(); \
 			if ((k) == 0)                                          \
+				g_stamp[8 * (wgid) + 4] = g_stamp[8 * (wgid) + 5] = \
+				g_stamp[8 * (wgid) + 6] = g_stamp[8 * (wgid) + 7] = 0; \
+			if ((k) == 0)                                          \
 				g_stamp[8 * (wgid) + 3] =                      \
 					(unsigned long long)(uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) | \
 					((unsigned long long)(uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32); \
 		}                                                              \
 	} while (0)
+/* time (ticks) a wave spends in its tail's exception (4), bulk (5) and
+ * payload (6) batches and waiting for the exception batches (7) */
+#define STAMP_T0() unsigned long long st_t0_ = __builtin_amdgcn_s_memrealtime()
+#define STAMP_ADD(wgid, lane, k)                                               \
+	do {                                                                   \
+		const unsigned long long st_t1_ = __builtin_amdgcn_s_memrealtime(); \
+		if ((lane) == 0 && (wgid) < (uint64_t)kStampWaves)             \
+			g_stamp[8 * (wgid) + (k)] += st_t1_ - st_t0_;          \
+		st_t0_ = st_t1_;                                               \
+	} while (0)
 #else
 #define STAMP(wgid, lane, k) do { } while (0)
+#define STAMP_T0() do { } while (0)
+#define STAMP_ADD(wgid, lane, k) do { } while (0)
 #endif
 
 /* ------------------------------------------------------------------ */
@@ -159,31 +175,7 @@ __device__ __forceinline__ uint32_t csum_replace2(uint32_t sum, uint32_t old,
 /* jhash (include/jhash.h:25-52), word form; jhash(key, 44) equals
  * jhash2(words, 11) on little-endian (jhash.h:68-142).                 */
 
-__device__ __forceinline__ uint32_t rol32(uint32_t w, uint32_t s)
-{
-	return (w << s) | (w >> ((32 - s) & 31));
-}
-
-#define JH_MIX(a, b, c)                                   \
-	do {                                              \
-		a -= c; a ^= rol32(c, 4);  c += b;        \
-		b -= a; b ^= rol32(a, 6);  a += c;        \
-		c -= b; c ^= rol32(b, 8);  b += a;        \
-		a -= c; a ^= rol32(c, 16); c += b;        \
-		b -= a; b ^= rol32(a, 19); a += c;        \
-		c -= b; c ^= rol32(b, 4);  b += a;        \
-	} while (0)
-
-#define JH_FINAL(a, b, c)                                 \
-	do {                                              \
-		c ^= b; c -= rol32(b, 14);                \
-		a ^= c; a -= rol32(c, 11);                \
-		b ^= a; b -= rol32(a, 25);                \
-		c ^= b; c -= rol32(b, 16);                \
-		a ^= c; a -= rol32(c, 4);                 \
-		b ^= a; b -= rol32(a, 14);                \
-		c ^= b; c -= rol32(b, 24);                \
-	} while (0)
+/* rol32, JH_MIX, JH_FINAL: xdpgpu_internal.h */
 
 __device__ __forceinline__ uint32_t jhash_key44(const uint32_t k[11],
 						uint32_t initval)
@@ -1111,7 +1103,12 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 				(uint32_t)(lo - lo_al));
 	__builtin_amdgcn_wave_barrier();
 
-	/* G-lane group streaming with dynamic frame assignment */
+	/* G-lane group streaming with dynamic frame assignment.  Loads under
+	 * their lane's range only: a branch-free form (every lane loading, the
+	 * chunks outside masked to zero) lets the compiler count loads in
+	 * flight, and two steps in flight per group then fit, but it ran 18 %
+	 * slower on 1500 B frames and 4 % on IMIX, with or without the second
+	 * step (the dead lanes' loads cost more than the overlap gains) */
 	uint32_t k = lane / G;             /* this group's frame */
 	uint32_t nxt = kWave / G;          /* next unassigned (uniform) */
 	bool live = k < nb;
@@ -1700,6 +1697,7 @@ __device__ __forceinline__ void rx_tail(const RxArgs &a, const FastWave &w,
 	const uint32_t nbb = (bc + kWave - 1) / kWave, nxb = (xc + kWave - 1) / kWave;
 	uint32_t ycn = 0, nyb = 0;
 	bool ready = nxb == 0;
+	STAMP_T0();
 	for (;;) {
 		const uint32_t q = lds_fetch_add(ctl + 3, 1, lane);
 		if (q < nxb) {
@@ -1712,6 +1710,7 @@ __device__ __forceinline__ void rx_tail(const RxArgs &a, const FastWave &w,
 					  my_bytes);
 			lds_dma_landed();
 			(void)lds_fetch_add(ctl + 5, 1, lane);
+			STAMP_ADD(rb * nw + wid, lane, 4);
 			continue;
 		}
 		if (q < nxb + nbb) {
@@ -1719,12 +1718,14 @@ __device__ __forceinline__ void rx_tail(const RxArgs &a, const FastWave &w,
 			bulk_batch<kTailU, true, false, kTailG>(a, meta, part4, lane, w.bl + b,
 								bc - b < (uint32_t)kWave ? bc - b : kWave,
 								cnt, my_bytes);
+			STAMP_ADD(rb * nw + wid, lane, 5);
 			continue;
 		}
 		if (!ready) {
 			while (lds_fetch_add(ctl + 5, 0, lane) < nxb)
 				__builtin_amdgcn_s_sleep(2);
 			ready = true;
+			STAMP_ADD(rb * nw + wid, lane, 7);
 		}
 		if (!nyb && !ycn) {
 			/* the count the exception batches' atomics left (read at
@@ -1741,9 +1742,8 @@ __device__ __forceinline__ void rx_tail(const RxArgs &a, const FastWave &w,
 		bulk_batch<kTailU, true, true, kTailG>(a, meta, part4, lane, yl + b,
 						      ycn - b < (uint32_t)kWave ? ycn - b : kWave,
 						      cnt, my_bytes);
+		STAMP_ADD(rb * nw + wid, lane, 6);
 	}
-	STAMP(rb * nw + wid, lane, 4);
-	STAMP(rb * nw + wid, lane, 5);
 }
 
 /*

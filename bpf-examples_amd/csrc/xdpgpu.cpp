@@ -998,6 +998,21 @@ int xdpgpu_nat64_dev(xdpgpu_ctx *ctx, void *d_umem, uint64_t umem_size,
 	return dyn ? nat64_commit(ctx, a, now, st) : 0;
 }
 
+int xdpgpu_synproxy_dev(xdpgpu_ctx *ctx, void *d_umem, uint64_t umem_size,
+			const xdpgpu_desc *d_descs, uint32_t n, const xdpgpu_synproxy_cfg *cfg,
+			uint8_t *d_verdict, xdpgpu_desc *d_out, uint64_t *d_synacks, void *stream)
+{
+	if (!ctx || !d_umem || !d_descs || !cfg || !d_verdict || !d_out)
+		return -EINVAL;
+	if (n == 0)
+		return 0;
+	HIP_TRY(ctx, hipSetDevice(ctx->cfg.device));
+	hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
+	HIP_TRY(ctx, launch_synproxy((uint8_t *)d_umem, umem_size, d_descs, n, *cfg, d_verdict,
+				     d_out, (unsigned long long *)d_synacks, st));
+	return 0;
+}
+
 int xdpgpu_ceiling_dev(xdpgpu_ctx *ctx, const void *d_umem, uint64_t umem_size,
 		       const xdpgpu_desc *d_descs, uint32_t n, uint8_t *d_verdict,
 		       void *d_res, void *d_tuples, void *stream)

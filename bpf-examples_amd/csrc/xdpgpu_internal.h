@@ -208,6 +208,63 @@ struct EchoArgs {
 };
 hipError_t launch_echo_writeback(const EchoArgs &a, hipStream_t stream);
 
+/* jhash (include/jhash.h:25-52) mixing steps, for the device kernels */
+__device__ __forceinline__ uint32_t rol32(uint32_t w, uint32_t s)
+{
+	return (w << s) | (w >> ((32 - s) & 31));
+}
+
+#define JH_MIX(a, b, c)                                   \
+	do {                                              \
+		a -= c; a ^= rol32(c, 4);  c += b;        \
+		b -= a; b ^= rol32(a, 6);  a += c;        \
+		c -= b; c ^= rol32(b, 8);  b += a;        \
+		a -= c; a ^= rol32(c, 16); c += b;        \
+		b -= a; b ^= rol32(a, 19); a += c;        \
+		c -= b; c ^= rol32(b, 4);  b += a;        \
+	} while (0)
+
+#define JH_FINAL(a, b, c)                                 \
+	do {                                              \
+		c ^= b; c -= rol32(b, 14);                \
+		a ^= c; a -= rol32(c, 11);                \
+		b ^= a; b -= rol32(a, 25);                \
+		c ^= b; c -= rol32(b, 16);                \
+		a ^= c; a -= rol32(c, 4);                 \
+		b ^= a; b -= rol32(a, 14);                \
+		c ^= b; c -= rol32(b, 24);                \
+	} while (0)
+
+/* jhash2 (include/jhash.h:114-142) of len words */
+__device__ __forceinline__ uint32_t jhash2_dev(const uint32_t *k, uint32_t len, uint32_t initval)
+{
+	uint32_t a, b, c;
+	a = b = c = 0xdeadbeefu + (len << 2) + initval;
+	while (len > 3) {
+		a += k[0];
+		b += k[1];
+		c += k[2];
+		JH_MIX(a, b, c);
+		len -= 3;
+		k += 3;
+	}
+	switch (len) {
+	case 3:
+		c += k[2];
+		[[fallthrough]];
+	case 2:
+		b += k[1];
+		[[fallthrough]];
+	case 1:
+		a += k[0];
+		JH_FINAL(a, b, c);
+		break;
+	default:
+		break;
+	}
+	return c;
+}
+
 /* nat64 state tables (v6_state_map and v4_reversemap, nat64_kern.c:17-46):
  * 4-way buckets of one 128-byte line, so a lookup touches one line; the
  * home bucket is fastrange(nat64_slot_hash(key), nbuckets), a full bucket
@@ -299,6 +356,9 @@ hipError_t launch_jhash(const uint8_t *keys, uint32_t key_len,
 			uint32_t *out, hipStream_t stream);
 hipError_t launch_ip_fast_csum(const uint8_t *hdrs, uint32_t stride,
 			       uint32_t n, uint16_t *out, hipStream_t stream);
+hipError_t launch_synproxy(uint8_t *umem, uint64_t usize, const xdpgpu_desc *desc,
+			   uint32_t n, const xdpgpu_synproxy_cfg &cfg, uint8_t *verdict,
+			   xdpgpu_desc *out, unsigned long long *synacks, hipStream_t stream);
 
 } // namespace xdpgpu
 

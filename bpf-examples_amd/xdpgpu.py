@@ -137,6 +137,12 @@ class Nat64Dyn(C.Structure):
                 ("now_ns", C.c_uint64), ("rsvd", C.c_uint64)]
 
 
+class SynproxyCfg(C.Structure):
+    """struct xdpgpu_synproxy_cfg"""
+    _fields_ = [("values", C.c_uint64), ("ports", C.c_uint16 * 8), ("now_ns", C.c_uint64),
+                ("tailroom", C.c_uint32), ("cookie_key", C.c_uint32), ("rsvd", C.c_uint32 * 4)]
+
+
 class XdpGpuError(RuntimeError):
     pass
 
@@ -155,7 +161,7 @@ EXPORTS = (
     "xdpgpu_pool_spec_default", "xdpgpu_hints_dev", "xdpgpu_host_alloc",
     "xdpgpu_host_free", "xdpgpu_jhash2_dev", "xdpgpu_jhash_nwords_dev",
     "xdpgpu_queue_stats", "xdpgpu_nat64_dynamic", "xdpgpu_nat64_clock",
-    "xdpgpu_nat64_state", "xdpgpu_nat64_direction",
+    "xdpgpu_nat64_state", "xdpgpu_nat64_direction", "xdpgpu_synproxy_dev",
 )
 
 # struct xdpgpu_hints (XDP hints in front of a frame)
@@ -194,6 +200,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.xdpgpu_nat64_setup.argtypes = [vp, C.POINTER(Nat64Cfg), vp, u32]
     lib.xdpgpu_nat64_dev.argtypes = [vp, vp, u64, vp, u32, vp, vp, vp]
     lib.xdpgpu_nat64_pool_config.argtypes = [u32, C.POINTER(Nat64Cfg), vp, u32]
+    lib.xdpgpu_synproxy_dev.argtypes = [vp, vp, u64, vp, u32, C.POINTER(SynproxyCfg), vp, vp,
+                                        vp, vp]
     lib.xdpgpu_nat64_dynamic.argtypes = [vp, C.POINTER(Nat64Dyn)]
     lib.xdpgpu_nat64_clock.argtypes = [vp, u64]
     lib.xdpgpu_nat64_direction.argtypes = [vp, u32]
@@ -408,6 +416,12 @@ class XdpGpu:
             self.h, ent.ctypes.data if n.value else None, n.value, C.byref(n), C.byref(d),
             q.ctypes.data if nq.value else None, nq.value, C.byref(nq)), "xdpgpu_nat64_state")
         return ent, int(d.next_addr), q
+
+    def synproxy_dev(self, umem, umem_size: int, descs, n: int, cfg: "SynproxyCfg",
+                     verdict, out, synacks=None, stream=None) -> None:
+        self._check(self.lib.xdpgpu_synproxy_dev(
+            self.h, _ptr(umem), umem_size, _ptr(descs), n, C.byref(cfg), _ptr(verdict),
+            _ptr(out), _ptr(synacks), _stream_handle(stream)), "xdpgpu_synproxy_dev")
 
     def ceiling_dev(self, umem, umem_size: int, descs, n: int, verdict, res,
                     tup, stream=None) -> None:

@@ -409,6 +409,42 @@ int xdpgpu_nat64_state(struct xdpgpu_ctx *ctx, struct xdpgpu_nat64_entry *out,
 		       uint32_t *queue, uint32_t qmax, uint32_t *nq);
 
 /* ------------------------------------------------------------------ */
+/* SYN proxy (xdp-synproxy/xdp_synproxy_kern.c, syncookie_xdp): a SYN to an
+ * allowed port is answered in place with a SYN-ACK carrying a cookie (the
+ * TCP checksum verify and recompute path), an ACK is
+ * checked against the cookie, other traffic passes.                     */
+
+/* The reference program's maps and clock.  Two things it takes from the
+ * kernel are outside this transform (xdp-synproxy row):
+ * the conntrack lookup (bpf_xdp_ct_lookup, :430-478; every frame is taken
+ * as not established, the answer for a new connection) and the kernel's
+ * SYN cookie (bpf_tcp_raw_gen/check_syncookie_*, :627-641, :717-734),
+ * replaced by a build-defined keyed cookie: jhash2 over the source and
+ * destination address words and the ports, with initval cookie_key +
+ * now_ns / 60 s, plus the client's sequence number; an ACK passes when its
+ * ack_seq - 1 matches that cookie for the current or the previous minute. */
+struct xdpgpu_synproxy_cfg {
+	uint64_t values;           /* values[0] (:76-81, :310-330): 0 = the
+				    * defaults, else mss4 | wscale << 16 |
+				    * ttl << 24 | mss6 << 32                */
+	uint16_t ports[8];         /* allowed_ports (:83-88), 0 terminates   */
+	uint64_t now_ns;           /* bpf_ktime_get_ns() for the batch       */
+	uint32_t tailroom;         /* bytes each frame may grow past its end
+				    * (the chunk's room, bpf_xdp_adjust_tail) */
+	uint32_t cookie_key;
+	uint32_t rsvd[4];
+};
+
+/* Process frames in place (device pointers): d_verdict[i] the XDP action
+ * (XDP_TX: a SYN-ACK was written over the frame), d_out[i] the frame's
+ * descriptor after the program's bpf_xdp_adjust_tail calls.  d_synacks
+ * (device u64, may be NULL) is incremented per SYN-ACK (values[1]). */
+int xdpgpu_synproxy_dev(struct xdpgpu_ctx *ctx, void *d_umem, uint64_t umem_size,
+			const struct xdpgpu_desc *d_descs, uint32_t n,
+			const struct xdpgpu_synproxy_cfg *cfg, uint8_t *d_verdict,
+			struct xdpgpu_desc *d_out, uint64_t *d_synacks, void *stream);
+
+/* ------------------------------------------------------------------ */
 /* Synthetic UMEM pool generator (host).  Replaces the reference's packet
  * generators gen_eth_hdr_data (xdpsock.c:893-971) and gen_base_pkt
  * (af_xdp_user.c:688-700) for pool mode.                              */

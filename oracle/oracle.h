@@ -71,6 +71,11 @@ int oracle_nat64_dyn(uint8_t *umem, uint64_t umem_size,
 int oracle_nat64_state_read(const struct oracle_nat64_state *st,
 			    struct xdpgpu_nat64_entry *out, uint32_t max, uint32_t *n,
 			    uint64_t *next_addr, uint32_t *queue, uint32_t qmax, uint32_t *nq);
+/* SYN proxy (synproxy_oracle.c): same inputs and outputs as
+ * xdpgpu_synproxy_dev, frames rewritten in place */
+int oracle_synproxy(uint8_t *umem, uint64_t umem_size, const struct xdpgpu_desc *descs,
+		    uint32_t n, const struct xdpgpu_synproxy_cfg *cfg, uint8_t *verdict,
+		    struct xdpgpu_desc *out, uint64_t *synacks);
 int oracle_v4addr_to_v6(const uint8_t a4[4], uint8_t a6[16],
 			const uint8_t pref[16], int plen);
 int oracle_v6addr_to_v4(const uint8_t a6[16], int plen, uint8_t a4[4],

@@ -97,6 +97,7 @@ def lib() -> C.CDLL:
                                        vp, vp]
         o.oracle_nat64_state_read.argtypes = [vp, vp, u32, C.POINTER(u32),
                                               C.POINTER(u64), vp, u32, C.POINTER(u32)]
+        o.oracle_synproxy.argtypes = [vp, u64, vp, u32, vp, vp, vp, C.POINTER(u64)]
         o.oracle_hints.argtypes = [vp, u64, vp, u32, u32, u32, vp]
         o.oracle_v4addr_to_v6.argtypes = [vp, vp, vp, C.c_int]
         o.oracle_v6addr_to_v4.argtypes = [vp, C.c_int, vp, vp]
@@ -252,6 +253,20 @@ class Nat64State:
 
     def __del__(self):
         self.close()
+
+
+def synproxy(umem: np.ndarray, descs: np.ndarray, cfg):
+    """The SYN proxy oracle in place on umem: (verdict, out descs, synacks).
+    cfg: xdpgpu.SynproxyCfg (the same C layout)."""
+    descs = np.ascontiguousarray(descs, DESC_DTYPE)
+    n = len(descs)
+    verdict = np.zeros(n, np.uint8)
+    out = np.zeros(n, DESC_DTYPE)
+    cnt = C.c_uint64(0)
+    lib().oracle_synproxy(umem.ctypes.data, umem.nbytes, descs.ctypes.data, n,
+                          C.addressof(cfg), verdict.ctypes.data, out.ctypes.data,
+                          C.byref(cnt))
+    return verdict, out, int(cnt.value)
 
 
 def hints(umem: np.ndarray, descs: np.ndarray, rx_time_id: int, mark_id: int):

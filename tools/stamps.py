@@ -40,9 +40,10 @@ for rep in range(6):
 s4 = st.reshape(-1, 8)
 live = s4[:, 0] > 0
 hw = s4[live, 3]
-s = s4[live][:, [0, 1, 2, 4, 5]].astype(np.int64)
+s = s4[live][:, [0, 1, 2]].astype(np.int64)
 t0 = s[:, 0].min()
 us = (s - t0) / 100.0            # 100 MHz ticks -> us
+ph = s4[live][:, 4:8].astype(np.int64) / 100.0   # tail time per batch kind
 waves = np.nonzero(live)[0]
 xcd = (waves // 4) % 8
 
@@ -52,8 +53,9 @@ def pct(a):
 
 
 out = {"waves": int(live.sum()), "tail_us": pct(us[:, 2] - us[:, 1]),
-       "tail_exception_us": pct(us[:, 3] - us[:, 1]), "tail_bulk_us": pct(us[:, 4] - us[:, 3]),
-       "tail_payload_us": pct(us[:, 2] - us[:, 4]), "start_us": pct(us[:, 0]), "loop_end_us": pct(us[:, 1]),
+       "tail_exception_us": pct(ph[:, 0]), "tail_bulk_us": pct(ph[:, 1]),
+       "tail_payload_us": pct(ph[:, 2]), "tail_wait_us": pct(ph[:, 3]),
+       "start_us": pct(us[:, 0]), "loop_end_us": pct(us[:, 1]),
        "end_us": pct(us[:, 2]), "loop_us": pct(us[:, 1] - us[:, 0])}
 out["per_xcd_loop_end_median"] = [round(float(np.median(us[xcd == k, 1])), 1) for k in range(8)]
 out["per_xcd_loop_end_max"] = [round(float(us[xcd == k, 1].max()), 1) for k in range(8)]
