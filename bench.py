@@ -292,6 +292,95 @@ def nat64_run(dev, stream, n, steps, local):
     return out
 
 
+def synflood_pool(n: int, seed: int):
+    """n IPv4 SYNs (74 B: MSS, SACK_PERM, timestamp, window scale options,
+    a Linux client's SYN) at a 128-byte stride, random source address, port,
+    sequence number and timestamp, valid checksums; SYN proxy leg."""
+    rng = np.random.default_rng(seed)
+    t = np.zeros((n, 74), np.uint8)
+    t[:, 0:14] = np.frombuffer(bytes([2, 0, 0, 0, 0, 1, 2, 0, 0, 0, 0, 2, 8, 0]), np.uint8)
+    t[:, 14:34] = np.frombuffer(bytes([0x45, 0, 0, 60, 0, 0, 0x40, 0, 64, 6, 0, 0,
+                                       10, 0, 0, 0, 10, 1, 0, 1]), np.uint8)
+    src = rng.integers(0, 1 << 16, n)
+    t[:, 28], t[:, 29] = src >> 8, src & 0xFF
+    t[:, 34:74] = np.frombuffer(bytes([0, 0, 0, 80, 0, 0, 0, 0, 0, 0, 0, 0, 0xA0, 0x02,
+                                       0xFF, 0xFF, 0, 0, 0, 0, 2, 4, 5, 0xB4, 4, 2, 8, 10,
+                                       0, 0, 0, 0, 0, 0, 0, 0, 1, 3, 3, 7]), np.uint8)
+    sport = rng.integers(1024, 1 << 16, n)
+    t[:, 34], t[:, 35] = sport >> 8, sport & 0xFF
+    t[:, 38:42] = rng.integers(0, 256, (n, 4), dtype=np.uint8)      # seq
+    t[:, 62:66] = rng.integers(0, 256, (n, 4), dtype=np.uint8)      # TSval
+
+    def csum(words):
+        s = words.sum(1, dtype=np.uint64)
+        while True:
+            hi = s >> np.uint64(16)
+            if not hi.any():
+                break
+            s = (s & np.uint64(0xFFFF)) + hi
+        return (~s.astype(np.uint32)) & 0xFFFF
+
+    def be_words(a):
+        a = a.astype(np.uint32)
+        return (a[:, 0::2] << 8) | a[:, 1::2]
+
+    c = csum(be_words(t[:, 14:34]))
+    t[:, 24], t[:, 25] = c >> 8, c & 0xFF
+    pseudo = np.concatenate([be_words(t[:, 26:34]),
+                             np.full((n, 1), 6 + 40, np.uint32)], 1)
+    c = csum(np.concatenate([be_words(t[:, 34:74]), pseudo], 1))
+    t[:, 50], t[:, 51] = c >> 8, c & 0xFF
+    umem = np.zeros(n * 128 + 64, np.uint8)
+    umem[:n * 128].reshape(n, 128)[:, :74] = t
+    descs = np.zeros(n, xdpgpu.DESC_DTYPE)
+    descs["addr"] = np.arange(n, dtype=np.uint64) * 128
+    descs["len"] = 74
+    return umem, descs
+
+
+def synproxy_run(dev, stream, n, steps, local):
+    """SYN proxy (xdp_synproxy_kern.c): n SYNs answered in place with
+    SYN-ACKs.  Like nat64, the pool is restored from a pristine device
+    copy before each launch (outside the timed region)."""
+    u, ds = synflood_pool(n, 0x5EED0007)
+    pristine = to_dev(u, dev)
+    work = torch.empty_like(pristine)
+    d_desc = to_dev(ds, dev, 0)
+    d_v = torch.empty(n, dtype=torch.uint8, device=dev)
+    d_out = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    d_cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    c = xdpgpu.SynproxyCfg()
+    c.ports[0] = 80
+    c.now_ns = 10**18
+    c.tailroom = 128 - 74
+    c.cookie_key = 0x5EED
+    ms = []
+    with xdpgpu.XdpGpu(local) as g:
+        for k in range(steps + 2):
+            with torch.cuda.stream(stream):
+                work.copy_(pristine, non_blocking=True)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            g.synproxy_dev(work, u.nbytes, d_desc, n, c, d_v, d_out, d_cnt, stream)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            if k >= 2:
+                ms.append(e0.elapsed_time(e1))
+    v = d_v.cpu().numpy()
+    t = float(np.mean(ms))
+    # read 16 (descriptor) + 74 (SYN), write 74 (SYN-ACK) + 16 (descriptor) + 1
+    algo = n * (16 + 74 + 74 + 16 + 1)
+    out = {"workload": f"{n} x 74B IPv4 SYNs (MSS/SACK/TS/WS options) at a 128B stride, "
+                       "SYN-ACK written in place (xdp_synproxy_kern.c)",
+           "frames": n, "mpps": round(n / t / 1e3, 1), "kernel_ms": round(t, 4),
+           "algorithmic_bytes_per_launch": algo, "gbps": round(algo / t / 1e6, 1),
+           "roofline_frac": round(algo / t / 1e6 / HBM_PEAK_GBS, 4),
+           "all_synack": bool((v == 3).all())}
+    del pristine, work, d_desc, d_v, d_out
+    torch.cuda.empty_cache()
+    return out
+
+
 def frags_run(dev, stream, n, steps, local, size=9000, chunk=4096):
     """Multi-buffer packets (XDPGPU_CFG_FRAGS): n jumbo frames, each cut in
     place into fragments of at most `chunk` bytes (XDP_PKT_CONTD on all but
@@ -386,7 +475,7 @@ def main():
     ap.add_argument("--window", type=int, default=64)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
-    ap.add_argument("--legs", default="1500,imix,nat64,frags,echo",
+    ap.add_argument("--legs", default="1500,imix,nat64,frags,echo,synproxy",
                     help="secondary workloads: comma list of 1500, imix, nat64, frags, echo")
     ap.add_argument("--imix-frames", type=int, default=16 << 20)
     ap.add_argument("--nat64-frames", type=int, default=16 << 20)
@@ -463,6 +552,8 @@ def main():
             secondary["multibuffer_9000B"] = frags_run(dev, stream, 1 << 16, steps2, local)
         if "echo" in legs:
             secondary["icmp6_echo"] = echo_run(dev, stream, 8 << 20, steps2, local)
+        if "synproxy" in legs:
+            secondary["synproxy"] = synproxy_run(dev, stream, 8 << 20, steps2, local)
 
     e2e = None
     if args.e2e and rank == 0 and world == 1:

@@ -4,8 +4,9 @@
  * program of xdp-synproxy/xdp_synproxy_kern.c (syncookie_xdp, :803-819)
  * over a batch of UMEM frames, one lane per frame.
  *
- * A lane stages its frame's first kRow bytes in an LDS row (16-byte loads
- * for 16-byte aligned frames, bytes otherwise), runs the program on the row
+ * A lane stages its frame's first kRow bytes in an LDS row (the wave's
+ * 16-byte aligned frames cooperatively, whole 16-byte chunks; others byte
+ * by byte), runs the program on the row
  * (TCP option bytes past the row are read from the UMEM, bytes past the
  * frame's end as the zeros bpf_xdp_adjust_tail grows it with), and writes
  * back what changed: the SYN-ACK's headers (at most 14 + 40 + 40 bytes, all
@@ -390,24 +391,41 @@ __global__ __launch_bounds__(kBlockS) void synproxy_kernel(uint8_t *umem, uint64
 	const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
 	const bool valid = active && (uint64_t)len <= usize && eff <= usize - len;
 	bool synack = false;
+	/* stage [0, kRow) of every lane's frame: 16-byte aligned frames whose
+	 * row lies in the UMEM cooperatively (q = 64 k + lane: chunk q % 9 of
+	 * frame q / 9, nine lanes per frame reading its 144 bytes as whole
+	 * chunks), the others byte by byte; zeros past each frame's end */
+	__shared__ uint64_t dtab_all[kBlockS];
+	uint64_t *dtab = dtab_all + (threadIdx.x & ~63u);
+	const int lane = threadIdx.x & 63;
+	const uint64_t us16 = usize & ~15ull;
+	const bool coop = valid && !(eff & 15) && eff + kRow <= us16;
+	dtab[lane] = coop ? eff : ~0ull;
+	__builtin_amdgcn_wave_barrier();
+	for (int k = 0; k < 9; k++) {
+		const int q = 64 * k + lane;
+		const int f = q / 9, c = q - 9 * (q / 9);
+		const uint64_t base = dtab[f];
+		if (base != ~0ull) {
+			const uint4 v = *reinterpret_cast<const uint4 *>(umem + base + 16 * c);
+			uint32_t *d = rows + ((threadIdx.x & ~63u) + f) * kRowDw + 4 * c;
+			d[0] = v.x;
+			d[1] = v.y;
+			d[2] = v.z;
+			d[3] = v.w;
+		}
+	}
+	__builtin_amdgcn_wave_barrier();
 	if (valid) {
 		uint8_t *g = umem + eff;
-		/* stage [0, kRow): the frame's bytes, zeros past its end */
-		const uint32_t st = len < (uint32_t)kRow ? len : (uint32_t)kRow;
-		if (!(eff & 3)) {
+		uint32_t *rw = rows + threadIdx.x * kRowDw;
+		if (coop) {
 			for (uint32_t w = 0; w < (uint32_t)kRow / 4; w++) {
-				uint32_t v = 0;
-				if (4 * w < st) {
-					if (4 * w + 4 <= len) {
-						v = *reinterpret_cast<const uint32_t *>(g + 4 * w);
-					} else {
-						for (uint32_t k = 4 * w; k < len; k++)
-							v |= (uint32_t)g[k] << (8 * (k - 4 * w));
-					}
-				}
-				*reinterpret_cast<uint32_t *>(row + 4 * w) = v;
+				if (4 * w + 4 > len)
+					rw[w] = 4 * w >= len ? 0u : rw[w] & (0xffffffffu >> (8 * (4 * w + 4 - len)));
 			}
 		} else {
+			const uint32_t st = len < (uint32_t)kRow ? len : (uint32_t)kRow;
 			for (uint32_t k = 0; k < (uint32_t)kRow; k++)
 				row[k] = k < st ? g[k] : 0;
 		}
