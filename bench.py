@@ -16,15 +16,16 @@ launch's kernel time from HIP events recorded on the launch stream around
 the kernel (xdpgpu_kernel_times), in a second pass of K launches on a
 context with XDPGPU_CFG_TIMING so the events do not perturb the timed
 steps.  traffic is the HBM bytes per launch from the committed rocprofv3
-PMC summary (profiles/*_pmc.json, tools/pmc_profile.sh).  The CPU baseline
+PMC summary (profiles/r<NN>_pmc.json, tools/pmc_profile.sh).  The CPU baseline
 is the lean CPU leg (oracle/cpu_leg.c: the same outputs as the oracle,
 checked on the sample) on this host's cores, rank 0 at N = 1 only, on a
 bounded sample: one pinned thread, then one thread per CPU of the affinity
 set, with the CPU model and the calibration probe beside the reference
 headers' own routines (oracle/_ref).  Secondary lines: config 2 geometry
 at 1500 B, config 3 (16 M IMIX, 44 B network_tuple), config 4 (16 M x
-128 B nat64 ingress), multi-buffer 9000 B packets and the ICMPv6 echo
-responder.
+128 B nat64 ingress, static and dynamic state), multi-buffer 9000 B
+packets, the ICMPv6 echo responder and the SYN proxy (8 M SYNs answered
+with SYN-ACKs).
 """
 from __future__ import annotations
 

@@ -25,7 +25,7 @@ namespace {
 
 constexpr int kRow = 144;                 /* staged bytes per frame */
 constexpr int kRowDw = kRow / 4 + 1;      /* odd dword stride: no bank conflicts */
-constexpr int kBlockS = 256;
+constexpr int kBlockS = 64;      /* one wave: LDS rows bound the CU to 15 waves */
 
 enum { SP_ABORTED = 0, SP_DROP = 1, SP_PASS = 2, SP_TX = 3 };
 
@@ -43,12 +43,24 @@ struct Frame {
 		return i < len0 ? g[i] : 0u;
 	}
 	__device__ void put(uint32_t i, uint32_t v) const { row[i] = (uint8_t)v; }
-	__device__ uint32_t be16(uint32_t i) const { return b(i) << 8 | b(i + 1); }
-	__device__ uint32_t be32(uint32_t i) const { return be16(i) << 16 | be16(i + 2); }
+	/* the LE word at byte i: two aligned LDS dwords and a byte align
+	 * inside the row (the row's dword after the last is in the row's
+	 * padding dword) */
 	__device__ uint32_t le32(uint32_t i) const
 	{
+		if (i + 4 <= (uint32_t)kRow) {
+			const uint32_t *w = reinterpret_cast<const uint32_t *>(row);
+			const uint32_t lo = w[i >> 2], hi = w[(i >> 2) + 1];
+			return __builtin_amdgcn_alignbyte(hi, lo, i & 3);
+		}
 		return b(i) | b(i + 1) << 8 | b(i + 2) << 16 | b(i + 3) << 24;
 	}
+	__device__ uint32_t be16(uint32_t i) const
+	{
+		const uint32_t v = le32(i);
+		return (v & 0xff) << 8 | ((v >> 8) & 0xff);
+	}
+	__device__ uint32_t be32(uint32_t i) const { return __builtin_bswap32(le32(i)); }
 	__device__ void put_be16(uint32_t i, uint32_t v) const
 	{
 		put(i, v >> 8);
@@ -62,7 +74,7 @@ struct Frame {
 };
 
 /* bpf_csum_diff(0, 0, p, n, 0): LE words, 64-bit accumulation */
-__device__ uint64_t sum32(const Frame &F, uint32_t at, uint32_t n)
+__device__ __forceinline__ uint64_t sum32(const Frame &F, uint32_t at, uint32_t n)
 {
 	uint64_t s = 0;
 	for (uint32_t i = 0; i + 4 <= n; i += 4)
@@ -71,7 +83,7 @@ __device__ uint64_t sum32(const Frame &F, uint32_t at, uint32_t n)
 }
 
 /* csum_fold (xdp_synproxy_kern.c:121-126) of a 64-bit sum */
-__device__ uint32_t fold(uint64_t s)
+__device__ __forceinline__ uint32_t fold(uint64_t s)
 {
 	s = (s & 0xffffffffu) + (s >> 32);
 	s = (s & 0xffffffffu) + (s >> 32);
@@ -82,7 +94,7 @@ __device__ uint32_t fold(uint64_t s)
 }
 
 /* csum_tcpudp_magic (:128-147, little-endian) / csum_ipv6_magic (:149-172) */
-__device__ uint32_t l4_magic(const Frame &F, uint32_t ip, bool v6, uint32_t len,
+__device__ __forceinline__ uint32_t l4_magic(const Frame &F, uint32_t ip, bool v6, uint32_t len,
 			     uint64_t body)
 {
 	uint64_t s = body;
@@ -100,7 +112,7 @@ __device__ uint32_t l4_magic(const Frame &F, uint32_t ip, bool v6, uint32_t len,
 }
 
 /* the build-defined cookie (include/xdpgpu.h) */
-__device__ uint32_t cookie_hash(const Frame &F, uint32_t ip, bool v6, uint32_t tcp,
+__device__ __forceinline__ uint32_t cookie_hash(const Frame &F, uint32_t ip, bool v6, uint32_t tcp,
 				uint32_t key, uint32_t count)
 {
 	uint32_t w[9];
@@ -116,7 +128,21 @@ __device__ uint32_t cookie_hash(const Frame &F, uint32_t ip, bool v6, uint32_t t
 		w[4] = F.le32(ip + 16);
 	}
 	w[8] = F.be16(tcp) << 16 | F.be16(tcp + 2);
-	return jhash2_dev(w, 9, key + count);
+	/* jhash2(w, 9, key + count), unrolled (include/jhash.h:114-142) */
+	uint32_t a = 0xdeadbeefu + (9u << 2) + key + count, b = a, c = a;
+	a += w[0];
+	b += w[1];
+	c += w[2];
+	JH_MIX(a, b, c);
+	a += w[3];
+	b += w[4];
+	c += w[5];
+	JH_MIX(a, b, c);
+	c += w[8];
+	b += w[7];
+	a += w[6];
+	JH_FINAL(a, b, c);
+	return c;
 }
 
 struct Opt {
@@ -125,7 +151,7 @@ struct Opt {
 };
 
 /* next() (:199-215) */
-__device__ bool next(Opt &c, uint32_t sz, uint32_t &at)
+__device__ __forceinline__ bool next(Opt &c, uint32_t sz, uint32_t &at)
 {
 	if (c.off > 0xffffu - sz || c.off + sz >= c.end)
 		return false;
@@ -135,7 +161,7 @@ __device__ bool next(Opt &c, uint32_t sz, uint32_t &at)
 }
 
 /* tscookie_tcpopt_parse (:217-262): true ends the walk */
-__device__ bool opt_parse(Opt &c, const Frame &F)
+__device__ __forceinline__ bool opt_parse(Opt &c, const Frame &F)
 {
 	const uint32_t off = c.off;
 	uint32_t op, sz, v;
@@ -151,28 +177,33 @@ __device__ bool opt_parse(Opt &c, const Frame &F)
 	const uint32_t osz = F.b(sz);
 	if (osz < 2)
 		return true;
+	/* the fields are updated by value (a conditional store to one of
+	 * them through a selected address would put the struct in scratch) */
+	uint32_t wscale = c.wscale, ts = c.ts, sack = c.sack, tsecr = c.tsecr;
 	if (code == 3) {
 		if (!next(c, 1, v))
 			return true;
-		if (osz == 3)
-			c.wscale = F.b(v) < 14 ? F.b(v) : 14;
+		const uint32_t x = F.b(v);
+		wscale = osz == 3 ? (x < 14 ? x : 14) : wscale;
 	} else if (code == 8) {
 		if (!next(c, 4, v))
 			return true;
-		if (osz == 10) {
-			c.ts = 1;
-			c.tsecr = F.le32(v);
-		}
+		const uint32_t x = F.le32(v);
+		ts = osz == 10 ? 1u : ts;
+		tsecr = osz == 10 ? x : tsecr;
 	} else if (code == 4) {
-		if (osz == 2)
-			c.sack = 1;
+		sack = osz == 2 ? 1u : sack;
 	}
+	c.wscale = wscale;
+	c.ts = ts;
+	c.sack = sack;
+	c.tsecr = tsecr;
 	c.off = off + osz;
 	return false;
 }
 
 /* syncookie_handle_syn (:577-715); len is the grown length */
-__device__ uint32_t handle_syn(const Frame &F, uint32_t &len, uint32_t ip, bool v6,
+__device__ __forceinline__ uint32_t handle_syn(const Frame &F, uint32_t &len, uint32_t ip, bool v6,
 			       uint32_t tcp, const xdpgpu_synproxy_cfg &cfg, bool &synack)
 {
 	uint32_t tcp_len = (F.b(tcp + 12) >> 4) * 4;
@@ -295,7 +326,7 @@ __device__ uint32_t handle_syn(const Frame &F, uint32_t &len, uint32_t ip, bool 
 }
 
 /* syncookie_handle_ack (:717-734), the build-defined cookie check */
-__device__ uint32_t handle_ack(const Frame &F, uint32_t ip, bool v6, uint32_t tcp,
+__device__ __forceinline__ uint32_t handle_ack(const Frame &F, uint32_t ip, bool v6, uint32_t tcp,
 			       const xdpgpu_synproxy_cfg &cfg)
 {
 	if (F.b(tcp + 13) & 0x04)
@@ -309,7 +340,7 @@ __device__ uint32_t handle_ack(const Frame &F, uint32_t ip, bool v6, uint32_t tc
 }
 
 /* syncookie_xdp (:803-819): part1 (:736-767), part2 (:769-801) */
-__device__ uint32_t sp_frame(const Frame &F, uint32_t &len, uint64_t room,
+__device__ __forceinline__ uint32_t sp_frame(const Frame &F, uint32_t &len, uint64_t room,
 			     const xdpgpu_synproxy_cfg &cfg, bool &synack, uint32_t &grow)
 {
 	grow = 0;
@@ -346,15 +377,16 @@ __device__ uint32_t sp_frame(const Frame &F, uint32_t &len, uint64_t room,
 		return SP_DROP;
 	if (!v6 && (F.be16(ip + 6) & 0x7fff) != 0x4000)
 		return SP_DROP;
-	bool allowed = false;
+	/* check_port_allowed (:342-365): the list up to its first 0 (constant
+	 * indices: a loop with an early exit indexes the argument's array
+	 * dynamically, which puts it in scratch memory) */
+	bool allowed = false, live = true;
 	const uint32_t port = F.be16(tcp + 2);
+#pragma unroll
 	for (int i = 0; i < 8; i++) {
-		if (cfg.ports[i] == 0)
-			break;
-		if (cfg.ports[i] == port) {
-			allowed = true;
-			break;
-		}
+		const uint32_t pv = cfg.ports[i];
+		live = live && pv != 0;
+		allowed = allowed || (live && pv == port);
 	}
 	if (!allowed)
 		return SP_PASS;
@@ -374,14 +406,14 @@ __device__ uint32_t sp_frame(const Frame &F, uint32_t &len, uint64_t room,
 		   : handle_ack(F, ip, v6, tcp, cfg);
 }
 
-__global__ __launch_bounds__(kBlockS) void synproxy_kernel(uint8_t *umem, uint64_t usize,
-							   const xdpgpu_desc *desc, uint32_t n,
-							   xdpgpu_synproxy_cfg cfg, uint8_t *verdict,
-							   xdpgpu_desc *out,
-							   unsigned long long *synacks)
+/* one tile of kBlockS frames (one wave) from frame t0 on; true: this
+ * lane's frame was answered with a SYN-ACK */
+__device__ __forceinline__ bool sp_tile(uint8_t *umem, uint64_t usize, const xdpgpu_desc *desc,
+					uint32_t n, const xdpgpu_synproxy_cfg &cfg,
+					uint8_t *verdict, xdpgpu_desc *out, uint32_t *rows,
+					uint64_t *dtab_all, uint2 *wtab_all, uint64_t t0)
 {
-	__shared__ uint32_t rows[kBlockS * kRowDw];
-	const uint64_t i = (uint64_t)blockIdx.x * kBlockS + threadIdx.x;
+	const uint64_t i = t0 + threadIdx.x;
 	const bool active = i < n;
 	uint8_t *row = reinterpret_cast<uint8_t *>(rows + threadIdx.x * kRowDw);
 	const uint4 dv = active ? *reinterpret_cast<const uint4 *>(desc + i)
@@ -391,11 +423,11 @@ __global__ __launch_bounds__(kBlockS) void synproxy_kernel(uint8_t *umem, uint64
 	const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
 	const bool valid = active && (uint64_t)len <= usize && eff <= usize - len;
 	bool synack = false;
+	uint32_t ws = 0, we = 0;   /* the byte range to write back (coop frames) */
 	/* stage [0, kRow) of every lane's frame: 16-byte aligned frames whose
 	 * row lies in the UMEM cooperatively (q = 64 k + lane: chunk q % 9 of
 	 * frame q / 9, nine lanes per frame reading its 144 bytes as whole
 	 * chunks), the others byte by byte; zeros past each frame's end */
-	__shared__ uint64_t dtab_all[kBlockS];
 	uint64_t *dtab = dtab_all + (threadIdx.x & ~63u);
 	const int lane = threadIdx.x & 63;
 	const uint64_t us16 = usize & ~15ull;
@@ -436,46 +468,130 @@ __global__ __launch_bounds__(kBlockS) void synproxy_kernel(uint8_t *umem, uint64
 		uint32_t grow = 0;
 		const uint32_t len0 = len;
 		const uint32_t act = sp_frame(F, len, room, cfg, synack, grow);
-		if (act == SP_TX) {
-			/* the SYN-ACK, and the rest of the growth as zeros */
-			const uint32_t end = len > len0 + grow ? len : len0 + grow;
-			for (uint32_t k = 0; k < end && k < (uint32_t)kRow; k++)
-				g[k] = row[k];
-			for (uint32_t k = len0 > (uint32_t)kRow ? len0 : (uint32_t)kRow;
-			     k < len0 + grow; k++)
+		/* the bytes to write back: the SYN-ACK and the rest of the growth
+		 * (zeros), or the growth of a frame passed or dropped after it */
+		ws = act == SP_TX ? 0u : len0;
+		we = grow ? len0 + grow : 0u;
+		if (act == SP_TX && len > we)
+			we = len;
+		if (we > (uint32_t)kRow) {
+			/* past the row: zeros of the growth only */
+			for (uint32_t k = len0 > (uint32_t)kRow ? len0 : (uint32_t)kRow; k < we; k++)
 				g[k] = 0;
-		} else if (grow) {
-			/* grown by bpf_xdp_adjust_tail, then passed or dropped */
-			for (uint32_t k = 0; k < grow; k++)
-				g[len0 + k] = 0;
+			we = kRow;
+		}
+		if (!coop) {
+			for (uint32_t k = ws; k < we; k++)
+				g[k] = row[k];
+			ws = we = 0;
 		}
 		verdict[i] = (uint8_t)act;
 	} else if (active) {
 		verdict[i] = SP_ABORTED;
+	}
+	/* cooperative write-back of the 16-byte aligned frames' ranges
+	 * [ws, we) from their rows: whole chunks as 16-byte stores, the
+	 * partial ones by dwords and bytes */
+	uint2 *wtab = wtab_all + (threadIdx.x & ~63u);
+	wtab[lane] = make_uint2(ws, we);
+	__builtin_amdgcn_wave_barrier();
+	for (int k = 0; k < 9; k++) {
+		const int q = 64 * k + lane;
+		const int f = q / 9, c = q - 9 * (q / 9);
+		const uint2 r = wtab[f];
+		const uint32_t lo = 16 * c, hi = lo + 16;
+		if (r.y <= lo || r.x >= hi)
+			continue;
+		const uint64_t base = dtab[f];
+		const uint32_t *src = rows + ((threadIdx.x & ~63u) + f) * kRowDw + 4 * c;
+		uint8_t *dst = umem + base + lo;
+		if (r.x <= lo && r.y >= hi) {
+			*reinterpret_cast<uint4 *>(dst) = make_uint4(src[0], src[1], src[2], src[3]);
+		} else {
+			const uint32_t a0 = r.x > lo ? r.x - lo : 0u;
+			const uint32_t b0 = r.y < hi ? r.y - lo : 16u;
+			for (uint32_t j = a0; j < b0; j++) {
+				if (!(j & 3) && j + 4 <= b0) {
+					*reinterpret_cast<uint32_t *>(dst + j) = src[j >> 2];
+					j += 3;
+				} else {
+					dst[j] = (uint8_t)(src[j >> 2] >> (8 * (j & 3)));
+				}
+			}
+		}
 	}
 	if (active) {
 		uint4 od = dv;
 		od.z = len;
 		*reinterpret_cast<uint4 *>(out + i) = od;
 	}
-	/* values[1] (values_inc_synacks, :332-340): one atomic per wave */
+	__builtin_amdgcn_wave_barrier();
+	return synack;
+}
+
+/* One wave per tile.  The SYN-ACK count (values[1], values_inc_synacks,
+ * :332-340) goes to one of kSpread counters picked by the block index (one
+ * atomic per wave on a single word serialised the launch: 1.7 ms per 8 M
+ * SYNs), which synproxy_sum_kernel adds to the caller's counter. */
+constexpr int kSpread = 256;
+__global__ __launch_bounds__(kBlockS) void synproxy_kernel(uint8_t *umem, uint64_t usize,
+							   const xdpgpu_desc *desc, uint32_t n,
+							   xdpgpu_synproxy_cfg cfg, uint8_t *verdict,
+							   xdpgpu_desc *out,
+							   unsigned long long *spread)
+{
+	__shared__ uint32_t rows[kBlockS * kRowDw];
+	__shared__ uint64_t dtab_all[kBlockS];
+	__shared__ uint2 wtab_all[kBlockS];
+	const bool synack = sp_tile(umem, usize, desc, n, cfg, verdict, out, rows, dtab_all,
+				    wtab_all, (uint64_t)blockIdx.x * kBlockS);
 	const uint64_t m = __ballot(synack);
-	if (synacks && m && (threadIdx.x & 63) == (uint32_t)(__builtin_ffsll((long long)m) - 1))
-		atomicAdd(synacks, (unsigned long long)__popcll(m));
+	if (spread && m && threadIdx.x == 0)
+		atomicAdd(spread + 16 * (blockIdx.x % kSpread), (unsigned long long)__popcll(m));
+}
+
+/* the spread counters into the caller's, and cleared for the next launch */
+__global__ void synproxy_sum_kernel(unsigned long long *spread, unsigned long long *synacks)
+{
+	unsigned long long v = spread[16 * threadIdx.x];
+	spread[16 * threadIdx.x] = 0;
+	for (int o = 32; o > 0; o >>= 1)
+		v += __shfl_xor(v, o);
+	__shared__ unsigned long long part[kSpread / 64];
+	if ((threadIdx.x & 63) == 0)
+		part[threadIdx.x / 64] = v;
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		unsigned long long t = 0;
+		for (int k = 0; k < kSpread / 64; k++)
+			t += part[k];
+		*synacks += t;
+	}
 }
 
 } // namespace
 
 hipError_t launch_synproxy(uint8_t *umem, uint64_t usize, const xdpgpu_desc *desc,
 			   uint32_t n, const xdpgpu_synproxy_cfg &cfg, uint8_t *verdict,
-			   xdpgpu_desc *out, unsigned long long *synacks, hipStream_t stream)
+			   xdpgpu_desc *out, unsigned long long *synacks,
+			   unsigned long long *spread, hipStream_t stream)
 {
 	const uint32_t blocks = (n + kBlockS - 1) / kBlockS;
 	if (!blocks)
 		return hipSuccess;
 	hipLaunchKernelGGL(synproxy_kernel, dim3(blocks), dim3(kBlockS), 0, stream, umem, usize,
-			   desc, n, cfg, verdict, out, synacks);
+			   desc, n, cfg, verdict, out, synacks ? spread : nullptr);
+	hipError_t e = hipGetLastError();
+	if (e != hipSuccess || !synacks)
+		return e;
+	hipLaunchKernelGGL(synproxy_sum_kernel, dim3(1), dim3(kSpread), 0, stream, spread,
+			   synacks);
 	return hipGetLastError();
+}
+
+uint32_t synproxy_spread_words()
+{
+	return 16 * kSpread;
 }
 
 } // namespace xdpgpu

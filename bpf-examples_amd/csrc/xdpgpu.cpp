@@ -112,6 +112,7 @@ struct xdpgpu_ctx {
 	uint64_t mcap = 0;
 	Nat64Patch *d_patch = nullptr;
 	uint64_t pcap = 0;
+	unsigned long long *d_spread = nullptr;   /* synproxy SYN-ACK counters */
 	uint32_t tn = 0;
 	char err[256];
 };
@@ -270,7 +271,7 @@ void xdpgpu_fini(xdpgpu_ctx *ctx)
 	if (ctx->d_v4map)
 		(void)hipFree(ctx->d_v4map);
 	for (void *p : {(void *)ctx->d_midx, (void *)ctx->d_msrc, (void *)ctx->d_mcnt,
-			(void *)ctx->d_mov, (void *)ctx->d_patch})
+			(void *)ctx->d_mov, (void *)ctx->d_patch, (void *)ctx->d_spread})
 		if (p)
 			(void)hipFree(p);
 	if (ctx->pinned)
@@ -1008,8 +1009,16 @@ int xdpgpu_synproxy_dev(xdpgpu_ctx *ctx, void *d_umem, uint64_t umem_size,
 		return 0;
 	HIP_TRY(ctx, hipSetDevice(ctx->cfg.device));
 	hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
+	if (d_synacks && !ctx->d_spread) {
+		/* the SYN-ACK counters, zeroed once: each launch's sum kernel
+		 * clears them (launches of one context are stream-ordered) */
+		const size_t bytes = (size_t)synproxy_spread_words() * 8;
+		if (hipMalloc(&ctx->d_spread, bytes) != hipSuccess)
+			return set_err(ctx, -ENOMEM, "synproxy counters");
+		HIP_TRY(ctx, hipMemset(ctx->d_spread, 0, bytes));
+	}
 	HIP_TRY(ctx, launch_synproxy((uint8_t *)d_umem, umem_size, d_descs, n, *cfg, d_verdict,
-				     d_out, (unsigned long long *)d_synacks, st));
+				     d_out, (unsigned long long *)d_synacks, ctx->d_spread, st));
 	return 0;
 }
 

@@ -358,7 +358,10 @@ hipError_t launch_ip_fast_csum(const uint8_t *hdrs, uint32_t stride,
 			       uint32_t n, uint16_t *out, hipStream_t stream);
 hipError_t launch_synproxy(uint8_t *umem, uint64_t usize, const xdpgpu_desc *desc,
 			   uint32_t n, const xdpgpu_synproxy_cfg &cfg, uint8_t *verdict,
-			   xdpgpu_desc *out, unsigned long long *synacks, hipStream_t stream);
+			   xdpgpu_desc *out, unsigned long long *synacks,
+			   unsigned long long *spread, hipStream_t stream);
+/* u64 words of the zeroed counter area launch_synproxy needs */
+uint32_t synproxy_spread_words();
 
 } // namespace xdpgpu
 

@@ -33,7 +33,9 @@ prof 1500 python3 tools/tune_rx.py --variants 64:0 --rounds 3 --frames 2097152 -
 prof imix python3 tools/tune_rx.py --variants 64:0 --rounds 3 --frames 16777216 --kind 1 --seed 0x5EED0003 --fmt 2
 prof nat64 python3 tools/nat64_probe.py --reps 5
 prof nat64_egress python3 tools/nat64_probe.py --reps 5 --direction 1
+prof nat64_dynamic python3 tools/nat_dyn_probe.py --frames 16777216 --reps 5
 prof frags python3 tools/frags_probe.py --reps 5
+prof synproxy python3 bench.py --no-cpu --legs synproxy --steps 5 --warmup 2
 step pmc 900 env DEST=$OUT/pmc_summary.json OUT=$OUT/pmc bash tools/pmc_profile.sh
 step pmc_imix 900 env DEST=$OUT/pmc_imix_summary.json OUT=$OUT/pmc_imix LABEL="config3 pool: 16777216 IMIX frames, 44-byte network_tuple (tools/tune_rx.py)" PMC_ARGS="--frames 16777216 --kind 1 --seed 0x5EED0003 --fmt 2" bash tools/pmc_profile.sh
 step e2e 600 python3 bench.py --no-cpu --no-secondary --steps 10 --e2e
