@@ -429,6 +429,19 @@ static int nl_talk(struct nlmsghdr *h)
 	return rc;
 }
 
+static void no_ipv6(const char *ifname)
+{
+	char path[128];
+	FILE *f;
+
+	snprintf(path, sizeof(path), "/proc/sys/net/ipv6/conf/%s/disable_ipv6", ifname);
+	f = fopen(path, "w");
+	if (f) {
+		fputs("1\n", f);
+		fclose(f);
+	}
+}
+
 int xsk_veth_create(const char *a, const char *b)
 {
 	struct nlreq q;
@@ -456,6 +469,11 @@ int xsk_veth_create(const char *a, const char *b)
 	rc = nl_talk(&q.h);
 	if (rc)
 		return rc;
+	/* no IPv6 on the pair: a new link's router solicitations, MLD
+	 * reports and DAD probes would otherwise arrive in the socket among
+	 * the test's frames (best effort: the sysctl may be absent) */
+	no_ipv6(a);
+	no_ipv6(b);
 	if ((rc = xsk_link_up(a)) || (rc = xsk_link_up(b)))
 		return rc;
 	return 0;
