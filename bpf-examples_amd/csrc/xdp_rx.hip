@@ -1065,6 +1065,11 @@ __device__ __forceinline__ uint4 ld_nt16(const void *p)
  * result record).  GEN true: exception-kernel entries (xdpgpu ylist: index,
  * partial sum | check word, range start | check offset, range end | flags;
  * any alignment).  meta: 64 uint4, part4: 256 uint4 of this wave's LDS. */
+/* the completed record of a bulk frame: a scattered 16-byte store */
+#ifndef XDP_TAIL_REC_NT
+#define XDP_TAIL_REC_NT 1
+#endif
+constexpr bool kTailRecNt = XDP_TAIL_REC_NT != 0;
 template <int U, bool NT, bool GEN, int G>
 __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 					   uint4 *part4, int lane,
@@ -1198,7 +1203,10 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 		rv.z |= (l4_ok ? XDPGPU_F_L4_OK : 0u) |
 			(absent ? XDPGPU_F_L4_ABSENT : 0u);
 		rv.w = l4 | (cl << 16);
-		st_nt16(a.res + i, rv);
+		if constexpr (kTailRecNt)
+			st_nt16(a.res + i, rv);
+		else
+			*reinterpret_cast<uint4 *>(a.res + i) = rv;
 		a.verdict[i] = (uint8_t)(drop ? XDPGPU_DROP : XDPGPU_REDIRECT);
 		my_bytes += dv.z;
 	}
