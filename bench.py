@@ -153,15 +153,40 @@ def cpu_baseline(umem, descs, flags, fmt, budget_s: float = 10.0):
            "reference_headers_mpps": round((1 << 20) / ref / 1e6, 1) if ref else None}
     if ref:
         cal["leg_over_reference"] = round(ref / mine, 3)
+    legs = cpu_legs(oracle)
     return {"value": round(mpps, 2), "unit": "Mpps", "cores": cores,
             "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
             "kind": "port", "cpu_model": cpu_model(),
             "gbps": round(mpps * 1e6 * BYTES_PER_FRAME / 1e9, 2),
             "single_thread_mpps": round(st_mpps, 2),
             "outputs_match_oracle": checked, "calibration": cal,
+            "secondary_legs_1thread": legs,
             "sample": f"{len(sample)} config-2 frames x {reps} passes of oracle/cpu_leg.c "
                       f"(gcc -O2) on {cores} threads pinned one per CPU ({dt:.1f} s); "
                       f"1 pinned thread: {len(one)} frames x {reps1} passes"}
+
+
+def cpu_legs(oracle) -> dict:
+    """Single-thread CPU rates beside the secondary GPU lines, on samples
+    of the same generators: IMIX through the lean leg (its fast shape, the
+    oracle for the rest) and the SYN proxy through its oracle restatement
+    (a loop-for-loop port of xdp_synproxy_kern.c).  nat64 has none: its
+    oracle searches the state table linearly (a test checker, not a CPU
+    form of the translator)."""
+    out = {}
+    u, d, _ = xdpgpu.pool_generate(1 << 18, xdpgpu.POOL_IMIX, 64, 0x5EED0003)
+    t, _ = oracle.leg_bench(u, d, 1, 3, True, xdpgpu.CFG_DEFAULT, 0, xdpgpu.TUPLE_NET)
+    out["imix_leg_mpps"] = round(3 * len(d) / t / 1e6, 2)
+    u, d = synflood_pool(1 << 18, 0x5EED0007)
+    c = xdpgpu.SynproxyCfg()
+    c.ports[0] = 80
+    c.now_ns = 10**18
+    c.tailroom = 128 - 74
+    t0 = time.perf_counter()
+    oracle.synproxy(u, d, c)
+    out["synproxy_oracle_mpps"] = round(len(d) / (time.perf_counter() - t0) / 1e6, 2)
+    out["threads"] = 1
+    return out
 
 
 def pmc_traffic(n: int, size: int):
