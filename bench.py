@@ -511,9 +511,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # XDPGPU_BENCH_REHEARSE=1: a rehearsal of the N-rank path on fewer GPUs
+    # than ranks (ranks share devices, gloo for the control collectives);
+    # its numbers are not a scaling measurement
+    rehearse = os.environ.get("XDPGPU_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)      # before RCCL binds the rank
     if world > 1:
-        dist.init_process_group("nccl")
+        dist.init_process_group("gloo" if rehearse else "nccl")
     dev = torch.device("cuda", local)
 
     # config 2 shard (config 5 at N > 1: same per-GPU content, seed offset)
@@ -541,7 +547,8 @@ def main():
     v = d_v.cpu().numpy()
     ok = bool(np.array_equal(v, expect))
     # max time / summed frames over ranks (no data-path collective)
-    wall_max, total_frames, all_ok = shard.reduce_timing(wall, n * args.steps, ok, dev)
+    wall_max, total_frames, all_ok = shard.reduce_timing(wall, n * args.steps, ok,
+                                                         None if rehearse else dev)
     mpps = total_frames / wall_max / 1e6
     gbps = total_frames * BYTES_PER_FRAME / wall_max / 1e9
     achieved = BYTES_PER_FRAME * n / (kms * 1e-3) / 1e9
@@ -636,7 +643,8 @@ def main():
                                    "packed 64B-stride UMEM, 1% bad L3 / 1% bad L4 / "
                                    "0.5% malformed / 0.1% ARP / 0.1% NDP",
                        "frames_per_gpu": n, "frame_size": args.size,
-                       "header_window": args.window, "parallelism": f"shard{world}"},
+                       "header_window": args.window, "parallelism": f"shard{world}",
+                       **({"rehearsal": "ranks sharing GPUs, gloo"} if rehearse else {})},
             "gbps": round(gbps, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
