@@ -1096,8 +1096,11 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 	const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
 	const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
 	const uint32_t cl = rv.w >> 16;
-	const uint32_t l4 = GEN ? (rv.w & 0xffff) : ((rv.z >> 16) & 0xff) + 20;
-	const uint32_t rhi = GEN ? (ye.w & 0xffff) : l4 + cl + (cl & 1);
+	/* GEN false: the fast shape's records; IPv6/UDP (V6 builds) has its
+	 * L4 header 40 bytes after l3 and no over-read byte */
+	const bool r6 = !GEN && (rv.z & XDPGPU_F_IPV6);
+	const uint32_t l4 = GEN ? (rv.w & 0xffff) : ((rv.z >> 16) & 0xff) + (r6 ? 40u : 20u);
+	const uint32_t rhi = GEN ? (ye.w & 0xffff) : l4 + cl + (r6 ? 0u : (cl & 1));
 	uint64_t lim = eff + rhi;
 	lim = lim < a.usize ? lim : a.usize;
 	/* absolute range [lo, lim), streamed from its 16-byte aligned start */
@@ -1193,7 +1196,7 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 	} else {
 		c4 = rv.w & 0xffff;
 		sum4 = fold16((uint64_t)(rv.y >> 16) + t);
-		absent = ((rv.z >> 8) & 0xff) == 17 && c4 == 0;
+		absent = !r6 && ((rv.z >> 8) & 0xff) == 17 && c4 == 0;
 		l3_bad = !(rv.z & XDPGPU_F_L3_OK);
 	}
 	const bool l4_ok = absent || (~fold16((uint64_t)sum4 + c4) & 0xffff) == 0;
@@ -1207,6 +1210,25 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 			st_nt16(a.res + i, rv);
 		else
 			*reinterpret_cast<uint4 *>(a.res + i) = rv;
+		if (!GEN && r6 && a.tup && a.tuple_fmt == XDPGPU_TUPLE_NET) {
+			/* an IPv6/UDP frame's network_tuple (the tile stored
+			 * none): the addresses and ports from the frame's
+			 * first line, which the payload stream just read */
+			const uint4 h1 = *reinterpret_cast<const uint4 *>(a.umem + eff + 16);
+			const uint4 h2 = *reinterpret_cast<const uint4 *>(a.umem + eff + 32);
+			const uint4 h3 = *reinterpret_cast<const uint4 *>(a.umem + eff + 48);
+			const uint32_t w[12] = {h1.x, h1.y, h1.z, h1.w, h2.x, h2.y,
+						h2.z, h2.w, h3.x, h3.y, h3.z, h3.w};   /* dwords 4..15 */
+			uint32_t *t = reinterpret_cast<uint32_t *>(a.tup + 44 * i);
+#pragma unroll
+			for (int k = 0; k < 4; k++) {
+				t[k] = (w[1 + k] >> 16) | (w[2 + k] << 16);
+				t[5 + k] = (w[5 + k] >> 16) | (w[6 + k] << 16);
+			}
+			t[4] = w[9] >> 16;
+			t[9] = w[10] & 0xffffu;
+			t[10] = 17u | (10u << 16);
+		}
 		a.verdict[i] = (uint8_t)(drop ? XDPGPU_DROP : XDPGPU_REDIRECT);
 		my_bytes += dv.z;
 	}
@@ -1399,7 +1421,8 @@ __device__ __forceinline__ void defer_append(bool want, uint64_t i, uint32_t *q,
 struct TileOut {
 	uint64_t t0;       /* first frame of the tile (wave-uniform)        */
 	uint32_t li;       /* this lane's frame in the tile                 */
-	uint32_t fl;       /* bit 0: verdict store, bit 1: record and tuple */
+	uint32_t fl;       /* bit 0: verdict store, bit 1: record and tuple,
+			    * bit 2: no tuple (IPv6: the bulk pass's)   */
 	uint32_t verdict;
 	uint32_t sa, da, ports, proto, vid;
 	uint4 rec;
@@ -1434,7 +1457,8 @@ __device__ __forceinline__ void store_tile(const RxArgs &a, const TileOut &o)
 	const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
 		tup ? (void *)(a.tup + tb * o.t0) : (void *)a.verdict, 0,
 		tup ? (int)(tb * kWave) : 0, kFmt);
-	const uint32_t b = out ? tb * o.li : kOff;
+	const bool tout = out && !(fl & 4);
+	const uint32_t b = tout ? tb * o.li : kOff;
 	const v4u_t w0 = net ? (v4u_t){0u, 0u, 0xffff0000u, o.sa}
 			     : (v4u_t){o.sa, o.da, o.ports, o.proto | (2u << 8) | (o.vid << 16)};
 	/* 16-byte tuples: whole lines, streamed (nt).  44-byte tuples: the
@@ -1447,9 +1471,9 @@ __device__ __forceinline__ void store_tile(const RxArgs &a, const TileOut &o)
 		__builtin_amdgcn_raw_buffer_store_b128(w0, rt, b, 0, 2);
 	}
 	__builtin_amdgcn_raw_buffer_store_b128((v4u_t){o.ports & 0xffff, 0u, 0u, 0xffff0000u},
-					       rt, net && out ? b + 16 : kOff, 0, 0);
+					       rt, net && tout ? b + 16 : kOff, 0, 0);
 	__builtin_amdgcn_raw_buffer_store_b96((v3u_t){o.da, o.ports >> 16, o.proto | (2u << 16)},
-					      rt, net && out ? b + 32 : kOff, 0, 0);
+					      rt, net && tout ? b + 32 : kOff, 0, 0);
 }
 
 /* Append to the block's list without an LDS queue: the wave reserves its
@@ -1469,7 +1493,7 @@ __device__ __forceinline__ void defer_direct(bool want, uint64_t i, uint32_t *gl
 		st_asm_sb32(uniform_ptr(gl), (base + rank) * 4u, (uint32_t)i);
 }
 
-template <bool LQ, bool ST = true>
+template <bool LQ, bool ST = true, bool V6 = false>
 __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[18],
 					  uint4 dv, uint64_t i, bool active,
 					  bool dma, int lane, FastWave &w,
@@ -1513,7 +1537,26 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 	 * past the window: the bulk kernel adds the payload sum */
 	const bool shape = fast;
 	fast = shape & (l4 + cl + (cl & 1) <= 64u);
-	const bool bulk = shape & !fast & (a.res != nullptr);
+	bool bulk = shape & !fast & (a.res != nullptr);
+
+	/* V6: untagged IPv6 + UDP with no extension header, the generic
+	 * parse's conditions (parse_ip6hdr, parse_udphdr): the UDP header at
+	 * 54-61 is in the window, the pseudo header's addresses at 22-53;
+	 * csum_ipv6_magic, an odd length zero padded, a stored 0 not absent */
+	bool v6 = false;
+	uint32_t ulen6 = 0;
+	if constexpr (V6) {
+		const uint32_t plen = bswap16(F[4] >> 16);
+		ulen6 = bswap16(F[14] >> 16);
+		v6 = (!a.force_generic) & staged & !v1 & ((F[3] & 0xffffu) == 0xdd86u) &
+		     (((F[3] >> 20) & 0xf) == 6) & ((F[5] & 0xff) == 17) & (len >= 62) &
+		     (54 + plen <= len) & (ulen6 >= 8) & (ulen6 <= plen) & (a.res != nullptr);
+		/* always through the bulk pass, which also writes the
+		 * network_tuple (its addresses are not among the words a tile
+		 * keeps for its stores); a payload inside the window is an
+		 * empty range there */
+		bulk = bulk | v6;
+	}
 
 	/* 3. defer the frames of other shapes to the exception list and
 	 * the long ones to the bulk list of this wave */
@@ -1550,27 +1593,57 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 			m &= udp ? 0xffffffffu : 0x0000ffffu;
 		s4 += r[j] & m;
 	}
-	const uint32_t l3c = ~fold16(s3) & 0xffff;
-	const bool l3_ok = fold16(s3 + c3) == 0xffff;
-	const uint32_t sum4 = fold16(s4);
-	const uint32_t l4c = ~sum4 & 0xffff;
-	const bool absent = udp && c4 == 0;
-	const bool l4_ok = absent || (~fold16((uint64_t)sum4 + c4) & 0xffff) == 0;
-	const bool drop = (a.flags & XDPGPU_CFG_VERIFY_CSUM) && (!l3_ok || !l4_ok);
 	uint32_t key[11] = {0, 0, 0xffff0000u, sa, ports & 0xffff,
 			    0, 0, 0xffff0000u, da, ports >> 16,
 			    proto | (2u << 16)};
+	uint64_t s3v = s3, s4v = s4;
+	uint32_t c3v = c3, c4v = c4, clv = cl, l4v = l4, protov = proto;
+	bool udpv = udp;
+	if constexpr (V6) {
+		/* the v6 frame's terms (selected per lane: branch free) */
+		uint64_t p6 = (uint64_t)__builtin_bswap32(ulen6) + __builtin_bswap32(17u);
+#pragma unroll
+		for (int k = 0; k < 4; k++) {
+			const uint32_t sk = (F[5 + k] >> 16) | (F[6 + k] << 16);
+			const uint32_t dk = (F[9 + k] >> 16) | (F[10 + k] << 16);
+			p6 += (uint64_t)sk + dk;
+			key[k] = v6 ? sk : key[k];
+			key[5 + k] = v6 ? dk : key[5 + k];
+		}
+		const int32_t e6 = (int32_t)(54 + ulen6);
+		const uint64_t s46 = p6 + (F[13] & 0xffff0000u) + (F[14] & first_bytes(e6 - 56)) +
+				     (F[15] & first_bytes(e6 - 60) & 0xffff0000u);
+		key[4] = v6 ? (F[13] >> 16) : key[4];
+		key[9] = v6 ? (F[14] & 0xffffu) : key[9];
+		key[10] = v6 ? (17u | (10u << 16)) : key[10];
+		s4v = v6 ? s46 : s4v;
+		s3v = v6 ? 0xffffull : s3v;      /* no IPv6 header checksum: l3 ok */
+		c3v = v6 ? 0u : c3v;
+		c4v = v6 ? (F[15] & 0xffffu) : c4v;
+		clv = v6 ? ulen6 : clv;
+		l4v = v6 ? 54u : l4v;
+		protov = v6 ? 17u : protov;
+		udpv = udpv & !v6;               /* a stored 0 is not absent */
+	}
+	const uint32_t l3c = v6 ? 0u : ~fold16(s3v) & 0xffff;
+	const bool l3_ok = fold16(s3v + c3v) == 0xffff;
+	const uint32_t sum4 = fold16(s4v);
+	const uint32_t l4c = ~sum4 & 0xffff;
+	const bool absent = udpv && c4v == 0;
+	const bool l4_ok = absent || (~fold16((uint64_t)sum4 + c4v) & 0xffff) == 0;
+	const bool drop = (a.flags & XDPGPU_CFG_VERIFY_CSUM) && (!l3_ok || !l4_ok);
 	/* a bulk frame's record carries its window sum in the l4_csum field
 	 * and its check word in l4_off until the bulk pass completes it */
 	uint4 rec;
 	rec.x = jhash_key44(key, a.initval);
 	rec.y = l3c | ((fast ? l4c : sum4) << 16);
 	rec.z = XDPGPU_F_IP | XDPGPU_F_L4 | (nv ? XDPGPU_F_VLAN : 0u) |
+		(v6 ? XDPGPU_F_IPV6 : 0u) |
 		(l3_ok ? XDPGPU_F_L3_OK : 0u) |
 		(fast && l4_ok ? XDPGPU_F_L4_OK : 0u) |
 		(fast && absent ? XDPGPU_F_L4_ABSENT : 0u) |
-		(proto << 8) | (l3 << 16) | (nv << 24);
-	rec.w = (fast ? l4 : c4) | (cl << 16);
+		(protov << 8) | (l3 << 16) | (nv << 24);
+	rec.w = (fast ? l4v : c4v) | (clv << 16);
 	const uint32_t vid = nv ? (bswap16(F[3] >> 16) & 0x0fff) : 0u;
 	const uint4 tv4 = make_uint4(sa, da, ports, proto | (2u << 8) | (vid << 16));
 	const bool out = fast || bulk;
@@ -1605,7 +1678,7 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 		/* the outputs, stored by the next step (store_tile) */
 		to->t0 = uniform_u64(i);   /* all lanes active: lane 0 */
 		to->li = (uint32_t)(i - to->t0);
-		to->fl = (fast ? 1u : 0u) | (out ? 2u : 0u);
+		to->fl = (fast ? 1u : 0u) | (out ? 2u : 0u) | (v6 ? 4u : 0u);
 		to->verdict = drop ? XDPGPU_DROP : XDPGPU_REDIRECT;
 		to->sa = sa;
 		to->da = da;
@@ -1890,7 +1963,7 @@ constexpr int kCuBlock = kCuWaves * kWave;
 /* DIAG (diagnostic A/B, cfg.tune bits 16-17): 1 = no compute (the
  * window's XOR stored as verdict, record and tuple: the same memory
  * traffic), 2 = the full compute with no output stores. */
-template <bool FRAGS, int DIAG = 0>
+template <bool FRAGS, int DIAG = 0, bool V6 = false>
 __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 {
 	__shared__ uint4 lds_all[kCuWaves * kDbWave];
@@ -2020,7 +2093,7 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 			__builtin_amdgcn_raw_buffer_store_b128((v4u_t){x, 0, x, 0}, rt,
 							       active ? 16 * li : off, 0, 2);
 		} else {
-			fast_tile<false, DIAG != 2>(a, F, dv, i, active, dma, lane, w, &pend);
+			fast_tile<false, DIAG != 2, V6>(a, F, dv, i, active, dma, lane, w, &pend);
 		}
 		return dn;
 	};
@@ -2471,6 +2544,8 @@ static hipError_t launch_db(RxArgs a, uint32_t max_blocks, hipStream_t stream,
 		hipLaunchKernelGGL((xdp_rx_db_kernel<false, 1>), grid, blk, 0, stream, a);
 	else if (diag == 2)
 		hipLaunchKernelGGL((xdp_rx_db_kernel<false, 2>), grid, blk, 0, stream, a);
+	else if (a.v6)
+		hipLaunchKernelGGL((xdp_rx_db_kernel<false, 0, true>), grid, blk, 0, stream, a);
 	else
 		hipLaunchKernelGGL((xdp_rx_db_kernel<false>), grid, blk, 0, stream, a);
 	const hipError_t e = hipGetLastError();
@@ -2501,6 +2576,11 @@ hipError_t launch_rx(const RxArgs &a, uint32_t window, uint32_t max_blocks,
 	if (window != 128 && !(tune & 0x8fffu)) {
 		RxArgs b = a;
 		b.diag = (tune >> 16) & 3;
+		/* untagged IPv6/UDP in the fast shape (IMIX's common IPv6
+		 * frame) for the 44-byte network_tuple and no tuple; bit 18
+		 * turns it off.  The 16-byte IPv4 tuple keeps the IPv4-only
+		 * kernel (config 2), whose registers it would cost. */
+		b.v6 = a.tuple_fmt != XDPGPU_TUPLE_V4 && !((tune >> 18) & 1);
 		return launch_db(b, max_blocks, stream, ev);
 	}
 	if (window == 128)

@@ -136,6 +136,8 @@ struct RxArgs {
 				    * of packets of several (frags.hip)     */
 	uint32_t diag;             /* set by the launcher: cfg.tune bits 16-17
 				    * (diagnostic kernel variants)          */
+	uint32_t v6;               /* set by the launcher: the fast shape
+				    * includes untagged IPv6/UDP           */
 	const unsigned long long *ndev; /* nullable: the frame count lives on
 				    * the device (the bounce batch of
 				    * frags.hip); n is then its upper bound */
