@@ -883,42 +883,48 @@ __device__ __forceinline__ void generic_batch(const RxArgs &a, uint32_t *win,
 			verdict = XDPGPU_TX;   /* rewritten below */
 		}
 	}
-	/* af_xdp_user.c:968-1040 echo responder, one frame at a time by the
-	 * whole wave: lane j writes byte j of the reply (MACs swapped, IPv6
-	 * addresses swapped, type 129, csum_replace2) */
-	uint64_t tx_mask = __ballot(verdict == XDPGPU_TX);
-	while (tx_mask) {
-		const int src = __builtin_ctzll(tx_mask);
-		tx_mask &= tx_mask - 1;
-		const uint64_t seff =
-			((uint64_t)readlane32((uint32_t)(eff >> 32), src) << 32) |
-			readlane32((uint32_t)eff, src);
-		const uint32_t *srow = win + src * SDW;
-		auto sb = [&](int j) -> uint32_t {
-			return (srow[j >> 2] >> ((j & 3) * 8)) & 0xff;
+	/* af_xdp_user.c:968-1040 echo responder: each TX lane rewrites its own
+	 * frame from its window row (MACs swapped, IPv6 addresses swapped,
+	 * type 129, csum_replace2): bytes 0-11 and 20-59 as dwords (the
+	 * unchanged bytes among them rewritten with their own values), bytes
+	 * one by one for a frame not 4-byte aligned.  (One frame at a time by
+	 * the whole wave, a byte per lane: the echo pool's launch 1.38 vs
+	 * 1.26 ms.) */
+	if (verdict == XDPGPU_TX) {
+		const uint32_t *row = win + lane * SDW;
+		auto rb = [&](int j) -> uint32_t { return (row[j >> 2] >> ((j & 3) * 8)) & 0xff; };
+		auto nb = [&](int j) -> uint32_t {
+			if (j < 6)
+				return rb(j + 6);
+			if (j < 12)
+				return rb(j - 6);
+			if (j >= 22 && j < 38)
+				return rb(j + 16);
+			if (j >= 38 && j < 54)
+				return rb(j - 16);
+			if (j == 54)
+				return 129u;
+			if (j == 56 || j == 57) {
+				const uint32_t ck = csum_replace2(rb(56) | (rb(57) << 8), 0x0080, 0x0081);
+				return j == 56 ? (ck & 0xff) : (ck >> 8);
+			}
+			return rb(j);
 		};
-		const int j = lane;
-		int from = -1;
-		uint32_t val = 0;
-		if (j < 6)
-			from = j + 6;
-		else if (j < 12)
-			from = j - 6;
-		else if (j >= 22 && j < 38)
-			from = j + 16;
-		else if (j >= 38 && j < 54)
-			from = j - 16;
-		if (from >= 0)
-			val = sb(from);
-		if (j == 54)
-			val = 129;
-		if (j == 56 || j == 57) {
-			const uint32_t ck = csum_replace2(sb(56) | (sb(57) << 8),
-							  0x0080, 0x0081);
-			val = (j == 56) ? (ck & 0xff) : (ck >> 8);
+		uint8_t *g = a.umem + eff;
+		if (!(eff & 3)) {
+			uint32_t *gw = reinterpret_cast<uint32_t *>(g);
+#pragma unroll
+			for (int d = 0; d < 15; d++) {
+				if (d >= 3 && d < 5)
+					continue;
+				gw[d] = nb(4 * d) | nb(4 * d + 1) << 8 | nb(4 * d + 2) << 16 |
+					nb(4 * d + 3) << 24;
+			}
+		} else {
+			for (int j = 0; j < 60; j++)
+				if (j < 12 || j >= 22)
+					g[j] = (uint8_t)nb(j);
 		}
-		if (from >= 0 || j == 54 || j == 56 || j == 57)
-			a.umem[seff + j] = (uint8_t)val;
 	}
 	const bool rec_live = verdict != XDPGPU_ABORTED && verdict != XDPGPU_PASS;
 
