@@ -1965,10 +1965,26 @@ constexpr int kCuBlock = kCuWaves * kWave;
  *
  * 15 waves per CU (4, 4, 4, 3 per SIMD: 15 x 10 KiB of buffers and the
  * block's counters in the CU's 160 KiB), 128 VGPRs.
+ *
+ * Shared tiles: the block's own tiles (above) are the first part of the
+ * batch; the rest (12/16 by default, RxArgs.steal_tiles) is claimed at run
+ * time, two tiles per claim, from 16 global counters (block b: counter b
+ * mod 16), so the CUs that run faster take more: with static shares the
+ * CUs' loop ends spread over 30 us of a 330 us launch.  Config 2: 0.3226
+ * vs 0.3435 ms without, in one process (tools/gpu_ab_steal.sh).
  */
 /* DIAG (diagnostic A/B, cfg.tune bits 16-17): 1 = no compute (the
  * window's XOR stored as verdict, record and tuple: the same memory
  * traffic), 2 = the full compute with no output stores. */
+/* Shared tiles one block may take: twice its share and a wave's worth
+ * more, so that the blocks of every head can drain it (each keeps claiming
+ * until its head is empty or it reaches the cap; a head has at least
+ * floor(nb / heads) >= nb / (2 heads) blocks). */
+__host__ __device__ inline uint64_t steal_cap(uint64_t sh, uint64_t nb)
+{
+	return 2 * ((sh + nb - 1) / nb) + 32;
+}
+
 template <bool FRAGS, int DIAG = 0, bool V6 = false>
 __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 {
@@ -1995,9 +2011,13 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 	const uint64_t wgid = rb * kCuWaves + wid;
 
 	if (threadIdx.x == 0) {
-		ctl[0] = ctl[1] = ctl[2] = ctl[3] = ctl[4] = ctl[5] = 0;
+		ctl[0] = ctl[1] = ctl[2] = ctl[3] = ctl[4] = ctl[5] = ctl[6] = 0;
 		a.ycount[rb] = 0;      /* filled by the exception pass */
 	}
+	/* the next launch's shared-tile counters (this launch's set was
+	 * zeroed by the one before) */
+	if (rb == 0 && threadIdx.x < kStealHeads && a.steal)
+		a.steal[((a.steal_set ^ 1) * kStealHeads + threadIdx.x) * kStealStride] = 0;
 	lds_dma_landed();
 	__syncthreads();
 
@@ -2011,9 +2031,33 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 	STAMP(wgid, lane, 0);
 
 	const bool dma = !a.force_generic && a.usize >= 64;
-	/* the block's next cnt tiles: b + k nb for k = the claim .. + cnt-1 */
+	/* the block's k-th tile (a.order): 0: b + k nb; 1: b per + k over a
+	 * contiguous range of per tiles; 2, 3: k nb + (b + k c) mod nb, c = 1,
+	 * 97 (each round of nb tiles still split over the blocks, each block
+	 * moving through the round's positions); ntiles past the block's
+	 * tiles.  Increasing in k. */
+	/* the block's own tiles are those below own; the shared ones above
+	 * are claimed after them (a.steal_tiles) */
+	const uint64_t shared = FRAGS || DIAG ? 0 : a.steal_tiles;
+	const uint64_t own = ntiles - shared;
+	const uint64_t per = (own + nb - 1) / nb;
+	const uint32_t order = a.order;
+	const uint64_t rot = order == 3 ? 97 : 1;
+	auto tile_of = [&](uint64_t k) -> uint64_t {
+		uint64_t t, lim = own;
+		if (order == 1) {
+			t = rb * per + k;
+			lim = min(own, rb * per + per);
+		} else if (order >= 2) {
+			t = k * nb + (rb + k * rot) % nb;
+		} else {
+			t = rb + k * nb;
+		}
+		return t < lim ? t : ntiles;
+	};
+	/* the block's next cnt tiles: claim indices k .. k + cnt-1 */
 	auto claim = [&](uint32_t cnt) -> uint64_t {
-		return rb + (uint64_t)lds_fetch_add(&ctl[0], cnt, lane) * nb;
+		return (uint64_t)lds_fetch_add(&ctl[0], cnt, lane);
 	};
 	/* descriptor index of lane's frame in tile tt, clamped to the batch */
 	auto desc_at = [&](uint64_t tt) -> uint64_t {
@@ -2078,7 +2122,7 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 			store_tile(a, pend);
 		issue_win(dn, tw < ntiles, win);
 		issue_desc(td, dsl);
-		tn = claim(1);
+		tn = tile_of(claim(1));
 		if constexpr (DIAG == 1) {
 			uint32_t x = dv.x ^ dv.z;
 #pragma unroll
@@ -2106,8 +2150,8 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 
 	/* the wave's tiles T0 < T1 < ...: the first five claimed at once */
 	const uint64_t first = claim(5);
-	uint64_t q0 = first, q1 = first + nb, q2 = first + 2 * nb, q3 = first + 3 * nb,
-		 q4 = first + 4 * nb, q5;
+	uint64_t q0 = tile_of(first), q1 = tile_of(first + 1), q2 = tile_of(first + 2),
+		 q3 = tile_of(first + 3), q4 = tile_of(first + 4), q5;
 	if (q0 < ntiles) {
 		/* prologue: descriptors of the first two tiles in registers;
 		 * then, in this order, descriptor DMA T2, window DMA T0,
@@ -2139,6 +2183,64 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 		}
 		if constexpr (DIAG != 1 && DIAG != 2)
 			store_tile(a, pend);   /* the last tile's outputs */
+	}
+	/* Shared tiles: with its own tiles done, the wave claims the tiles of
+	 * its block's head (block b: head b mod heads) one at a time from the
+	 * head's global counter, each claim first reserving one of the
+	 * block's steal_cap() slots (its list regions hold that many more
+	 * tiles), until the head is empty.  CUs run their own tiles at
+	 * rates up to 10 % apart (tools/stamps.py); the shared tiles go to
+	 * whichever are done first.  Not pipelined: every access waited. */
+	if (shared) {
+		const uint64_t heads = min((uint64_t)kStealHeads, nb);
+		const uint64_t h = rb % heads;
+		uint32_t *ctr = a.steal + (a.steal_set * kStealHeads + h) * kStealStride;
+		const uint32_t cap = (uint32_t)steal_cap(shared, nb);
+		lds_dma_landed();   /* the loop's last DMAs into win0/dsl0 */
+		/* the claim of the first pair; later claims are issued before
+		 * the wait for the current pair's windows, so that the atomic's
+		 * round trip overlaps the DMA's */
+		uint32_t v = 0;
+		if (lds_fetch_add(&ctl[6], 2, lane) + 2 <= cap && lane == 0)
+			v = atomicAdd(ctr, 1u);
+		else if (lane == 0)
+			v = 0x7fffffffu;   /* over the cap: no claim */
+		while (own + h < ntiles) {
+			/* claim v: head h's tiles 2v and 2v + 1, the j-th being
+			 * own + j heads + h, so that a tile goes to the XCD (b mod
+			 * 8) the own-tile order gives it; the launcher makes own a
+			 * multiple of the heads.  (A tile's XCD matters: an order
+			 * that moved the blocks through all positions of each
+			 * round ran 11 % slower.)  Both tiles' DMAs in flight at
+			 * once. */
+			const uint64_t t0 =
+				own + (uint64_t)__builtin_amdgcn_readfirstlane(v) * 2 * heads + h;
+			if (t0 >= ntiles)
+				break;
+			const uint64_t t1 = t0 + heads;
+			const uint4 dv0 = *reinterpret_cast<const uint4 *>(a.desc + desc_at(t0));
+			const uint4 dv1 = *reinterpret_cast<const uint4 *>(a.desc + desc_at(t1));
+			issue_win(dv0, true, win0);
+			issue_win(dv1, t1 < ntiles, win1);
+			/* the next pair's claim (or none over the cap) */
+			v = 0x7fffffffu;
+			if (lds_fetch_add(&ctl[6], 2, lane) + 2 <= cap && lane == 0)
+				v = atomicAdd(ctr, 1u);
+			uint32_t F[18];
+			uint4 dn;
+			lds_dma_landed();
+			read_tile_db<10>(win0, dsl0, lane, F, dn);
+			const uint64_t i0 = t0 * kWave + lane;
+			fast_tile<false, true, V6>(a, F, dv0, i0, i0 < nfr, dma, lane, w, &pend);
+			store_tile(a, pend);
+			if (t1 >= ntiles)
+				break;
+			read_tile_db<10>(win1, dsl1, lane, F, dn);
+			const uint64_t i1 = t1 * kWave + lane;
+			fast_tile<false, true, V6>(a, F, dv1, i1, i1 < nfr, dma, lane, w, &pend);
+			store_tile(a, pend);
+		}
+		lds_dma_landed();   /* a claim left outstanding at a break */
 	}
 	STAMP(wgid, lane, 1);
 
@@ -2541,6 +2643,22 @@ static hipError_t launch_db(RxArgs a, uint32_t max_blocks, hipStream_t stream,
 	/* list regions per block: its share of the tiles */
 	a.xregion = (uint32_t)(((ntiles + blocks - 1) / blocks) * kWave);
 	a.nregions = (uint32_t)blocks;
+	/* shared tiles (xdp_rx_db_kernel): the last ntiles x steal_16ths / 16,
+	 * for batches of at least 64 tiles per block; a block's region then
+	 * holds its own tiles and up to steal_cap() shared ones */
+	a.steal_tiles = 0;
+	if (a.steal && a.steal_16ths && !a.frags && !a.ndev && !diag &&
+	    ntiles >= 64 * blocks) {
+		/* own a multiple of the heads (xdp_rx_db_kernel's head order) */
+		const uint64_t own = (ntiles - ntiles * min(a.steal_16ths, 16u) / 16) &
+				     ~(uint64_t)(kStealHeads - 1);
+		const uint64_t sh = ntiles - own;
+		const uint64_t xr = ((own + blocks - 1) / blocks + steal_cap(sh, blocks)) * kWave;
+		if (xr * blocks <= a.xcap && xr <= 0xffffffffull) {
+			a.steal_tiles = (uint32_t)sh;
+			a.xregion = (uint32_t)xr;
+		}
+	}
 	if (ev)
 		(void)hipEventRecord(ev[0], stream);
 	const dim3 grid((uint32_t)blocks), blk(kCuBlock);
@@ -2587,6 +2705,8 @@ hipError_t launch_rx(const RxArgs &a, uint32_t window, uint32_t max_blocks,
 		 * turns it off.  The 16-byte IPv4 tuple keeps the IPv4-only
 		 * kernel (config 2), whose registers it would cost. */
 		b.v6 = a.tuple_fmt != XDPGPU_TUPLE_V4 && !((tune >> 18) & 1);
+		/* bits 19-20: the tile order (xdp_rx_db_kernel) */
+		b.order = (tune >> 19) & 3;
 		return launch_db(b, max_blocks, stream, ev);
 	}
 	if (window == 128)

@@ -48,6 +48,10 @@ struct Slot {
 	uint4 *d_ylist = nullptr;     /* exception payload sums (generic -> bulk) */
 	uint64_t xcap = 0;
 	uint32_t *d_xcount = nullptr;
+	/* xdp_rx_db_kernel's shared-tile claim counters (RxArgs.steal): two
+	 * sets, the next launch's zeroed by the current one */
+	uint32_t *d_steal = nullptr;
+	uint32_t steal_set = 0;
 	/* multi-buffer packets (XDPGPU_CFG_FRAGS) */
 	unsigned long long *d_fc = nullptr;   /* fragment kernels' counters:
 					       * 2 totals, then 2 per block */
@@ -177,6 +181,8 @@ static void free_slot(Slot &s)
 		(void)hipFree(s.d_xlist);
 	if (s.d_xcount)
 		(void)hipFree(s.d_xcount);
+	if (s.d_steal)
+		(void)hipFree(s.d_steal);
 	if (s.d_ylist)
 		(void)hipFree(s.d_ylist);
 	if (s.h_fc)
@@ -445,13 +451,25 @@ static int ensure_slot_buffers(xdpgpu_ctx *ctx, Slot &s, uint32_t n)
  * tiles, xcap entries each, and their per-wave counts. */
 static int ensure_xlist(xdpgpu_ctx *ctx, Slot &s, uint32_t n)
 {
-	const uint64_t need = (uint64_t)n + 64ull * 4 * kMaxRxBlocks + 64;
+	/* the frames, as many more for xdp_rx_db_kernel's shared tiles
+	 * (launch_db: a block's region holds its own tiles and up to twice its
+	 * share of the shared ones, up to the whole batch), and per-block
+	 * slack */
+	const uint64_t need = 3ull * n + 64ull * 40 * kMaxRxBlocks + 1024;
 	/* per-wave exception, bulk and deferred-payload counts */
 	const size_t cbytes = (size_t)kMaxRxBlocks * 4 * 3 * sizeof(uint32_t);
 	if (!s.d_xcount && (hipMalloc(&s.d_xcount, cbytes) != hipSuccess ||
 			    hipMemset(s.d_xcount, 0, cbytes) != hipSuccess ||
 			    hipDeviceSynchronize() != hipSuccess))
 		return set_err(ctx, -ENOMEM, "exception counts");
+	const size_t sbytes = 2ull * kStealHeads * kStealStride * sizeof(uint32_t);
+	if (!s.d_steal && (hipMalloc(&s.d_steal, sbytes) != hipSuccess ||
+			   hipMemset(s.d_steal, 0, sbytes) != hipSuccess ||
+			   hipDeviceSynchronize() != hipSuccess)) {
+		(void)hipFree(s.d_steal);
+		s.d_steal = nullptr;
+		return set_err(ctx, -ENOMEM, "shared-tile counters");
+	}
 	if (s.xcap >= need)
 		return 0;
 	if (s.d_xlist || s.d_ylist) {
@@ -563,6 +581,17 @@ static int enqueue_rx(xdpgpu_ctx *ctx, Slot &s, uint8_t *d_umem, uint64_t usize,
 	a.ydefer = !((ctx->cfg.tune >> 8) & 1);
 	a.force_generic = (ctx->cfg.tune >> 9) & 1;
 	a.frags = (ctx->cfg.flags & XDPGPU_CFG_FRAGS) ? 1u : 0u;
+	a.xcap = s.xcap;
+	a.steal = s.d_steal;
+	a.steal_set = s.steal_set;
+	/* shared tiles, in 16ths of the batch (cfg.tune bits 21-23): 0 =
+	 * 12, 1 = none, 2 = 4, 3 = 8, 4 = 16 (all), 5 = 12, 6 = 2, 7 = 14.
+	 * Config 2, one box, one process: none 0.3435 ms, 8 0.3284, 12
+	 * 0.3226, 14 0.3227, 16 0.331 (tools/gpu_ab_steal.sh) */
+	{
+		static const uint32_t k16ths[8] = {12, 0, 4, 8, 16, 12, 2, 14};
+		a.steal_16ths = k16ths[(ctx->cfg.tune >> 21) & 7];
+	}
 
 	/* Multi-buffer packets.  No host round trip: the bounce arrays are
 	 * sized from bounds known here (a packet has at least two
@@ -614,6 +643,8 @@ static int enqueue_rx(xdpgpu_ctx *ctx, Slot &s, uint8_t *d_umem, uint64_t usize,
 		ev = ctx->tev + 4 * ctx->tn++;
 	HIP_TRY(ctx, launch_rx(a, ctx->cfg.window, ctx->max_blocks, stream,
 			       ctx->cfg.tune, ev));
+	/* the launch zeroed the other counter set: the next one uses it */
+	s.steal_set ^= 1;
 	if (a.frags) {
 		/* one frame per packet: gathered into the bounce UMEM, the RX
 		 * kernels over the bounce batch, the outputs back to the

@@ -105,6 +105,9 @@ constexpr uint32_t kMaxRxBlocks = 2048;
 /* Counter slots of a context slot: one per block of the per-block kernels,
  * then one per wave of the double-buffered RX kernel (xdp_rx_db_kernel). */
 constexpr uint32_t kStatSlots = kMaxRxBlocks * 5;
+/* Global claim counters of xdp_rx_db_kernel's shared tiles (RxArgs.steal):
+ * heads per set, u32 words per head (one 128-byte line each). */
+constexpr uint32_t kStealHeads = 16, kStealStride = 32;
 
 struct RxArgs {
 	uint8_t *umem;
@@ -138,6 +141,19 @@ struct RxArgs {
 				    * (diagnostic kernel variants)          */
 	uint32_t v6;               /* set by the launcher: the fast shape
 				    * includes untagged IPv6/UDP           */
+	uint32_t order;            /* set by the launcher: xdp_rx_db_kernel's
+				    * tile order (cfg.tune bits 19-20)     */
+	/* xdp_rx_db_kernel's shared tiles: the last steal_tiles tiles of the
+	 * batch are claimed at run time from kStealHeads global counters by
+	 * any block done with its own (set by the launcher; 0: none) */
+	uint32_t *steal;           /* 2 sets x kStealHeads counters, 128 B
+				    * apart: a launch uses set steal_set
+				    * and zeroes the other for the next    */
+	uint32_t steal_set;
+	uint32_t steal_16ths;      /* shared tiles = tiles x steal_16ths / 16
+				    * (0: none)                            */
+	uint32_t steal_tiles;      /* set by the launcher                  */
+	uint64_t xcap;             /* entries of each deferral list        */
 	const unsigned long long *ndev; /* nullable: the frame count lives on
 				    * the device (the bounce batch of
 				    * frags.hip); n is then its upper bound */
