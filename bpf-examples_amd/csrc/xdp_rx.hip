@@ -2185,60 +2185,69 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 			store_tile(a, pend);   /* the last tile's outputs */
 	}
 	/* Shared tiles: with its own tiles done, the wave claims the tiles of
-	 * its block's head (block b: head b mod heads) one at a time from the
-	 * head's global counter, each claim first reserving one of the
+	 * its block's head (block b: head b mod heads) two at a time from the
+	 * head's global counter, each claim first reserving two of the
 	 * block's steal_cap() slots (its list regions hold that many more
 	 * tiles), until the head is empty.  CUs run their own tiles at
 	 * rates up to 10 % apart (tools/stamps.py); the shared tiles go to
-	 * whichever are done first.  Not pipelined: every access waited. */
+	 * whichever are done first. */
 	if (shared) {
 		const uint64_t heads = min((uint64_t)kStealHeads, nb);
 		const uint64_t h = rb % heads;
 		uint32_t *ctr = a.steal + (a.steal_set * kStealHeads + h) * kStealStride;
 		const uint32_t cap = (uint32_t)steal_cap(shared, nb);
 		lds_dma_landed();   /* the loop's last DMAs into win0/dsl0 */
-		/* the claim of the first pair; later claims are issued before
-		 * the wait for the current pair's windows, so that the atomic's
-		 * round trip overlaps the DMA's */
-		uint32_t v = 0;
-		if (lds_fetch_add(&ctl[6], 2, lane) + 2 <= cap && lane == 0)
-			v = atomicAdd(ctr, 1u);
-		else if (lane == 0)
-			v = 0x7fffffffu;   /* over the cap: no claim */
-		while (own + h < ntiles) {
-			/* claim v: head h's tiles 2v and 2v + 1, the j-th being
-			 * own + j heads + h, so that a tile goes to the XCD (b mod
-			 * 8) the own-tile order gives it; the launcher makes own a
-			 * multiple of the heads.  (A tile's XCD matters: an order
-			 * that moved the blocks through all positions of each
-			 * round ran 11 % slower.)  Both tiles' DMAs in flight at
-			 * once. */
-			const uint64_t t0 =
-				own + (uint64_t)__builtin_amdgcn_readfirstlane(v) * 2 * heads + h;
-			if (t0 >= ntiles)
-				break;
-			const uint64_t t1 = t0 + heads;
-			const uint4 dv0 = *reinterpret_cast<const uint4 *>(a.desc + desc_at(t0));
-			const uint4 dv1 = *reinterpret_cast<const uint4 *>(a.desc + desc_at(t1));
-			issue_win(dv0, true, win0);
-			issue_win(dv1, t1 < ntiles, win1);
-			/* the next pair's claim (or none over the cap) */
-			v = 0x7fffffffu;
+		/* A claim v is head h's tiles 2v and 2v + 1, the j-th being
+		 * own + j heads + h, so that a tile goes to the XCD (b mod 8)
+		 * the own-tile order gives it; the launcher makes own a
+		 * multiple of the heads.  (A tile's XCD matters: an order that
+		 * moved the blocks through all positions of each round ran 11 %
+		 * slower.)  claim() reserves two of the block's slots first and
+		 * returns lane 0's claim (no claim over the cap). */
+		auto claim2 = [&]() -> uint32_t {
+			uint32_t v = 0x7fffffffu;
 			if (lds_fetch_add(&ctl[6], 2, lane) + 2 <= cap && lane == 0)
 				v = atomicAdd(ctr, 1u);
-			uint32_t F[18];
-			uint4 dn;
-			lds_dma_landed();
-			read_tile_db<10>(win0, dsl0, lane, F, dn);
-			const uint64_t i0 = t0 * kWave + lane;
-			fast_tile<false, true, V6>(a, F, dv0, i0, i0 < nfr, dma, lane, w, &pend);
-			store_tile(a, pend);
-			if (t1 >= ntiles)
-				break;
-			read_tile_db<10>(win1, dsl1, lane, F, dn);
-			const uint64_t i1 = t1 * kWave + lane;
-			fast_tile<false, true, V6>(a, F, dv1, i1, i1 < nfr, dma, lane, w, &pend);
-			store_tile(a, pend);
+			return v;
+		};
+		auto first_of = [&](uint32_t v) -> uint64_t {
+			const uint64_t t =
+				own + (uint64_t)__builtin_amdgcn_readfirstlane(v) * 2 * heads + h;
+			return t < ntiles ? t : ntiles;
+		};
+		auto second_of = [&](uint64_t t) -> uint64_t {
+			return t + heads < ntiles ? t + heads : ntiles;
+		};
+		uint64_t c0 = own + h < ntiles ? first_of(claim2()) : ntiles;
+		if (c0 < ntiles) {
+			/* per pair: descriptors, windows and the next claim in
+			 * flight, one wait, then the two tiles.  (Pipelined over
+			 * pairs, each buffer refilled as soon as read: 0.3361 vs
+			 * 0.3250 ms on config 2, one process.) */
+			for (;;) {
+				const uint64_t c1 = second_of(c0);
+				const uint4 d0 = *reinterpret_cast<const uint4 *>(a.desc + desc_at(c0));
+				const uint4 d1 = *reinterpret_cast<const uint4 *>(a.desc + desc_at(c1));
+				issue_win(d0, true, win0);
+				issue_win(d1, c1 < ntiles, win1);
+				const uint32_t vn = claim2();
+				uint32_t F[18];
+				uint4 dn;
+				lds_dma_landed();
+				read_tile_db<10>(win0, dsl0, lane, F, dn);
+				const uint64_t i0 = c0 * kWave + lane;
+				fast_tile<false, true, V6>(a, F, d0, i0, i0 < nfr, dma, lane, w, &pend);
+				store_tile(a, pend);
+				if (c1 >= ntiles)
+					break;
+				read_tile_db<10>(win1, dsl1, lane, F, dn);
+				const uint64_t i1 = c1 * kWave + lane;
+				fast_tile<false, true, V6>(a, F, d1, i1, i1 < nfr, dma, lane, w, &pend);
+				store_tile(a, pend);
+				c0 = first_of(vn);
+				if (c0 >= ntiles)
+					break;
+			}
 		}
 		lds_dma_landed();   /* a claim left outstanding at a break */
 	}
