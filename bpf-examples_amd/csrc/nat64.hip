@@ -1107,8 +1107,8 @@ __global__ __launch_bounds__(kCuBlockN, 1) void xdp_nat64_fast_kernel(Nat64Args 
 	/* translated first 64 bytes of each frame, stored transposed */
 	__shared__ uint4 obuf_all[kCuWavesN * 4 * kWaveN];
 	__shared__ uint64_t otab_all[kCuWavesN * kWaveN];
-	/* the block's tile claims and slow-list length */
-	__shared__ uint32_t ctl[2];
+	/* the block's tile claims, slow-list length, shared-tile slots */
+	__shared__ uint32_t ctl[3];
 	const int lane = threadIdx.x & (kWaveN - 1);
 	const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveN);
 	uint4 *buf = buf_all + wid * 4 * kWaveN;
@@ -1119,17 +1119,56 @@ __global__ __launch_bounds__(kCuBlockN, 1) void xdp_nat64_fast_kernel(Nat64Args 
 	const Tables T = {a.v6map, a.v6nb, a.v4map, a.v4nb, a.dyn, a.now, a.thr};
 
 	if (threadIdx.x == 0)
-		ctl[0] = ctl[1] = 0;
+		ctl[0] = ctl[1] = ctl[2] = 0;
+	const uint64_t rb = blockIdx.x, nb = gridDim.x;
+	/* the next launch's shared-tile counters (this launch's set was
+	 * zeroed by the one before) */
+	if (rb == 0 && threadIdx.x < kStealHeads && a.steal)
+		a.steal[((a.steal_set ^ 1) * kStealHeads + threadIdx.x) * kStealStride] = 0;
 	__syncthreads();
 
 	const uint64_t ntiles = ((uint64_t)a.n + kWaveN - 1) / kWaveN;
-	const uint64_t rb = blockIdx.x, nb = gridDim.x;
+	/* Shared tiles, as in xdp_rx_db_kernel: the block's own tiles b,
+	 * b + nb, ... below own, then those above, one per claim from the
+	 * global counter of head b mod heads (tile own + v heads + h), each
+	 * claim first reserving one of the block's steal_cap() slots.  A
+	 * claim is issued one step before its tile is needed and read after
+	 * the next step's full wait, so its round trip is hidden. */
+	const uint64_t shared = a.steal ? a.steal_tiles : 0;
+	const uint64_t own = ntiles - shared;
+	const uint64_t heads = min((uint64_t)kStealHeads, nb), h = rb % heads;
+	uint32_t *ctr = a.steal + (a.steal_set * kStealHeads + h) * kStealStride;
+	const uint32_t scap = (uint32_t)steal_cap(shared, nb);
+	bool stealing = false;
+	uint32_t vpend = 0x7fffffffu;
+	auto gclaim = [&]() -> uint32_t {
+		uint32_t v = 0x7fffffffu;
+		if (lds_fetch_add(&ctl[2], 1, lane) < scap && lane == 0)
+			v = atomicAdd(ctr, 1u);
+		return v;
+	};
 	uint32_t *xl = a.xlist + rb * a.xregion;
 	uint32_t xq_n = 0;
 	const uint64_t us16 = (a.usize + 15) & ~15ull;
 	const bool dma = a.usize >= 64;
 	auto claim = [&](uint32_t cnt) -> uint64_t {
 		return rb + (uint64_t)lds_fetch_add(&ctl[0], cnt, lane) * nb;
+	};
+	/* the next tile: an own tile, else the shared tile of the claim
+	 * pending since the last step (the first one claimed now) */
+	auto next_tile = [&]() -> uint64_t {
+		if (!stealing) {
+			const uint64_t t = claim(1);
+			if (t < own)
+				return t;
+			stealing = true;
+			if (!shared)
+				return ntiles;
+			vpend = gclaim();
+		}
+		const uint32_t v = __builtin_amdgcn_readfirstlane(vpend);
+		const uint64_t t = v < 0x7fffffffu ? own + (uint64_t)v * heads + h : ntiles;
+		return t < ntiles ? t : ntiles;
 	};
 	/* 64 queued slow frames to the block's list */
 	auto flush = [&](uint32_t cnt) {
@@ -1162,8 +1201,12 @@ __global__ __launch_bounds__(kCuBlockN, 1) void xdp_nat64_fast_kernel(Nat64Args 
 	};
 
 	/* the wave's tiles: qa (in the buffer), qb (its descriptor loaded) */
-	const uint64_t first = claim(2);
-	uint64_t qa = first, qb = first + nb;
+	uint64_t qa = next_tile();
+	if (stealing && qa < ntiles)
+		vpend = gclaim();
+	uint64_t qb = next_tile();
+	if (stealing && qb < ntiles)
+		vpend = gclaim();
 	uint4 dcur = make_uint4(0, 0, 0, 0), dnext = dcur;
 	if (qa < ntiles) {
 		dcur = ld_desc(qa);
@@ -1189,9 +1232,13 @@ __global__ __launch_bounds__(kCuBlockN, 1) void xdp_nat64_fast_kernel(Nat64Args 
 		}
 		lds_reads_done();
 		__builtin_amdgcn_wave_barrier();
+		/* resolved before this step's first vector memory op: a pending
+		 * claim has landed in the wait above */
+		const uint64_t qc = next_tile();
 		dcur = dnext;
 		issue(dcur, qb < ntiles);
-		const uint64_t qc = claim(1);
+		if (stealing && qc < ntiles)
+			vpend = gclaim();
 		dnext = ld_desc(qc);
 
 		const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
@@ -1310,10 +1357,24 @@ hipError_t launch_nat64(const Nat64Args &a0, uint32_t max_blocks, hipStream_t st
 	}
 	if (a.fast) {
 		const uint32_t blocks = nat64_grid(a.n, max_blocks);
-		/* one slow-list region per block: its share of the tiles */
+		/* one slow-list region per block: its share of the tiles, and
+		 * with shared tiles (batches of at least 64 tiles per block) up
+		 * to steal_cap() more */
 		a.nregions = blocks;
 		const uint64_t tiles = ((uint64_t)a.n + kWaveN - 1) / kWaveN;
 		a.xregion = (uint32_t)(((tiles + a.nregions - 1) / a.nregions) * kWaveN);
+		a.steal_tiles = 0;
+		if (a.steal && a.steal_16ths && !a.diag && tiles >= 64ull * blocks) {
+			const uint64_t own = (tiles - tiles * min(a.steal_16ths, 16u) / 16) &
+					     ~(uint64_t)(kStealHeads - 1);
+			const uint64_t sh = tiles - own;
+			const uint64_t xr =
+				((own + blocks - 1) / blocks + steal_cap(sh, blocks)) * kWaveN;
+			if (xr * blocks <= a.xcap && xr <= 0xffffffffull) {
+				a.steal_tiles = (uint32_t)sh;
+				a.xregion = (uint32_t)xr;
+			}
+		}
 		if (a.cfg.direction == XDPGPU_NAT64_EGRESS)
 			hipLaunchKernelGGL(xdp_nat64_fast_kernel<true>, dim3(blocks),
 					   dim3(kCuBlockN), 0, stream, a);

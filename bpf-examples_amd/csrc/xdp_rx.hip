@@ -1976,15 +1976,6 @@ constexpr int kCuBlock = kCuWaves * kWave;
 /* DIAG (diagnostic A/B, cfg.tune bits 16-17): 1 = no compute (the
  * window's XOR stored as verdict, record and tuple: the same memory
  * traffic), 2 = the full compute with no output stores. */
-/* Shared tiles one block may take: twice its share and a wave's worth
- * more, so that the blocks of every head can drain it (each keeps claiming
- * until its head is empty or it reaches the cap; a head has at least
- * floor(nb / heads) >= nb / (2 heads) blocks). */
-__host__ __device__ inline uint64_t steal_cap(uint64_t sh, uint64_t nb)
-{
-	return 2 * ((sh + nb - 1) / nb) + 32;
-}
-
 template <bool FRAGS, int DIAG = 0, bool V6 = false>
 __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 {

@@ -999,6 +999,11 @@ int xdpgpu_nat64_dev(xdpgpu_ctx *ctx, void *d_umem, uint64_t umem_size,
 			return rc;
 		a.xlist = ctx->slot[0].d_xlist;
 		a.xcount = ctx->slot[0].d_xcount;
+		a.xcap = ctx->slot[0].xcap;
+		/* shared tiles (cfg.tune bit 14: none): 12/16 of the batch */
+		a.steal = ctx->slot[0].d_steal;
+		a.steal_set = ctx->slot[0].steal_set;
+		a.steal_16ths = (ctx->cfg.tune >> 14) & 1 ? 0u : 12u;
 		for (int k = 0; k < 4; k++) {
 			uint8_t m[4], w[4];
 			for (int j = 0; j < 4; j++) {
@@ -1024,6 +1029,8 @@ int xdpgpu_nat64_dev(xdpgpu_ctx *ctx, void *d_umem, uint64_t umem_size,
 	if (rc)
 		return rc;
 	HIP_TRY(ctx, launch_nat64(a, ctx->max_blocks, st));
+	/* the fast kernel zeroed the other counter set (as the RX launch) */
+	ctx->slot[0].steal_set ^= 1;
 	rc = scratch_leave(ctx, ctx->slot[0], st);
 	if (rc)
 		return rc;

@@ -108,6 +108,14 @@ constexpr uint32_t kStatSlots = kMaxRxBlocks * 5;
 /* Global claim counters of xdp_rx_db_kernel's shared tiles (RxArgs.steal):
  * heads per set, u32 words per head (one 128-byte line each). */
 constexpr uint32_t kStealHeads = 16, kStealStride = 32;
+/* Shared tiles one block may take: twice its share and 32 more, so that the
+ * blocks of every head can drain it (each keeps claiming until its head is
+ * empty or it reaches the cap; a head has at least floor(nb / heads) >=
+ * nb / (2 heads) blocks). */
+__host__ __device__ inline uint64_t steal_cap(uint64_t sh, uint64_t nb)
+{
+	return 2 * ((sh + nb - 1) / nb) + 32;
+}
 
 struct RxArgs {
 	uint8_t *umem;
@@ -346,6 +354,12 @@ struct Nat64Args {
 	uint32_t *xlist;           /* slow frames, xregion per fast wave    */
 	uint32_t *xcount;
 	uint32_t xregion, nregions;
+	uint64_t xcap;             /* entries of the slow list              */
+	/* the fast kernel's shared tiles, as RxArgs.steal (xdp_rx_db_kernel):
+	 * counters (nullable), their set, and the tiles (set by the
+	 * launcher) */
+	uint32_t *steal;
+	uint32_t steal_set, steal_16ths, steal_tiles;
 	/* dynamic state (xdpgpu_nat64_dynamic): a hit stamps last_seen with
 	 * the batch clock `now`; a miss, or a hit on an entry that timed out
 	 * (last_seen < thr, not static), is left untouched and listed for the

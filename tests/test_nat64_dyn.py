@@ -319,12 +319,13 @@ def test_gpu_dyn_wrap_and_egress():
 
 @pytest.mark.gpu
 def test_gpu_dyn_large():
-    """a 256 K-frame batch from 2000 sources over a /16 with 200 static
-    entries (the fast kernel's path), then the same frames past the timeout
-    (every dynamic entry timed out: all listed, all hits)"""
+    """a 1 M-frame batch from 2000 sources over a /16 with 200 static
+    entries (the fast kernel's path, with its shared tiles: 64 tiles per
+    CU), then the same frames past the timeout (every dynamic entry timed
+    out: all listed, all hits)"""
     rng = np.random.default_rng(11)
     cfg = pool_cfg(mask_bits=16)
-    n, nsrc = 1 << 18, 2000
+    n, nsrc = 1 << 20, 2000
     ks = rng.integers(1, nsrc + 1, n)
     base = dyn_frames([src(1)], "u")[0]
     fr0 = base + bytes(max(0, 96 - len(base)))
@@ -332,10 +333,9 @@ def test_gpu_dyn_large():
     umem = np.zeros(n * stride + 256, np.uint8)
     descs = np.zeros(n, xdpgpu.DESC_DTYPE)
     tmpl = np.frombuffer(fr0, np.uint8)
-    for k in range(n):
-        off = k * stride + 64
-        umem[off:off + len(fr0)] = tmpl
-        descs[k] = (off, len(fr0), 0)
+    umem[64:64 + n * stride].reshape(n, stride)[:, :len(fr0)] = tmpl
+    descs["addr"] = np.arange(n, dtype=np.uint64) * stride + 64
+    descs["len"] = len(fr0)
     # per-frame source: rewrite the last 16 bits of the source and fix the
     # UDP checksum incrementally (ones' complement of the difference)
     lo = (ks + 0x1000).astype(np.uint32)
