@@ -45,7 +45,9 @@ t0 = s[:, 0].min()
 us = (s - t0) / 100.0            # 100 MHz ticks -> us
 ph = s4[live][:, 4:8].astype(np.int64) / 100.0   # tail time per batch kind
 waves = np.nonzero(live)[0]
-xcd = (waves // 4) % 8
+# blocks of the double-buffered kernel (15 waves each) go round-robin to
+# the 8 XCDs
+xcd = (waves // 15) % 8
 
 
 def pct(a):
@@ -57,6 +59,11 @@ out = {"waves": int(live.sum()), "tail_us": pct(us[:, 2] - us[:, 1]),
        "tail_payload_us": pct(ph[:, 2]), "tail_wait_us": pct(ph[:, 3]),
        "start_us": pct(us[:, 0]), "loop_end_us": pct(us[:, 1]),
        "end_us": pct(us[:, 2]), "loop_us": pct(us[:, 1] - us[:, 0])}
+# its shared-tile heads (block b: head b mod 16)
+blk = waves // 15
+head = blk % 16
+out["per_head_loop_end_median"] = [round(float(np.median(us[head == k, 1])), 1) for k in range(16)]
+out["per_head_loop_end_max"] = [round(float(us[head == k, 1].max()), 1) for k in range(16)]
 out["per_xcd_loop_end_median"] = [round(float(np.median(us[xcd == k, 1])), 1) for k in range(8)]
 out["per_xcd_loop_end_max"] = [round(float(us[xcd == k, 1].max()), 1) for k in range(8)]
 # where each wave ran: HW_ID (wave 3:0, simd 5:4, cu 11:8, sh 12, se 15:13),
