@@ -1105,8 +1105,10 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 	/* GEN false: the fast shape's records; IPv6/UDP (V6 builds) has its
 	 * L4 header 40 bytes after l3 and no over-read byte */
 	const bool r6 = !GEN && (rv.z & XDPGPU_F_IPV6);
+	/* IPv4 ICMP (V6 builds): no over-read byte either */
+	const bool nov = r6 || ((rv.z >> 8) & 0xff) == 1;
 	const uint32_t l4 = GEN ? (rv.w & 0xffff) : ((rv.z >> 16) & 0xff) + (r6 ? 40u : 20u);
-	const uint32_t rhi = GEN ? (ye.w & 0xffff) : l4 + cl + (r6 ? 0u : (cl & 1));
+	const uint32_t rhi = GEN ? (ye.w & 0xffff) : l4 + cl + (nov ? 0u : (cl & 1));
 	uint64_t lim = eff + rhi;
 	lim = lim < a.usize ? lim : a.usize;
 	/* absolute range [lo, lim), streamed from its 16-byte aligned start */
@@ -1530,19 +1532,26 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 	const uint32_t tot = bswap16(r[4] & 0xffff);
 	const uint32_t proto = r[5] >> 24;
 	const bool udp = proto == 17;
+	/* V6 builds (the 44-byte network_tuple and no tuple: IMIX) also take
+	 * IPv4 ICMP: the message sum with no pseudo header and no over-read
+	 * byte (an odd length zero padded, do_csum), no ports in the key */
+	const bool icmp = V6 && proto == 1;
 	const uint32_t thl = ((r[11] >> 20) & 0xf) * 4;
 	const uint32_t cl = udp ? bswap16(r[9] >> 16) : tot - 20;
 	const bool ok_udp = (len >= l4 + 8) & (cl >= 8) & (l4 + cl <= l3 + tot);
 	const bool ok_tcp = (len >= l4 + 20) & (thl >= 20) & (l4 + thl <= len) &
 			    (cl >= thl);
+	const bool ok_icmp = (len >= l4 + 8) & (cl >= 8);
 	bool fast = (!a.force_generic) & staged &
 		    ((r[3] & 0x00ffffffu) == 0x00450008u) &
-		    ((r[5] & 0xff3fu) == 0) & (udp | (proto == 6)) &
-		    (tot >= 20) & (l3 + tot <= len) & (udp ? ok_udp : ok_tcp);
+		    ((r[5] & 0xff3fu) == 0) & (udp | (proto == 6) | icmp) &
+		    (tot >= 20) & (l3 + tot <= len) &
+		    (udp ? ok_udp : icmp ? ok_icmp : ok_tcp);
 	/* a checksum range (with udp_csum's odd over-read byte) that ends
 	 * past the window: the bulk kernel adds the payload sum */
 	const bool shape = fast;
-	fast = shape & (l4 + cl + (cl & 1) <= 64u);
+	const uint32_t over = icmp ? 0u : (cl & 1);
+	fast = shape & (l4 + cl + over <= 64u);
 	bool bulk = shape & !fast & (a.res != nullptr);
 
 	/* V6: untagged IPv6 + UDP with no extension header, the generic
@@ -1577,26 +1586,28 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 	/* 4. fast frames: flow key, hash, tuple, checksums, verdict */
 	const uint32_t sa = (r[6] >> 16) | (r[7] << 16);
 	const uint32_t da = (r[7] >> 16) | (r[8] << 16);
-	const uint32_t ports = (r[8] >> 16) | (r[9] << 16);
+	const uint32_t ports = icmp ? 0u : (r[8] >> 16) | (r[9] << 16);
 	/* IPv4 header sum, check word (r6 low half) excluded */
 	const uint64_t s3 = (uint64_t)(r[3] & 0xffff0000u) + r[4] + r[5] +
 			    (r[6] & 0xffff0000u) + r[7] + (r[8] & 0xffffu);
 	const uint32_t c3 = r[6] & 0xffff;
-	const uint32_t c4 = udp ? (r[10] & 0xffff) : (r[12] >> 16);
+	const uint32_t c4 = udp ? (r[10] & 0xffff) : icmp ? (r[9] & 0xffff) : (r[12] >> 16);
 	/* L4 sum over [34, end) of the shifted frame with the pseudo
 	 * header, check word excluded; udp_csum's odd-length over-read
 	 * byte included (lib_checksum.h:142-179).  For a bulk frame the
 	 * window part: frame bytes [l4, 64) (F[16], F[17] are zero). */
-	const int32_t e = (int32_t)(34 + cl + (cl & 1));
-	uint64_t s4 = (uint64_t)(r[8] & 0xffff0000u) + sa + da +
-		      ((uint64_t)(proto + cl) << 8);
+	const int32_t e = (int32_t)(34 + cl + over);
+	uint64_t s4 = (uint64_t)(r[8] & 0xffff0000u) +
+		      (icmp ? 0ull : (uint64_t)sa + da + ((uint64_t)(proto + cl) << 8));
 #pragma unroll
 	for (int j = 9; j < 16; j++) {
 		uint32_t m = first_bytes(e - 4 * j);
+		if (j == 9)
+			m &= icmp ? 0xffff0000u : 0xffffffffu;
 		if (j == 10)
 			m &= udp ? 0xffff0000u : 0xffffffffu;
 		if (j == 12)
-			m &= udp ? 0xffffffffu : 0x0000ffffu;
+			m &= udp || icmp ? 0xffffffffu : 0x0000ffffu;
 		s4 += r[j] & m;
 	}
 	uint32_t key[11] = {0, 0, 0xffff0000u, sa, ports & 0xffff,

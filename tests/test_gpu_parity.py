@@ -144,7 +144,7 @@ def test_pool_vs_oracle(dev, name, kind, size, seed, n, kw, window, tune):
 
 
 def bulk_frames(seed: int, n: int):
-    """Fast-shape IPv4 UDP/TCP frames of every length class around and past
+    """Fast-shape IPv4 UDP/TCP/ICMP frames of every length class around and past
     the 64-byte header window (0..2 VLAN tags, odd lengths, trailing pad,
     bad and absent checksums), 16-byte aligned with random gaps; the last
     frame ends at the UMEM end with an odd UDP length (over-read past the
@@ -161,6 +161,10 @@ def bulk_frames(seed: int, n: int):
             fr = F.v4_frame(17, seg, tags=tags)
             if rng.random() < 0.05:
                 fr = fr[:-len(seg)] + F.set_csum(seg, 6, 0)
+        elif rng.random() < 0.2:
+            # IPv4 ICMP: the fast shape of the network_tuple builds (no
+            # pseudo header, no over-read byte)
+            fr = F.v4_frame(1, F.icmp(8, 0, b"\x12\x34\x00\x01" + pay), tags=tags)
         else:
             fr = F.v4_frame(6, F.tcp(int(rng.integers(1, 65536)), 80, pay,
                                      doff=int(rng.integers(5, 9))), tags=tags)
