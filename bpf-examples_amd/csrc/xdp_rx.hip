@@ -1111,6 +1111,16 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 	const uint32_t rhi = GEN ? (ye.w & 0xffff) : l4 + cl + (nov ? 0u : (cl & 1));
 	uint64_t lim = eff + rhi;
 	lim = lim < a.usize ? lim : a.usize;
+	/* an IPv6/UDP frame's network_tuple words (the tile stored none):
+	 * frame bytes [16, 64), loaded here so that the round trip overlaps
+	 * the payload streaming */
+	const bool tup6 = !GEN && act && r6 && a.tup && a.tuple_fmt == XDPGPU_TUPLE_NET;
+	uint4 h1 = make_uint4(0, 0, 0, 0), h2 = h1, h3 = h1;
+	if (tup6) {
+		h1 = *reinterpret_cast<const uint4 *>(a.umem + eff + 16);
+		h2 = *reinterpret_cast<const uint4 *>(a.umem + eff + 32);
+		h3 = *reinterpret_cast<const uint4 *>(a.umem + eff + 48);
+	}
 	/* absolute range [lo, lim), streamed from its 16-byte aligned start */
 	const uint64_t lo = eff + (GEN ? (ye.z & 0xffff) : 64u);
 	const uint64_t lo_al = lo & ~15ull;
@@ -1218,13 +1228,9 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 			st_nt16(a.res + i, rv);
 		else
 			*reinterpret_cast<uint4 *>(a.res + i) = rv;
-		if (!GEN && r6 && a.tup && a.tuple_fmt == XDPGPU_TUPLE_NET) {
-			/* an IPv6/UDP frame's network_tuple (the tile stored
-			 * none): the addresses and ports from the frame's
-			 * first line, which the payload stream just read */
-			const uint4 h1 = *reinterpret_cast<const uint4 *>(a.umem + eff + 16);
-			const uint4 h2 = *reinterpret_cast<const uint4 *>(a.umem + eff + 32);
-			const uint4 h3 = *reinterpret_cast<const uint4 *>(a.umem + eff + 48);
+		if (tup6) {
+			/* the addresses and ports, from the words loaded with
+			 * the batch */
 			const uint32_t w[12] = {h1.x, h1.y, h1.z, h1.w, h2.x, h2.y,
 						h2.z, h2.w, h3.x, h3.y, h3.z, h3.w};   /* dwords 4..15 */
 			uint32_t *t = reinterpret_cast<uint32_t *>(a.tup + 44 * i);
