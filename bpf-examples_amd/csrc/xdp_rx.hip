@@ -1239,9 +1239,11 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 				t[k] = (w[1 + k] >> 16) | (w[2 + k] << 16);
 				t[5 + k] = (w[5 + k] >> 16) | (w[6 + k] << 16);
 			}
-			t[4] = w[9] >> 16;
-			t[9] = w[10] & 0xffffu;
-			t[10] = 17u | (10u << 16);
+			/* ports for UDP; ICMPv6 has none */
+			const uint32_t p6 = (rv.z >> 8) & 0xff;
+			t[4] = p6 == 17 ? w[9] >> 16 : 0u;
+			t[9] = p6 == 17 ? w[10] & 0xffffu : 0u;
+			t[10] = p6 | (10u << 16);
 		}
 		a.verdict[i] = (uint8_t)(drop ? XDPGPU_DROP : XDPGPU_REDIRECT);
 		my_bytes += dv.z;
@@ -1564,14 +1566,22 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 	 * parse's conditions (parse_ip6hdr, parse_udphdr): the UDP header at
 	 * 54-61 is in the window, the pseudo header's addresses at 22-53;
 	 * csum_ipv6_magic, an odd length zero padded, a stored 0 not absent */
-	bool v6 = false;
+	bool v6 = false, i6 = false;
 	uint32_t ulen6 = 0;
 	if constexpr (V6) {
 		const uint32_t plen = bswap16(F[4] >> 16);
-		ulen6 = bswap16(F[14] >> 16);
+		const uint32_t nh6 = F[5] & 0xff;
+		/* ICMPv6 too (its range the payload length), but neither NDP
+		 * (PASS, af_xdp_kern.c:114-148) nor an echo request the echo
+		 * responder answers (the exception path's TX rewrite) */
+		const uint32_t ity = (F[13] >> 16) & 0xff;
+		i6 = (nh6 == 58) & (plen >= 8) & !((ity >= 133) & (ity <= 137)) &
+		     !((a.flags & XDPGPU_CFG_ICMP6_ECHO) && ity == 128);
+		ulen6 = i6 ? plen : bswap16(F[14] >> 16);
 		v6 = (!a.force_generic) & staged & !v1 & ((F[3] & 0xffffu) == 0xdd86u) &
-		     (((F[3] >> 20) & 0xf) == 6) & ((F[5] & 0xff) == 17) & (len >= 62) &
+		     (((F[3] >> 20) & 0xf) == 6) & ((nh6 == 17) | i6) & (len >= 62) &
 		     (54 + plen <= len) & (ulen6 >= 8) & (ulen6 <= plen) & (a.res != nullptr);
+		i6 = i6 & v6;
 		/* always through the bulk pass, which also writes the
 		 * network_tuple (its addresses are not among the words a tile
 		 * keeps for its stores); a payload inside the window is an
@@ -1624,7 +1634,7 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 	bool udpv = udp;
 	if constexpr (V6) {
 		/* the v6 frame's terms (selected per lane: branch free) */
-		uint64_t p6 = (uint64_t)__builtin_bswap32(ulen6) + __builtin_bswap32(17u);
+		uint64_t p6 = (uint64_t)__builtin_bswap32(ulen6) + __builtin_bswap32(i6 ? 58u : 17u);
 #pragma unroll
 		for (int k = 0; k < 4; k++) {
 			const uint32_t sk = (F[5 + k] >> 16) | (F[6 + k] << 16);
@@ -1634,18 +1644,20 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 			key[5 + k] = v6 ? dk : key[5 + k];
 		}
 		const int32_t e6 = (int32_t)(54 + ulen6);
-		const uint64_t s46 = p6 + (F[13] & 0xffff0000u) + (F[14] & first_bytes(e6 - 56)) +
-				     (F[15] & first_bytes(e6 - 60) & 0xffff0000u);
-		key[4] = v6 ? (F[13] >> 16) : key[4];
-		key[9] = v6 ? (F[14] & 0xffffu) : key[9];
-		key[10] = v6 ? (17u | (10u << 16)) : key[10];
+		/* check word: UDP bytes 60-61, ICMPv6 bytes 56-57 */
+		const uint64_t s46 = p6 + (F[13] & 0xffff0000u) +
+				     (F[14] & first_bytes(e6 - 56) & (i6 ? 0xffff0000u : ~0u)) +
+				     (F[15] & first_bytes(e6 - 60) & (i6 ? ~0u : 0xffff0000u));
+		key[4] = v6 ? (i6 ? 0u : F[13] >> 16) : key[4];
+		key[9] = v6 ? (i6 ? 0u : F[14] & 0xffffu) : key[9];
+		key[10] = v6 ? ((i6 ? 58u : 17u) | (10u << 16)) : key[10];
 		s4v = v6 ? s46 : s4v;
 		s3v = v6 ? 0xffffull : s3v;      /* no IPv6 header checksum: l3 ok */
 		c3v = v6 ? 0u : c3v;
-		c4v = v6 ? (F[15] & 0xffffu) : c4v;
+		c4v = v6 ? (i6 ? F[14] & 0xffffu : F[15] & 0xffffu) : c4v;
 		clv = v6 ? ulen6 : clv;
 		l4v = v6 ? 54u : l4v;
-		protov = v6 ? 17u : protov;
+		protov = v6 ? (i6 ? 58u : 17u) : protov;
 		udpv = udpv & !v6;               /* a stored 0 is not absent */
 	}
 	const uint32_t l3c = v6 ? 0u : ~fold16(s3v) & 0xffff;

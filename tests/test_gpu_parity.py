@@ -326,3 +326,63 @@ def test_ip_fast_csum_primitive_vectors(dev):
     torch.cuda.synchronize()
     np.testing.assert_array_equal(out.cpu().numpy().view(np.uint16), vec["ip_fast_csum"])
     ctx.close()
+
+
+def icmp6_frames(seed: int, n: int):
+    """Untagged ICMPv6 frames of every type class (NDP 133-137, echo
+    request/reply, errors, unknown), lengths around and past the 64-byte
+    window (odd ones too), some with bad checksums or a trailing pad, 16-byte
+    aligned; and UDP/IPv6 frames beside them."""
+    import frames as F
+    rng = np.random.default_rng(seed)
+    types = [1, 2, 3, 4, 128, 129, 130, 133, 134, 135, 136, 137, 143, 200]
+    blobs = []
+    for k in range(n):
+        plen = int(rng.integers(0, 60)) if k % 3 else int(rng.integers(0, 1500))
+        pay = rng.integers(0, 256, plen, dtype=np.uint8).tobytes()
+        if k % 5 == 4:
+            fr = F.v6_frame(17, F.udp(int(rng.integers(1, 65536)), 53, pay))
+        else:
+            typ = types[k % len(types)]
+            fr = F.v6_frame(58, F.icmp(typ, int(rng.integers(0, 3)), b"\x00\x01\x00\x02" + pay))
+        if rng.random() < 0.1:
+            b = bytearray(fr)
+            b[-1 - int(rng.integers(0, 8))] ^= 0x5A
+            fr = bytes(b)
+        if rng.random() < 0.1:
+            fr += rng.integers(0, 256, int(rng.integers(1, 9)), dtype=np.uint8).tobytes()
+        blobs.append(fr)
+    offs, o = [], 0
+    for fr in blobs:
+        o += 16 * int(rng.integers(0, 3))
+        offs.append(o)
+        o = (o + len(fr) + 15) & ~15
+    umem = np.zeros(o + 16, np.uint8)
+    for off, fr in zip(offs, blobs):
+        umem[off:off + len(fr)] = np.frombuffer(fr, np.uint8)
+    descs = np.zeros(n, xdpgpu.DESC_DTYPE)
+    descs["addr"] = offs
+    descs["len"] = [len(fr) for fr in blobs]
+    return umem, descs
+
+
+@pytest.mark.parametrize("tune", [0, 1 << 15, 1 << 21])
+def test_v6_build_icmp_vs_oracle(dev, golden, tune):
+    """The network_tuple / no-tuple builds with and without the echo
+    responder: IPv4 ICMP and ICMPv6 other than NDP (and, with the
+    responder, other than echo requests) go through the fast shape and the
+    bulk pass; the golden fixtures, ICMPv6 frames of every type class and
+    the IMIX pool against the oracle."""
+    fx, _ = golden
+    cases = [("golden", fx["umem"], fx["descs"].view(xdpgpu.DESC_DTYPE)),
+             ("icmp6", *icmp6_frames(31, 2000))]
+    um, ds, _ = xdpgpu.pool_generate(300000, xdpgpu.POOL_IMIX, 64, 0x5EED0003)
+    cases.append(("imix", um, ds))
+    for name, umem, descs in cases:
+        for flags, iv, fmt in ((0x5, 0, 2), (0x4, 7, 0), (0x7, 0x1234, 2)):
+            ou = umem.copy()
+            ov, ores, otup, ost = oracle.process(ou, descs, flags, iv, fmt)
+            v, res, tup, um2, st = run_dev(umem, descs, flags, iv, fmt, 64, tune)
+            assert_same((v, res, tup, um2), (ov, ores, otup, ou),
+                        f"{name}/{flags:#x}/fmt{fmt}")
+            oracle_stats_match(st, ost)
