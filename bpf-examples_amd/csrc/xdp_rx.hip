@@ -1450,6 +1450,19 @@ struct TileOut {
  * store the configuration does not need, at an offset past its resource's
  * size (dropped by the hardware); no branches. */
 constexpr int kTileStores = 5;
+/* cache policy (buffer aux bits) of the tile's verdict, record and 16-byte
+ * tuple stores: build knobs for A/B (0 plain, 2 non-temporal).  Config 2,
+ * alternating processes (tools/gpu_ab_stores.sh): non-temporal verdicts
+ * 0.3292 vs 0.3376 ms plain; plain records and tuples 0.400 ms */
+#ifndef XDP_VERDICT_AUX
+#define XDP_VERDICT_AUX 2
+#endif
+#ifndef XDP_REC_AUX
+#define XDP_REC_AUX 2
+#endif
+#ifndef XDP_TUP4_AUX
+#define XDP_TUP4_AUX 2
+#endif
 __device__ __forceinline__ void store_tile(const RxArgs &a, const TileOut &o)
 {
 	constexpr uint32_t kOff = 0x80000000u;
@@ -1459,14 +1472,14 @@ __device__ __forceinline__ void store_tile(const RxArgs &a, const TileOut &o)
 	const __amdgpu_buffer_rsrc_t rv =
 		__builtin_amdgcn_make_buffer_rsrc(a.verdict + o.t0, 0, kWave, kFmt);
 	__builtin_amdgcn_raw_buffer_store_b8((uint8_t)o.verdict, rv,
-					     (fl & 1) ? o.li : kOff, 0, 0);
+					     (fl & 1) ? o.li : kOff, 0, XDP_VERDICT_AUX);
 	const bool out = fl & 2;
 	/* a missing output: a resource of no records over the verdicts */
 	const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
 		a.res ? (void *)(a.res + o.t0) : (void *)a.verdict, 0,
 		a.res ? 16 * kWave : 0, kFmt);
 	__builtin_amdgcn_raw_buffer_store_b128((v4u_t){o.rec.x, o.rec.y, o.rec.z, o.rec.w},
-					       rr, out ? 16 * o.li : kOff, 0, 2 /* nt */);
+					       rr, out ? 16 * o.li : kOff, 0, XDP_REC_AUX);
 	const bool net = a.tuple_fmt == XDPGPU_TUPLE_NET;
 	const bool tup = a.tup && (net || a.tuple_fmt == XDPGPU_TUPLE_V4);
 	const uint32_t tb = net ? 44u : 16u;
@@ -1484,7 +1497,7 @@ __device__ __forceinline__ void store_tile(const RxArgs &a, const TileOut &o)
 	if (net) {
 		__builtin_amdgcn_raw_buffer_store_b128(w0, rt, b, 0, 0);
 	} else {
-		__builtin_amdgcn_raw_buffer_store_b128(w0, rt, b, 0, 2);
+		__builtin_amdgcn_raw_buffer_store_b128(w0, rt, b, 0, XDP_TUP4_AUX);
 	}
 	__builtin_amdgcn_raw_buffer_store_b128((v4u_t){o.ports & 0xffff, 0u, 0u, 0xffff0000u},
 					       rt, net && tout ? b + 16 : kOff, 0, 0);
