@@ -1088,6 +1088,14 @@ __device__ __forceinline__ void egress_tile(const Nat64Args &a, const Tables &T,
  * frames go to the block's list (an LDS atomic reserves each wave's 64
  * entries), which xdp_nat64_kernel walks as one region per block. */
 constexpr int kCuWavesN = 16;
+/* the fast kernel's action and output-descriptor stores non-temporal
+ * (build knob for A/B): ingress 1.006 vs 1.048 ms with plain stores,
+ * alternating processes (tools/gpu_ab_outnt.sh) */
+#ifndef XDP_NAT64_OUT_NT
+#define XDP_NAT64_OUT_NT 1
+#endif
+constexpr bool kOutNt = XDP_NAT64_OUT_NT != 0;
+typedef uint32_t v4u_n __attribute__((ext_vector_type(4)));
 /* the window DMA's cache policy: plain, not non-temporal — the frame's
  * lines are rewritten in place right after (an in-place rewrite of 64 of
  * each 128 bytes: 0.83 ms per 16 M frames with plain loads, 1.18 ms with
@@ -1297,7 +1305,10 @@ __global__ __launch_bounds__(kCuBlockN, 1) void xdp_nat64_fast_kernel(Nat64Args 
 		}
 		__builtin_amdgcn_wave_barrier();
 		if (active && !slow) {
-			a.action[i] = (uint8_t)act;
+			if constexpr (kOutNt)
+				__builtin_nontemporal_store((uint8_t)act, a.action + i);
+			else
+				a.action[i] = (uint8_t)act;
 			uint4 od = dv;
 			if (xlate) {
 				/* the frame starts 20 bytes later (IPv4) or
@@ -1307,7 +1318,12 @@ __global__ __launch_bounds__(kCuBlockN, 1) void xdp_nat64_fast_kernel(Nat64Args 
 				od.y = (uint32_t)(na >> 32);
 				od.z = EG ? len + 20 : len - 20;
 			}
-			*reinterpret_cast<uint4 *>(a.out + i) = od;
+			if constexpr (kOutNt) {
+				const v4u_n o4 = {od.x, od.y, od.z, od.w};
+				__builtin_nontemporal_store(o4, reinterpret_cast<v4u_n *>(a.out + i));
+			} else {
+				*reinterpret_cast<uint4 *>(a.out + i) = od;
+			}
 		}
 		qa = qb;
 		qb = qc;

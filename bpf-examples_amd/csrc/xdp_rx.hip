@@ -1076,6 +1076,12 @@ __device__ __forceinline__ uint4 ld_nt16(const void *p)
 #define XDP_TAIL_REC_NT 1
 #endif
 constexpr bool kTailRecNt = XDP_TAIL_REC_NT != 0;
+/* the bulk pass's verdict bytes non-temporal (build knob): IMIX 2.260 vs
+ * 2.252 ms plain, alternating processes (tools/gpu_ab_outnt.sh) */
+#ifndef XDP_TAIL_VERDICT_NT
+#define XDP_TAIL_VERDICT_NT 0
+#endif
+constexpr bool kTailVerdictNt = XDP_TAIL_VERDICT_NT != 0;
 template <int U, bool NT, bool GEN, int G>
 __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 					   uint4 *part4, int lane,
@@ -1245,7 +1251,11 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 			t[9] = p6 == 17 ? w[10] & 0xffffu : 0u;
 			t[10] = p6 | (10u << 16);
 		}
-		a.verdict[i] = (uint8_t)(drop ? XDPGPU_DROP : XDPGPU_REDIRECT);
+		if constexpr (kTailVerdictNt)
+			__builtin_nontemporal_store((uint8_t)(drop ? XDPGPU_DROP : XDPGPU_REDIRECT),
+						    a.verdict + i);
+		else
+			a.verdict[i] = (uint8_t)(drop ? XDPGPU_DROP : XDPGPU_REDIRECT);
 		my_bytes += dv.z;
 	}
 	if (a.stats) {
