@@ -2028,6 +2028,12 @@ constexpr int kCuBlock = kCuWaves * kWave;
 /* DIAG (diagnostic A/B, cfg.tune bits 16-17): 1 = no compute (the
  * window's XOR stored as verdict, record and tuple: the same memory
  * traffic), 2 = the full compute with no output stores. */
+/* cache policy of the tile loop's descriptor DMA (build knob for A/B):
+ * non-temporal, config 2 0.3249 vs 0.3298 ms plain, alternating processes
+ * (tools/gpu_ab_desc.sh; 1500 B and IMIX within 0.3 %) */
+#ifndef XDP_DESC_AUX
+#define XDP_DESC_AUX 2
+#endif
 template <bool FRAGS, int DIAG = 0, bool V6 = false>
 __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 {
@@ -2137,7 +2143,7 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 		if (DBG_BAD(di >= nfr, 5, di))
 			di = 0;
 		__builtin_amdgcn_global_load_lds((const void *)(a.desc + di),
-						 (lds_void_t *)slot, 16, 0, 0);
+						 (lds_void_t *)slot, 16, 0, XDP_DESC_AUX);
 	};
 	/* the previous step's outputs, stored after this step's wait (the
 	 * first step stores an empty TileOut: every lane out of range) */
