@@ -2029,10 +2029,12 @@ constexpr int kCuBlock = kCuWaves * kWave;
  * window's XOR stored as verdict, record and tuple: the same memory
  * traffic), 2 = the full compute with no output stores. */
 /* cache policy of the tile loop's descriptor DMA (build knob for A/B):
- * non-temporal, config 2 0.3249 vs 0.3298 ms plain, alternating processes
- * (tools/gpu_ab_desc.sh; 1500 B and IMIX within 0.3 %) */
+ * plain.  Non-temporal ran config 2 at 0.3249 vs 0.3298 ms
+ * (tools/gpu_ab_desc.sh) but the maximum-size frames test then raised an
+ * illegal memory access (tests/test_max_frames.py, round-2 evidence run);
+ * not understood, not used */
 #ifndef XDP_DESC_AUX
-#define XDP_DESC_AUX 2
+#define XDP_DESC_AUX 0
 #endif
 template <bool FRAGS, int DIAG = 0, bool V6 = false>
 __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
