@@ -499,8 +499,18 @@ int rx_run(const struct rx_source *src, const struct rx_opts *o,
 				uint32_t e = s->n - 1;
 				while (e && (s->d[e - 1].options & XDPGPU_PKT_CONTD))
 					e--;
-				if (e)
+				if (e) {
 					s->n = e;
+				} else if (s->n == o->batch) {
+					/* one packet fills the whole batch and goes on:
+					 * it cannot be cut (its verdict needs all of it) */
+					fprintf(stderr, "%s: a packet has more than -b %u fragments\n",
+						o->prog, o->batch);
+					rc = -E2BIG;
+					break;
+				}
+				/* else the count (-C) ends inside the packet: its
+				 * fragments go as they are (ABORTED, frags.hip) */
 			}
 			rc = xdpgpu_submit(ctx, k & 1, s->d, s->n, s->v, NULL, NULL);
 			if (rc)
@@ -584,34 +594,59 @@ struct injector {
 	const char *ifname;
 	volatile uint64_t received;  /* frames the RX loop has taken */
 	volatile uint64_t sent;
+	volatile uint64_t lost;      /* frames the kernel dropped (no fill
+				      * buffer, RX ring full): given up on  */
 	volatile int stop;
+	volatile int done;           /* every frame sent                   */
 	int rc;
 };
 
 /* Sends the source's frames into the peer, cycling it, keeping at most
  * ring_size / 2 frames ahead of the receiver (no RX-ring overflow: every
- * frame sent is received, so verdicts line up with the source). */
+ * frame sent is received, so verdicts line up with the source).  A window
+ * that does not move for 100 ms means the kernel dropped frames of it (a
+ * frame finds no fill buffer when the receiver holds them all): those
+ * count as lost and sending goes on. */
 static void *inject_main(void *arg)
 {
 	struct injector *in = arg;
 	const struct rx_source *src = in->lv->inject;
 	const uint64_t window = in->lv->ring_size / 2;
 	uint64_t k = 0;
+	const int fd = xsk_packet_socket(in->ifname);
 
+	if (fd < 0) {
+		in->rc = fd;
+		return NULL;
+	}
+
+	uint64_t lost = 0, last_rx = 0, t_stall = 0;
 	while (!in->stop && k < in->lv->inject_count) {
 		uint64_t m = in->lv->inject_count - k;
-		const uint64_t room = window - (k - in->received);
-		if (k - in->received >= window) {
+		const uint64_t got = in->received + lost;
+		const uint64_t ahead = k > got ? k - got : 0;
+		if (ahead >= window) {
+			const uint64_t t = now_ns();
+			if (in->received != last_rx || !t_stall) {
+				last_rx = in->received;
+				t_stall = t;
+			} else if (t - t_stall > 100000000ull) {
+				lost += ahead;
+				in->lost = lost;
+				t_stall = 0;
+			}
 			usleep(20);
 			continue;
 		}
+		t_stall = 0;
+		const uint64_t room = window - ahead;
 		m = m < room ? m : room;
 		m = m < 256 ? m : 256;
 		const uint32_t at = (uint32_t)(k % src->n);
 		if (m > src->n - at)
 			m = src->n - at;
-		const int r = xsk_inject(in->ifname, src->umem,
-					 (const struct xdp_desc *)(src->descs + at), (uint32_t)m);
+		const int r = xsk_inject_fd(fd, src->umem,
+					    (const struct xdp_desc *)(src->descs + at), (uint32_t)m);
 		if (r < 0) {
 			in->rc = r;
 			break;
@@ -619,7 +654,56 @@ static void *inject_main(void *arg)
 		k += (uint64_t)r;
 		in->sent = k;
 	}
+	close(fd);
+	in->done = 1;
 	return NULL;
+}
+
+/* Give n frames back to the fill ring.  The kernel publishes the fill
+ * ring's consumer index lazily (it can deliver a frame to the RX ring
+ * before its fill entry reads as consumed), so a full fill ring is waited
+ * out, as xdpsock's reserve loop does (rx_drop, xdpsock.c:1472-1482: wake
+ * the kernel and retry).  0 or -errno (-ETIMEDOUT after 5 s). */
+static int fill_all(struct xsk_sock *x, const uint64_t *a, uint32_t n)
+{
+	const uint64_t t0 = now_ns();
+	for (uint32_t spin = 0;; spin++) {
+		const int r = xsk_fill(x, a, n);
+		if (r != -ENOSPC)
+			return r;
+		xsk_wakeup_rx(x, 0);
+		if (spin > 64) {
+			if (now_ns() - t0 > 5000000000ull)
+				return -ETIMEDOUT;
+			usleep(10);
+		}
+	}
+}
+
+/* Queue n TX descriptors whatever the ring's state: while the TX ring has
+ * no room, recycle what the kernel has sent (completion ring -> fill ring)
+ * and kick it, as l2fwd's reserve loop does (complete_tx_l2fwd + kick_tx,
+ * xdpsock.c:1736-1746).  scratch holds cap addresses.  0 or -errno
+ * (-ETIMEDOUT when the kernel sends nothing for 5 s). */
+static int tx_all(struct xsk_sock *x, const struct xdp_desc *d, uint32_t n,
+		  uint64_t *scratch, uint32_t cap)
+{
+	const uint64_t t0 = now_ns();
+	for (uint32_t spin = 0;; spin++) {
+		int r = xsk_tx(x, d, n);
+		if (r != -ENOSPC)
+			return r;
+		const uint32_t c = xsk_complete(x, scratch, cap);
+		if (c && (r = fill_all(x, scratch, c)))
+			return r;
+		if ((r = xsk_kick_tx(x)))
+			return r;
+		if (!c && spin > 64) {
+			if (now_ns() - t0 > 5000000000ull)
+				return -ETIMEDOUT;
+			usleep(10);
+		}
+	}
 }
 
 int rx_run_live(const struct rx_live *lv, const struct rx_opts *o, struct rx_totals *out)
@@ -672,21 +756,25 @@ int rx_run_live(const struct rx_live *lv, const struct rx_opts *o, struct rx_tot
 		rc = (rc == -EPERM || rc == -EACCES || rc == -EAFNOSUPPORT) ? 1 : rc;
 		goto out;
 	}
-	rc = xdpgpu_init(&cfg, &ctx);
-	if (rc) {
-		fprintf(stderr, "%s: xdpgpu_init: %s%s\n", o->prog, strerror(-rc),
-			rc == -ENODEV ? " (no GPU: this build has no CPU fallback)" : "");
-		goto out;
-	}
-	rc = xdpgpu_register_umem(ctx, x.umem, x.umem_size, lv->frame_size, 0, 0);
-	if (rc) {
-		fprintf(stderr, "%s: xdpgpu_register_umem: %s %s\n", o->prog, strerror(-rc),
-			xdpgpu_last_error(ctx));
-		goto out;
+	if (!o->plumbing) {
+		rc = xdpgpu_init(&cfg, &ctx);
+		if (rc) {
+			fprintf(stderr, "%s: xdpgpu_init: %s%s\n", o->prog, strerror(-rc),
+				rc == -ENODEV ? " (no GPU: this build has no CPU fallback)" : "");
+			goto out;
+		}
+		rc = xdpgpu_register_umem(ctx, x.umem, x.umem_size, lv->frame_size, 0, 0);
+		if (rc) {
+			fprintf(stderr, "%s: xdpgpu_register_umem: %s %s\n", o->prog,
+				strerror(-rc), xdpgpu_last_error(ctx));
+			goto out;
+		}
 	}
 	for (int k = 0; k < 2; k++) {
-		slot[k].d = xdpgpu_host_alloc((uint64_t)o->batch * sizeof(*slot[k].d));
-		slot[k].v = xdpgpu_host_alloc(o->batch);
+		/* plumbing: no GPU, plain host memory */
+		const uint64_t db = (uint64_t)o->batch * sizeof(*slot[k].d);
+		slot[k].d = o->plumbing ? malloc(db) : xdpgpu_host_alloc(db);
+		slot[k].v = o->plumbing ? malloc(o->batch) : xdpgpu_host_alloc(o->batch);
 		if (!slot[k].d || !slot[k].v)
 			rc = -ENOMEM;
 	}
@@ -725,15 +813,15 @@ int rx_run_live(const struct rx_live *lv, const struct rx_opts *o, struct rx_tot
 	const uint64_t t0 = now_ns();
 	struct rx_stats_state st = { .t_prev = t0 };
 	const char *label = o->label ? o->label : o->prog;
-	uint64_t seen = 0;
+	uint64_t seen = 0, t_last = t0;    /* last frame received */
 	uint32_t k = 0, idle = 0;
 
 	while (!rc) {
 		struct rx_slot *s = &slot[k & 1];
 		const bool stop = rx_done || (o->count && seen >= o->count) ||
 				  (o->duration_ns && now_ns() - t0 >= o->duration_ns) ||
-				  (lv->inject && !o->count && !o->duration_ns &&
-				   seen >= lv->inject_count);
+				  (lv->inject && !o->count && !o->duration_ns && in.done &&
+				   (seen >= in.sent - in.lost || now_ns() - t_last > 200000000ull));
 		s->n = 0;
 		if (!stop) {
 			uint32_t want = o->batch;
@@ -741,19 +829,25 @@ int rx_run_live(const struct rx_live *lv, const struct rx_opts *o, struct rx_tot
 				want = (uint32_t)(o->count - seen);
 			s->n = xsk_rx(&x, (struct xdp_desc *)s->d, want);
 			if (s->n) {
-				rc = xdpgpu_submit(ctx, k & 1, s->d, s->n, s->v, NULL, NULL);
+				/* plumbing: every frame is the application's, as
+				 * in xdpsock's own loop (no verdict compute) */
+				if (o->plumbing)
+					memset(s->v, XDPGPU_REDIRECT, s->n);
+				else
+					rc = xdpgpu_submit(ctx, k & 1, s->d, s->n, s->v, NULL, NULL);
 				if (rc)
 					break;
 				s->busy = true;
 				s->first = seen;
 				seen += s->n;
 				in.received = seen;
+				t_last = now_ns();
 			}
 		}
 		/* the previous batch: wait, apply its verdicts to the rings */
 		struct rx_slot *p = &slot[(k + 1) & 1];
 		if (p->busy) {
-			rc = xdpgpu_wait(ctx, (k + 1) & 1);
+			rc = o->plumbing ? 0 : xdpgpu_wait(ctx, (k + 1) & 1);
 			if (rc)
 				break;
 			p->busy = false;
@@ -766,7 +860,7 @@ int rx_run_live(const struct rx_live *lv, const struct rx_opts *o, struct rx_tot
 				out->rx_frags++;
 				out->rx_pkts++;
 				out->rx_bytes += p->d[i].len;
-				if (v < XDPGPU_NUM_VERDICTS)
+				if (v < XDPGPU_NUM_VERDICTS && !o->plumbing)
 					out->verdict[v]++;
 				if (verdicts && p->first + i < o->count)
 					verdicts[p->first + i] = v;
@@ -788,17 +882,18 @@ int rx_run_live(const struct rx_live *lv, const struct rx_opts *o, struct rx_tot
 					fill[nfree + nfill++] = a - a % lv->frame_size;
 				}
 			}
-			if (ntx)
-				rc = xsk_tx(&x, txd, ntx);
-			if (!rc && nfill)
-				rc = xsk_fill(&x, fill + nfree, nfill);
+			/* the fill ring first: tx_all uses the same scratch */
+			if (nfill)
+				rc = fill_all(&x, fill + nfree, nfill);
+			if (!rc && ntx)
+				rc = tx_all(&x, txd, ntx, fill + nfree, lv->ring_size);
 			out->batches++;
 		}
 		/* sent frames back to the fill ring (complete_tx_l2fwd) */
 		if (!rc) {
 			uint32_t c = xsk_complete(&x, fill + nfree, lv->ring_size);
 			if (c)
-				rc = xsk_fill(&x, fill + nfree, c);
+				rc = fill_all(&x, fill + nfree, c);
 			else if (x.tx.cached_prod != x.tx.cached_cons)
 				(void)xsk_kick_tx(&x);
 		}
@@ -818,14 +913,22 @@ int rx_run_live(const struct rx_live *lv, const struct rx_opts *o, struct rx_tot
 				print_stats(o, out, &st, label, t);
 		}
 	}
-	for (int j = 0; j < 2; j++)
+	for (int j = 0; j < 2 && ctx; j++)
 		if (slot[j].busy)
 			(void)xdpgpu_wait(ctx, j);
 	const uint64_t t1 = now_ns();
+	if (th_up) {
+		/* the injector's counts are final before they are printed */
+		in.stop = 1;
+		pthread_join(th, NULL);
+		th_up = false;
+		if (!rc && in.rc)
+			rc = in.rc;
+	}
 	out->seconds = (double)(t1 - t0) / 1e9;
 	if (rc)
 		fprintf(stderr, "%s: live RX failed: %s %s\n", o->prog, strerror(-rc),
-			xdpgpu_last_error(ctx));
+			ctx ? xdpgpu_last_error(ctx) : "");
 	else if (!o->quiet)
 		print_stats(o, out, &st, label, t1);
 	if (!rc && verdicts) {
@@ -838,15 +941,19 @@ int rx_run_live(const struct rx_live *lv, const struct rx_opts *o, struct rx_tot
 	}
 	if (!rc && o->json) {
 		const double mpps = out->seconds > 0 ? out->rx_pkts / out->seconds / 1e6 : 0;
-		printf("{\"prog\": \"%s\", \"live\": \"%s:%u\", \"frames\": %llu, \"seconds\": %.6f, "
+		printf("{\"prog\": \"%s\", \"live\": \"%s:%u\", \"plumbing\": %s, "
+		       "\"mode\": \"%s\", \"frames\": %llu, \"seconds\": %.6f, "
 		       "\"mpps\": %.3f, \"rx_pkts\": %llu, \"rx_bytes\": %llu, \"tx_pkts\": %llu, "
-		       "\"injected\": %llu, \"batch\": %u, \"batches\": %llu, "
+		       "\"injected\": %llu, \"lost\": %llu, \"batch\": %u, \"batches\": %llu, "
 		       "\"verdict\": {\"ABORTED\": %llu, \"DROP\": %llu, \"PASS\": %llu, "
 		       "\"TX\": %llu, \"REDIRECT\": %llu}}\n",
-		       o->prog, lv->ifname, lv->queue, (unsigned long long)out->rx_pkts,
+		       o->prog, lv->ifname, lv->queue, o->plumbing ? "true" : "false",
+		       o->mode == RX_MODE_L2FWD ? "l2fwd" : o->mode == RX_MODE_ECHO ? "echo" : "rxdrop",
+		       (unsigned long long)out->rx_pkts,
 		       out->seconds, mpps, (unsigned long long)out->rx_pkts,
 		       (unsigned long long)out->rx_bytes, (unsigned long long)out->tx_pkts,
-		       (unsigned long long)in.sent, o->batch, (unsigned long long)out->batches,
+		       (unsigned long long)in.sent, (unsigned long long)in.lost, o->batch,
+		       (unsigned long long)out->batches,
 		       (unsigned long long)out->verdict[0], (unsigned long long)out->verdict[1],
 		       (unsigned long long)out->verdict[2], (unsigned long long)out->verdict[3],
 		       (unsigned long long)out->verdict[4]);
@@ -860,8 +967,13 @@ out:
 			rc = in.rc;
 	}
 	for (int j = 0; j < 2; j++) {
-		xdpgpu_host_free(slot[j].d);
-		xdpgpu_host_free(slot[j].v);
+		if (o->plumbing) {
+			free(slot[j].d);
+			free(slot[j].v);
+		} else {
+			xdpgpu_host_free(slot[j].d);
+			xdpgpu_host_free(slot[j].v);
+		}
 	}
 	free(fill);
 	free(txd);

@@ -84,6 +84,10 @@ struct rx_opts {
 	bool frags;              /* multi-buffer packets (XDPGPU_CFG_FRAGS):
 				  * batches end on a packet's last fragment,
 				  * packets and fragments counted apart    */
+	bool plumbing;           /* live mode without the GPU: the reference's
+				  * own bodies only (rx_drop recycles, l2fwd
+				  * swaps MACs and sends everything), config 1
+				  * as xdpsock runs it on a veth            */
 	const char *verdict_out; /* per-frame verdicts of the first pass      */
 	const char *tx_pcap;     /* frames sent on TX in the first pass       */
 	const char *prog;        /* program name for messages                 */

@@ -22,7 +22,9 @@
  * --seed S, --pcap FILE, --no-verify, --initval N, --json, --verdicts FILE,
  * --tx-pcap FILE, --dry-run; live mode: --veth PEER (make the veth pair
  * IF <-> PEER, as testenv.sh does), --inject N (send N frames of the pool
- * the pool options describe into PEER), --inject-pcap FILE.  Exit status:
+ * the pool options describe into PEER), --inject-pcap FILE, --plumbing
+ * (xdpsock's own rx_drop / l2fwd bodies with no GPU: config 1 as the
+ * reference runs it, for its xdpsock-format pps).  Exit status:
  * 0, 1 on a failure (live: also when the host refuses AF_XDP), 2 on a bad
  * option (xdpsock's usage() exits with EXIT_FAILURE).
  */
@@ -47,7 +49,7 @@
 enum {
 	OPT_GPU = 256, OPT_POOL, OPT_POOL_KIND, OPT_SEED, OPT_PCAP, OPT_NO_VERIFY,
 	OPT_INITVAL, OPT_JSON, OPT_VERDICTS, OPT_TX_PCAP, OPT_DRY_RUN, OPT_HELP,
-	OPT_VETH, OPT_INJECT, OPT_INJECT_PCAP,
+	OPT_VETH, OPT_INJECT, OPT_INJECT_PCAP, OPT_PLUMBING,
 };
 
 static struct option long_options[] = {
@@ -104,6 +106,7 @@ static struct option long_options[] = {
 	{ "veth", required_argument, 0, OPT_VETH },
 	{ "inject", required_argument, 0, OPT_INJECT },
 	{ "inject-pcap", required_argument, 0, OPT_INJECT_PCAP },
+	{ "plumbing", no_argument, 0, OPT_PLUMBING },
 	{ "help", no_argument, 0, OPT_HELP },
 	{ 0, 0, 0, 0 }
 };
@@ -155,7 +158,9 @@ static void usage(const char *prog)
 		"      --dry-run        Build the UMEM, describe it, no GPU\n"
 		"      --veth=peer      Live: make the veth pair IF <-> peer (removed at exit)\n"
 		"      --inject=n       Live: send n frames of the pool (pool options) into peer\n"
-		"      --inject-pcap=f  Live: send the frames of a pcap file into peer\n",
+		"      --inject-pcap=f  Live: send the frames of a pcap file into peer\n"
+		"      --plumbing       Live: xdpsock's own rx_drop / l2fwd bodies, no GPU\n"
+		"                       (config 1: the reference's CPU-only run on a veth)\n",
 		prog, DEFAULT_FRAME_SIZE, 64, MIN_PKT_SIZE, MAX_PKT_SIZE, MIN_PKT_SIZE,
 		DEFAULT_PATTERN);
 	exit(2);
@@ -328,6 +333,7 @@ int main(int argc, char **argv)
 		case OPT_VETH: veth = optarg; break;
 		case OPT_INJECT: inject_n = strtoull(optarg, NULL, 0); break;
 		case OPT_INJECT_PCAP: inject_pcap = optarg; break;
+		case OPT_PLUMBING: o.plumbing = true; break;
 		default:
 			usage(prog);
 		}
@@ -339,8 +345,9 @@ int main(int argc, char **argv)
 		fprintf(stderr, "%s: give -i IF (live AF_XDP), --pool N or --pcap FILE\n", prog);
 		usage(prog);
 	}
-	if (!live && (veth || inject_n || inject_pcap)) {
-		fprintf(stderr, "%s: --veth / --inject are live-mode options (-i IF)\n", prog);
+	if (!live && (veth || inject_n || inject_pcap || o.plumbing)) {
+		fprintf(stderr, "%s: --veth / --inject / --plumbing are live-mode options (-i IF)\n",
+			prog);
 		usage(prog);
 	}
 	if (pool_n && pcap) {

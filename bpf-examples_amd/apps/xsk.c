@@ -511,21 +511,21 @@ int xsk_link_delete(const char *name)
 
 /* ------------------------------------------------------------------ */
 
-int xsk_inject(const char *ifname, const uint8_t *umem, const struct xdp_desc *d,
-	       uint32_t n)
+int xsk_packet_socket(const char *ifname)
 {
 	const int ifindex = (int)if_nametoindex(ifname);
-	int fd, sent = 0;
+	int fd;
 
 	if (!ifindex)
 		return -ENODEV;
-	fd = socket(AF_PACKET, SOCK_RAW | SOCK_CLOEXEC, htons(ETH_P_ALL));
+	fd = socket(AF_PACKET, SOCK_RAW | SOCK_CLOEXEC, 0);
 	if (fd < 0)
 		return -errno;
+	/* protocol 0: a send-only socket (no copy of every frame the
+	 * interface receives is queued to it) */
 	struct sockaddr_ll ll;
 	memset(&ll, 0, sizeof(ll));
 	ll.sll_family = AF_PACKET;
-	ll.sll_protocol = htons(ETH_P_ALL);
 	ll.sll_ifindex = ifindex;
 	if (bind(fd, (struct sockaddr *)&ll, sizeof(ll))) {
 		const int e = -errno;
@@ -533,24 +533,49 @@ int xsk_inject(const char *ifname, const uint8_t *umem, const struct xdp_desc *d
 		close(fd);
 		return e;
 	}
-	for (uint32_t i = 0; i < n; i++) {
-		const uint64_t eff = (d[i].addr & ((1ull << XSK_UNALIGNED_BUF_OFFSET_SHIFT) - 1)) +
-				     (d[i].addr >> XSK_UNALIGNED_BUF_OFFSET_SHIFT);
+	return fd;
+}
 
-		for (;;) {
-			if (send(fd, umem + eff, d[i].len, 0) >= 0) {
-				sent++;
-				break;
-			}
-			if (errno != ENOBUFS && errno != EAGAIN) {
-				const int e = -errno;
+int xsk_inject_fd(int fd, const uint8_t *umem, const struct xdp_desc *d, uint32_t n)
+{
+	enum { kBatch = 64 };
+	struct mmsghdr mm[kBatch];
+	struct iovec iov[kBatch];
+	uint32_t sent = 0;
 
-				close(fd);
-				return sent ? sent : e;
-			}
-			usleep(50);
+	while (sent < n) {
+		const uint32_t m = n - sent < kBatch ? n - sent : kBatch;
+		for (uint32_t i = 0; i < m; i++) {
+			const struct xdp_desc *x = &d[sent + i];
+			const uint64_t eff = (x->addr & ((1ull << XSK_UNALIGNED_BUF_OFFSET_SHIFT) - 1)) +
+					     (x->addr >> XSK_UNALIGNED_BUF_OFFSET_SHIFT);
+
+			iov[i].iov_base = (void *)(umem + eff);
+			iov[i].iov_len = x->len;
+			memset(&mm[i], 0, sizeof(mm[i]));
+			mm[i].msg_hdr.msg_iov = &iov[i];
+			mm[i].msg_hdr.msg_iovlen = 1;
 		}
+		const int r = sendmmsg(fd, mm, m, 0);
+		if (r > 0) {
+			sent += (uint32_t)r;
+			continue;
+		}
+		if (r < 0 && errno != ENOBUFS && errno != EAGAIN)
+			return sent ? (int)sent : -errno;
+		usleep(50);
 	}
+	return (int)sent;
+}
+
+int xsk_inject(const char *ifname, const uint8_t *umem, const struct xdp_desc *d,
+	       uint32_t n)
+{
+	const int fd = xsk_packet_socket(ifname);
+
+	if (fd < 0)
+		return fd;
+	const int r = xsk_inject_fd(fd, umem, d, n);
 	close(fd);
-	return sent;
+	return r;
 }

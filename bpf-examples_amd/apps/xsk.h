@@ -88,5 +88,9 @@ int xsk_link_up(const char *name);
  * sent or -errno. */
 int xsk_inject(const char *ifname, const uint8_t *umem,
 	       const struct xdp_desc *d, uint32_t n);
+/* The same over a send-only AF_PACKET socket kept open (sendmmsg, 64
+ * frames a call): xsk_packet_socket returns its fd or -errno. */
+int xsk_packet_socket(const char *ifname);
+int xsk_inject_fd(int fd, const uint8_t *umem, const struct xdp_desc *d, uint32_t n);
 
 #endif /* XSK_H */

@@ -1019,18 +1019,17 @@ int xdpgpu_nat64_dev(xdpgpu_ctx *ctx, void *d_umem, uint64_t umem_size,
 		memcpy(a.pref_w, ctx->ncfg.v6_prefix, 12);
 	}
 	hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
-	if (dyn)
-		HIP_TRY(ctx, hipMemsetAsync(ctx->d_mcnt, 0, 16, st));
-	if (!a.fast) {
-		HIP_TRY(ctx, launch_nat64(a, ctx->max_blocks, st));
-		return dyn ? nat64_commit(ctx, a, now, st) : 0;
-	}
+	/* the shared-tile heads and the dynamic-state miss list are the
+	 * context's: ordered after their last user on another stream */
 	int rc = scratch_enter(ctx, ctx->slot[0], st);
 	if (rc)
 		return rc;
+	if (dyn)
+		HIP_TRY(ctx, hipMemsetAsync(ctx->d_mcnt, 0, 16, st));
 	HIP_TRY(ctx, launch_nat64(a, ctx->max_blocks, st));
 	/* the fast kernel zeroed the other counter set (as the RX launch) */
-	ctx->slot[0].steal_set ^= 1;
+	if (a.fast)
+		ctx->slot[0].steal_set ^= 1;
 	rc = scratch_leave(ctx, ctx->slot[0], st);
 	if (rc)
 		return rc;
@@ -1055,9 +1054,15 @@ int xdpgpu_synproxy_dev(xdpgpu_ctx *ctx, void *d_umem, uint64_t umem_size,
 			return set_err(ctx, -ENOMEM, "synproxy counters");
 		HIP_TRY(ctx, hipMemset(ctx->d_spread, 0, bytes));
 	}
+	/* the counters are the context's: a launch on another stream waits
+	 * for the last launch that used them (its sum kernel reads and
+	 * clears them), as the context's launches are ordered (xdpgpu.h) */
+	int rc = scratch_enter(ctx, ctx->slot[0], st);
+	if (rc)
+		return rc;
 	HIP_TRY(ctx, launch_synproxy((uint8_t *)d_umem, umem_size, d_descs, n, *cfg, d_verdict,
 				     d_out, (unsigned long long *)d_synacks, ctx->d_spread, st));
-	return 0;
+	return scratch_leave(ctx, ctx->slot[0], st);
 }
 
 int xdpgpu_ceiling_dev(xdpgpu_ctx *ctx, const void *d_umem, uint64_t umem_size,

@@ -32,6 +32,19 @@ def _gpu_drain(request):
     probe.add_(1)
     assert int(probe.sum().item()) == 4096
     torch.cuda.synchronize()
+    # a bounds-checked build (-DXDPGPU_DBG, tools/dbg_build.sh, selected with
+    # XDPGPU_LIB): every access the RX kernels clamped is a failure of the
+    # test that launched them (code -> [count, last value])
+    xg = sys.modules.get("xdpgpu")
+    lib = getattr(xg, "_lib", None) if xg else None
+    if lib is not None and hasattr(lib, "xdpgpu_debug_read"):
+        import ctypes
+        import numpy as np
+        dbg = np.zeros(64, np.uint64)
+        assert lib.xdpgpu_debug_read(ctypes.c_void_p(dbg.ctypes.data)) == 0
+        rec = {k: (int(dbg[2 * k]), hex(int(dbg[2 * k + 1])))
+               for k in range(32) if dbg[2 * k]}
+        assert not rec, f"bounds checks of the debug build fired: {rec}"
 
 
 @pytest.fixture(scope="session")

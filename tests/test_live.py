@@ -42,6 +42,39 @@ def test_xsk_plumbing_live():
     assert '"ok": true' in r.stdout
 
 
+def _xdpsock_gpu():
+    exe = os.path.join(APPS, "xdpsock-gpu")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", APPS, "xdpsock-gpu"], check=True)
+    return exe
+
+
+@pytest.mark.parametrize("mode", ["-l", "-r"], ids=["l2fwd", "rxdrop"])
+def test_xdpsock_plumbing_config1(mode):
+    """Config 1: xdpsock's own l2fwd / rx_drop bodies (xdpsock.c:1718-1784,
+    1462-1506) over the build's rings on a veth pair, no GPU (--plumbing):
+    every injected frame received, l2fwd sends every one back with its MACs
+    swapped, and the xdpsock-format statistics table is printed."""
+    n = 20000
+    r = subprocess.run([_xdpsock_gpu(), "-i", "xgp1a", "--veth", "xgp1b", "--inject", str(n),
+                        mode, "--plumbing", "--json"], capture_output=True, text=True,
+                       timeout=120)
+    if r.returncode == 1 and ("AF_XDP on" in r.stderr or "veth" in r.stderr):
+        pytest.skip(f"host refuses live AF_XDP: {r.stderr.strip()}")
+    assert r.returncode == 0, r.stdout + r.stderr
+    import json
+    js = json.loads(r.stdout.strip().splitlines()[-1])
+    assert js["plumbing"] is True and js["mode"] == ("l2fwd" if mode == "-l" else "rxdrop")
+    assert js["injected"] == n
+    # the kernel may add its own frames (IPv6 neighbour discovery on link
+    # up) and drop some under load; almost every injected frame arrives
+    assert js["rx_pkts"] >= 0.98 * n
+    assert js["tx_pkts"] == (js["rx_pkts"] if mode == "-l" else 0)
+    assert sum(js["verdict"].values()) == 0          # no verdict compute
+    # dump_stats' table (xdpsock.c:478-582)
+    assert " sock0@xgp1a:0 " in r.stdout and "\nrx " in r.stdout and "\ntx " in r.stdout
+
+
 def test_live_fixture_is_the_pool_frames():
     """The captured frames are the generator's frames, in the order sent."""
     fx = np.load(FIXTURE)

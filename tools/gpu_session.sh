@@ -1,0 +1,120 @@
+#!/bin/bash
+# One gpurun session, steps named on the command line (in order):
+#
+#   bash tools/gpu_session.sh smoke pytest bench prof:config2 pmc ...
+#
+# Every step that touches the GPU runs under its own time limit.  Anything
+# but exit 0 or a plain test/Python failure (1) ends the session at once
+# (a fault, an abort, a time limit: nothing more runs on the GPU).  Each
+# session writes into its own directory gpurun_out/<RUN>/ (RUN defaults to
+# the UTC time), so a failing log is never overwritten by the next run.
+#
+# Steps:
+#   smoke                  __graft_entry__.smoke()
+#   pytest                 the whole -m gpu suite
+#   pytest:FILE[,FILE..]   those test files only (-m gpu)
+#   dbgtests:LIB:FILES     FILES (-m gpu) against a bounds-checked build
+#                          (tests/conftest.py fails a test whose kernels
+#                          clamped an access)
+#   bench                  python bench.py (every leg)
+#   bench:ARGS             python bench.py ARGS (words split on '+')
+#   prof:NAME              rocprofv3 --kernel-trace --stats of a workload
+#                          (config2 1500 imix imix30 nat64 nat64_egress
+#                          nat64_dynamic frags synproxy echo)
+#   pmc:NAME               PMC passes (tools/pmc_profile.sh) on a workload
+#                          (config2 imix imix30 nat64 nat64_egress 1500)
+#   ab:LIB                 A/B: the in-tree library vs LIB, alternating
+#                          processes (IMIX, 1500 B, config 2)
+#   stamps                 per-wave timeline (build/stamps, tools/stamps.py)
+#   probe                  tools/order_probe (LDS-DMA / vmcnt ordering)
+#   e2e                    PCIe-inclusive host path (bench.py --e2e)
+#   cli                    xdpsock-gpu over a 16 M-frame pool
+set -u
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+RUN=${RUN:-$(date -u +%Y%m%dT%H%M%S)}
+OUT=gpurun_out/$RUN
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+echo "== session $RUN: $*"
+
+step() {  # name timeout cmd...
+	local name=$1 t=$2; shift 2
+	echo "== $name: $*"
+	timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+	local rc=$?
+	echo "== $name rc=$rc"
+	tail -n 6 "$OUT/$name.log" | cut -c1-400
+	if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+		echo "== stopping after $name (rc=$rc)"
+		exit $rc
+	fi
+	return 0
+}
+
+# workload command lines shared by prof: and pmc:
+workload() {
+	case $1 in
+	config2) echo "python3 tools/tune_rx.py --variants 64:0 --rounds 3" ;;
+	1500) echo "python3 tools/tune_rx.py --variants 64:0 --rounds 3 --frames 2097152 --size 1500" ;;
+	imix) echo "python3 tools/tune_rx.py --variants 64:0 --rounds 3 --frames 16777216 --kind 1 --seed 0x5EED0003 --fmt 2" ;;
+	imix30) echo "python3 tools/tune_rx.py --variants 64:0 --rounds 3 --frames 16777216 --kind 4 --seed 0x5EED0003 --fmt 2" ;;
+	nat64) echo "python3 tools/nat64_probe.py --reps 5" ;;
+	nat64_egress) echo "python3 tools/nat64_probe.py --reps 5 --direction 1" ;;
+	nat64_dynamic) echo "python3 tools/nat_dyn_probe.py --frames 16777216 --reps 5" ;;
+	frags) echo "python3 tools/frags_probe.py --reps 5" ;;
+	synproxy) echo "python3 bench.py --no-cpu --legs synproxy --steps 5 --warmup 2" ;;
+	echo) echo "python3 bench.py --no-cpu --legs echo --steps 5 --warmup 2" ;;
+	bench) echo "python3 bench.py --no-cpu --no-secondary --steps 20" ;;
+	*) echo "unknown workload $1" >&2; exit 2 ;;
+	esac
+}
+
+for s in "$@"; do
+	name=${s%%:*}
+	arg=${s#*:}
+	[ "$arg" = "$s" ] && arg=
+	case $name in
+	smoke) step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
+	pytest)
+		files=tests
+		[ -n "$arg" ] && files=${arg//,/ }
+		# shellcheck disable=SC2086
+		step "pytest${arg:+_$(echo "$arg" | tr ',/' '__')}" 1100 python3 -u -m pytest $files \
+			-m gpu -v --timeout 200 --timeout-method thread ;;
+	dbgtests)
+		lib=${arg%%:*}
+		files=${arg#*:}
+		# shellcheck disable=SC2086
+		step "dbgtests_$(basename "$(dirname "$lib")")" 1100 env XDPGPU_LIB="$lib" \
+			python3 -u -m pytest ${files//,/ } -m gpu -v --timeout 200 --timeout-method thread ;;
+	bench)
+		# shellcheck disable=SC2086
+		step "bench${arg:+_$(echo "$arg" | tr '+-' '__')}" 600 python3 bench.py ${arg//+/ } ;;
+	prof)
+		# shellcheck disable=SC2046
+		step "prof_$arg" 400 rocprofv3 --kernel-trace --stats --output-format csv \
+			-d "$OUT/prof_$arg" -o run -- $(workload "$arg") ;;
+	pmc)
+		step "pmc_$arg" 900 env DEST="$OUT/pmc_$arg.json" OUT="$OUT/pmc_$arg" \
+			PMC_CMD="$(workload "$arg")" LABEL="$arg" bash tools/pmc_profile.sh ;;
+	ab)
+		for r in 1 2; do
+			for lib in bpf-examples_amd/csrc/libxdpgpu.so "$arg"; do
+				tag=$(basename "$(dirname "$lib")")_$r
+				# shellcheck disable=SC2046
+				step "ab_imix_$tag" 150 env XDPGPU_LIB="$lib" $(workload imix)
+				# shellcheck disable=SC2046
+				step "ab_1500_$tag" 150 env XDPGPU_LIB="$lib" $(workload 1500)
+				# shellcheck disable=SC2046
+				step "ab_config2_$tag" 150 env XDPGPU_LIB="$lib" $(workload config2)
+			done
+		done ;;
+	stamps) step stamps 200 env XDPGPU_LIB=build/stamps/libxdpgpu.so python3 -u tools/stamps.py ;;
+	probe) step probe 120 tools/order_probe 64 ;;
+	e2e) step e2e 600 python3 bench.py --no-cpu --no-secondary --steps 10 --e2e ;;
+	cli) step cli 300 bpf-examples_amd/apps/xdpsock-gpu --pool 16777216 --pool-kind udp4 \
+		-b 1048576 -C 67108864 --json -Q ;;
+	*) echo "unknown step $s"; exit 2 ;;
+	esac
+done
+echo "== session $RUN done"
