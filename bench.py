@@ -153,8 +153,30 @@ def cpu_baseline(umem, descs, flags, fmt, budget_s: float = 10.0):
            "reference_headers_mpps": round((1 << 20) / ref / 1e6, 1) if ref else None}
     if ref:
         cal["leg_over_reference"] = round(ref / mine, 3)
+    # the same work with the reference headers' own routines (checksums
+    # verified and recomputed as two passes each, as the reference idiom
+    # does; oracle/ref_harness.c ref_leg_bench), on the same threads
+    refleg = None
+    r1 = oracle.ref_leg_bench(umem, one, 1, 1, True, flags, 0, fmt)
+    if r1 is not None:
+        rr1 = max(1, int(3.0 / max(r1[0], 1e-3)))
+        r1 = oracle.ref_leg_bench(umem, one, 1, rr1, True, flags, 0, fmt)
+        rdt, _ = oracle.ref_leg_bench(umem, sample, cores, 2, True, flags, 0, fmt)
+        rreps = max(1, int(budget_s / max(rdt, 1e-3)))
+        rdt, (rv, rres, rtup) = oracle.ref_leg_bench(umem, sample, cores, rreps, True, flags,
+                                                     0, fmt)
+        rmpps = len(sample) * rreps / rdt / 1e6
+        refleg = {"reference_mpps": round(rmpps, 2),
+                  "reference_single_thread_mpps": round(len(one) * rr1 / r1[0] / 1e6, 2),
+                  "reference_outputs_match_leg": bool(
+                      np.array_equal(rv, v) and rres.tobytes() == res.tobytes()),
+                  "leg_over_reference": round(mpps / rmpps, 3),
+                  "reference_sample": f"{len(sample)} frames x {rreps} passes on {cores} "
+                                      f"threads ({rdt:.1f} s): lib_checksum.h ip_fast_csum / "
+                                      "udp_csum and jhash.h jhash compiled from the reference "
+                                      "(oracle/_ref), parse restated"}
     legs = cpu_legs(oracle)
-    return {"value": round(mpps, 2), "unit": "Mpps", "cores": cores,
+    out = {"value": round(mpps, 2), "unit": "Mpps", "cores": cores,
             "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
             "kind": "port", "cpu_model": cpu_model(),
             "gbps": round(mpps * 1e6 * BYTES_PER_FRAME / 1e9, 2),
@@ -164,6 +186,9 @@ def cpu_baseline(umem, descs, flags, fmt, budget_s: float = 10.0):
             "sample": f"{len(sample)} config-2 frames x {reps} passes of oracle/cpu_leg.c "
                       f"(gcc -O2) on {cores} threads pinned one per CPU ({dt:.1f} s); "
                       f"1 pinned thread: {len(one)} frames x {reps1} passes"}
+    if refleg:
+        out.update(refleg)
+    return out
 
 
 def cpu_legs(oracle) -> dict:

@@ -143,6 +143,9 @@ def ref_lib() -> Optional[C.CDLL]:
         r.ref_jhash_1word.restype = u32
         r.ref_probe.argtypes = [vp, C.c_uint64, vp, u32, u32, C.POINTER(C.c_uint64)]
         r.ref_probe.restype = C.c_double
+        r.ref_leg_bench.argtypes = [vp, C.c_uint64, vp, u32, u32, u32, u32, vp, vp, vp, u32,
+                                    u32, C.c_int]
+        r.ref_leg_bench.restype = C.c_double
         _r = r
     return _r
 
@@ -344,6 +347,27 @@ def leg_bench(umem: np.ndarray, descs: np.ndarray, threads: int, reps: int, pin:
     tup = np.zeros(max(1, n * tb), np.uint8)
     dt = o.cpu_leg_bench(umem.ctypes.data, umem.nbytes, descs.ctypes.data, n, flags,
                          initval, tuple_fmt, verdict.ctypes.data, res.ctypes.data,
+                         tup.ctypes.data if tb else None, threads, reps, 1 if pin else 0)
+    return dt, (verdict, res, tup)
+
+
+def ref_leg_bench(umem: np.ndarray, descs: np.ndarray, threads: int, reps: int, pin: bool,
+                  flags: int = 0x5, initval: int = 0, tuple_fmt: int = 1):
+    """As leg_bench, with the reference headers' own checksum and hash
+    routines (oracle/ref_harness.c ref_leg_bench); None off this container
+    or when oracle/_ref was not built.  umem is written (check words zeroed
+    and restored), so pass a copy when it is shared."""
+    r = ref_lib()
+    if r is None:
+        return None
+    descs = np.ascontiguousarray(descs, DESC_DTYPE)
+    n = len(descs)
+    verdict = np.zeros(n, np.uint8)
+    res = np.zeros(n, RESULT_DTYPE)
+    tb = TUPLE_BYTES[tuple_fmt]
+    tup = np.zeros(max(1, n * tb), np.uint8)
+    dt = r.ref_leg_bench(umem.ctypes.data, umem.nbytes, descs.ctypes.data, n, flags, initval,
+                         tuple_fmt, verdict.ctypes.data, res.ctypes.data,
                          tup.ctypes.data if tb else None, threads, reps, 1 if pin else 0)
     return dt, (verdict, res, tup)
 

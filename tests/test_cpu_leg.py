@@ -72,3 +72,27 @@ def test_leg_bench_and_probe_run():
     assert mine > 0
     if os.path.isdir("/root/reference"):
         assert ref is not None and ref > 0
+
+
+@pytest.mark.parametrize("flags,iv,fmt", [c for c in CFGS if c[2]])
+@pytest.mark.parametrize("kind,size,n", [(xdpgpu.POOL_UDP4, 64, 1 << 16),
+                                         (xdpgpu.POOL_UDP4, 1500, 1 << 13),
+                                         (xdpgpu.POOL_IMIX, 64, 1 << 15)],
+                         ids=["udp64", "udp1500", "imix"])
+def test_reference_routine_leg_vs_oracle(kind, size, n, flags, iv, fmt):
+    """The reference-routine leg (lib_checksum.h / jhash.h's own functions,
+    oracle/ref_harness.c ref_leg_bench) gives the oracle's verdicts, records
+    and tuples on every frame, and leaves the UMEM as it found it (the check
+    words it zeroes are restored)."""
+    if not os.path.isdir("/root/reference"):
+        pytest.skip("reference tree absent (oracle/_ref is built from it)")
+    umem, descs, _ = xdpgpu.pool_generate(n, kind, size, 0x5EED0034)
+    u = umem.copy()
+    r = oracle.ref_leg_bench(u, descs, 3, 2, False, flags, iv, fmt)
+    assert r is not None
+    dt, (v, res, tup) = r
+    ov, ores, otup, _ = oracle.process(umem.copy(), descs, flags, iv, fmt)
+    np.testing.assert_array_equal(v, ov)
+    assert res.tobytes() == ores.tobytes()
+    assert tup[: len(otup)].tobytes() == otup.tobytes()
+    assert np.array_equal(u, umem)

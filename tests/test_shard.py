@@ -69,3 +69,54 @@ def test_two_rank_gloo_reduction(tmp_path):
     assert [got["verdict"][v] for v in shard.VERDICT_NAMES] == want["verdict"]
     secs, frames, ok = np.load(tmp_path / "timing.npy")
     assert secs == 1.5 and frames == N_TOTAL and ok == 1.0
+
+
+def _torchrun(script_args, env_extra=None, timeout=240):
+    import subprocess
+    import sys
+    env = dict(os.environ)
+    env.update(env_extra or {})
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}"] + script_args
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env,
+                          cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+@pytest.mark.gpu
+def test_two_rank_device_shards(tmp_path):
+    """The N > 1 path on the device: two ranks (one process each, as
+    bench.py runs under torch.distributed.run), each with its own context on
+    cuda:0 and its config-5 shard, every frame compared with the oracle on
+    each rank; counters and timing reduced over gloo as bench.py reduces
+    them over RCCL, and the reduced device counters equal the reduced
+    oracle counters (tests/shard_worker.py)."""
+    import json
+    out = tmp_path / "shards.json"
+    r = _torchrun([os.path.join("tests", "shard_worker.py"), str(out)])
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    js = json.loads(out.read_text())
+    assert js["world"] == 2 and js["all_ok"] is True
+    assert js["frames"] == 2 * (1 << 18) and js["seconds_max"] > 0
+    assert js["device_stats"] == js["oracle_stats"]
+    assert js["device_stats"]["frames"] == 2 * (1 << 18)
+
+
+@pytest.mark.gpu
+def test_bench_two_rank_rehearsal():
+    """bench.py's own N-rank path (torchrun launch, set_device before the
+    process group, per-rank shards with offset seeds, barrier-bracketed
+    timing, max-over-ranks reduction, one rank-0 line), two ranks sharing
+    cuda:0 (XDPGPU_BENCH_REHEARSE=1: gloo for the three control scalars):
+    the rank-0 line reports both ranks' frames and correct verdicts."""
+    import json
+    r = _torchrun(["bench.py", "--gpus", "2", "--frames", str(1 << 20), "--steps", "3",
+                   "--warmup", "1", "--no-cpu", "--no-secondary"],
+                  {"XDPGPU_BENCH_REHEARSE": "1"})
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    js = json.loads(lines[0])
+    assert js["n_gpus"] == 2 and js["verdicts_ok"] is True and js["value"] > 0
+    assert js["scaling"] == "weak" and js["config"]["parallelism"] == "shard2"
+    assert js["config"]["frames_per_gpu"] == 1 << 20
