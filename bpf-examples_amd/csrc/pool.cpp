@@ -300,7 +300,11 @@ uint32_t gen_random_frame(const xdpgpu_pool_spec *sp, uint64_t idx, uint8_t *p,
 		size = c < 7 ? 64 : c < 11 ? 570 : 1500;
 		uint32_t tv = r.below(100);
 		tags = tv < 20 ? 1 : tv < 22 ? 2 : 0;
-		v6 = size > 64 && r.below(100) < 30;
+		/* 30 % of the pool IPv6, all of it in the
+		 * 570/1500 B classes (5/12 of the frames): 72 % of those */
+		const uint64_t v6ppm = sp->ppm_v6 ? sp->ppm_v6 : 300000;
+		const uint64_t big = v6ppm * 12 / 5;
+		v6 = size > 64 && r.below(1000000) < (big < 1000000 ? big : 1000000);
 		uint32_t pv = r.below(100);
 		l4p = pv < 80 ? 17 : pv < 95 ? 6 : (v6 ? 58 : 1);
 		if (v6 && r.below(100) < 5)
@@ -668,8 +672,10 @@ void xdpgpu_pool_spec_default(xdpgpu_pool_spec *spec, uint32_t kind,
 		spec->ppm_ndp = 1000;
 		spec->ppm_echo6 = 0;
 	}
-	if (kind == XDPGPU_POOL_IMIX)
+	if (kind == XDPGPU_POOL_IMIX) {
 		spec->frame_size = 64; /* size of special (ARP/NDP) frames */
+		spec->ppm_v6 = 300000; /* 70 % IPv4 / 30 % IPv6 */
+	}
 	if (kind == XDPGPU_POOL_NAT64 || kind == XDPGPU_POOL_NAT64_V4) {
 		/* config 4: 128 B frames, 10 % ICMPv6 echo; 0.5 % of each
 		 * corruption class */

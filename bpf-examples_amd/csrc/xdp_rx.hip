@@ -1071,6 +1071,17 @@ __device__ __forceinline__ uint4 ld_nt16(const void *p)
  * result record).  GEN true: exception-kernel entries (xdpgpu ylist: index,
  * partial sum | check word, range start | check offset, range end | flags;
  * any alignment).  meta: 64 uint4, part4: 256 uint4 of this wave's LDS. */
+/* the little-endian 16-bit word at byte offset o (0..14) of a 16-byte
+ * chunk */
+__device__ __forceinline__ uint32_t u16_at(uint4 x, uint32_t o)
+{
+	const uint32_t k = (o >> 2) & 3;
+	const uint32_t w = k == 0 ? x.x : k == 1 ? x.y : k == 2 ? x.z : x.w;
+	const uint32_t w2 = k == 0 ? x.y : k == 1 ? x.z : k == 2 ? x.w : 0u;
+	const uint64_t d = ((uint64_t)w2 << 32) | w;
+	return (uint32_t)(d >> (8 * (o & 3))) & 0xffff;
+}
+
 /* the completed record of a bulk frame: a scattered 16-byte store */
 #ifndef XDP_TAIL_REC_NT
 #define XDP_TAIL_REC_NT 1
@@ -1127,6 +1138,15 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 		h2 = *reinterpret_cast<const uint4 *>(a.umem + eff + 32);
 		h3 = *reinterpret_cast<const uint4 *>(a.umem + eff + 48);
 	}
+	/* a "late" IPv6 frame (fast_tile): its check word (and TCP's data
+	 * offset) lie in frame bytes [64, 80), which the UMEM holds (both
+	 * before l4 + 20 <= len) */
+	const uint32_t p6 = (rv.z >> 8) & 0xff;
+	const uint32_t chk6 = p6 == 6 ? 16u : p6 == 17 ? 6u : 2u;
+	const bool late = r6 && l4 + chk6 >= 64;
+	uint4 x64 = make_uint4(0, 0, 0, 0);
+	if (act && late)
+		x64 = *reinterpret_cast<const uint4 *>(a.umem + eff + 64);
 	/* absolute range [lo, lim), streamed from its 16-byte aligned start */
 	const uint64_t lo = eff + (GEN ? (ye.z & 0xffff) : 64u);
 	const uint64_t lo_al = lo & ~15ull;
@@ -1219,13 +1239,42 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 			 !(rv.z & XDPGPU_F_L3_OK);
 	} else {
 		c4 = rv.w & 0xffff;
+		if (late) {
+			/* the check word is among the summed halves (an even
+			 * frame offset in a range from byte 64): taken out
+			 * exactly */
+			c4 = u16_at(x64, l4 + chk6 - 64);
+			t -= c4;
+		}
 		sum4 = fold16((uint64_t)(rv.y >> 16) + t);
 		absent = !r6 && ((rv.z >> 8) & 0xff) == 17 && c4 == 0;
 		l3_bad = !(rv.z & XDPGPU_F_L3_OK);
 	}
+	/* IPv6/TCP: parse_tcphdr's data offset checks (parsing_helpers.h:
+	 * 295-318, and the range at least the header), ABORTED otherwise */
+	bool abort6 = false;
+	if constexpr (!GEN) {
+		const uint32_t thl = ((u16_at(x64, l4 + 12 - 64) & 0xff) >> 4) * 4;
+		abort6 = late && p6 == 6 && ((thl < 20) | (l4 + thl > dv.z) | (cl < thl));
+	}
 	const bool l4_ok = absent || (~fold16((uint64_t)sum4 + c4) & 0xffff) == 0;
 	const bool drop = (a.flags & XDPGPU_CFG_VERIFY_CSUM) && (l3_bad || !l4_ok);
-	if (act) {
+	if (act && abort6) {
+		/* ABORTED frames carry all-zero records and tuples */
+		const uint4 z = make_uint4(0, 0, 0, 0);
+		if constexpr (kTailRecNt)
+			st_nt16(a.res + i, z);
+		else
+			*reinterpret_cast<uint4 *>(a.res + i) = z;
+		if (tup6) {
+			uint32_t *tz = reinterpret_cast<uint32_t *>(a.tup + 44 * i);
+#pragma unroll
+			for (int k = 0; k < 11; k++)
+				tz[k] = 0u;
+		}
+		a.verdict[i] = (uint8_t)XDPGPU_ABORTED;
+		my_bytes += dv.z;
+	} else if (act) {
 		rv.y = (rv.y & 0xffff) | ((~sum4 & 0xffff) << 16);
 		rv.z |= (l4_ok ? XDPGPU_F_L4_OK : 0u) |
 			(absent ? XDPGPU_F_L4_ABSENT : 0u);
@@ -1236,19 +1285,27 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 			*reinterpret_cast<uint4 *>(a.res + i) = rv;
 		if (tup6) {
 			/* the addresses and ports, from the words loaded with
-			 * the batch */
-			const uint32_t w[12] = {h1.x, h1.y, h1.z, h1.w, h2.x, h2.y,
-						h2.z, h2.w, h3.x, h3.y, h3.z, h3.w};   /* dwords 4..15 */
+			 * the batch, shifted by the tags (nv dwords; the fast
+			 * shape keeps them inside bytes [16, 64)) */
+			const uint32_t w0[12] = {h1.x, h1.y, h1.z, h1.w, h2.x, h2.y,
+						 h2.z, h2.w, h3.x, h3.y, h3.z, h3.w};   /* dwords 4..15 */
+			const uint32_t nv = rv.z >> 24;
+			uint32_t w[12];
+#pragma unroll
+			for (int k = 0; k < 12; k++)
+				w[k] = nv == 0 ? w0[k]
+				     : nv == 1 ? (k + 1 < 12 ? w0[k + 1] : 0u)
+					       : (k + 2 < 12 ? w0[k + 2] : 0u);
 			uint32_t *t = reinterpret_cast<uint32_t *>(a.tup + 44 * i);
 #pragma unroll
 			for (int k = 0; k < 4; k++) {
 				t[k] = (w[1 + k] >> 16) | (w[2 + k] << 16);
 				t[5 + k] = (w[5 + k] >> 16) | (w[6 + k] << 16);
 			}
-			/* ports for UDP; ICMPv6 has none */
-			const uint32_t p6 = (rv.z >> 8) & 0xff;
-			t[4] = p6 == 17 ? w[9] >> 16 : 0u;
-			t[9] = p6 == 17 ? w[10] & 0xffffu : 0u;
+			/* ports for UDP and TCP; ICMPv6 has none */
+			const bool ports = p6 == 17 || p6 == 6;
+			t[4] = ports ? w[9] >> 16 : 0u;
+			t[9] = ports ? w[10] & 0xffffu : 0u;
 			t[10] = p6 | (10u << 16);
 		}
 		if constexpr (kTailVerdictNt)
@@ -1259,12 +1316,14 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 		my_bytes += dv.z;
 	}
 	if (a.stats) {
+		const bool fin = act && !abort6;
 		cnt[CNT_FRAMES] += __popcll(__ballot(act));
-		cnt[CNT_VERDICT0 + XDPGPU_DROP] += __popcll(__ballot(act && drop));
-		cnt[CNT_VERDICT0 + XDPGPU_REDIRECT] += __popcll(__ballot(act && !drop));
-		cnt[CNT_L3_BAD] += __popcll(__ballot(act && l3_bad));
-		cnt[CNT_L4_BAD] += __popcll(__ballot(act && !l4_ok));
-		cnt[CNT_L4_ABSENT] += __popcll(__ballot(act && absent));
+		cnt[CNT_VERDICT0 + XDPGPU_ABORTED] += __popcll(__ballot(act && abort6));
+		cnt[CNT_VERDICT0 + XDPGPU_DROP] += __popcll(__ballot(fin && drop));
+		cnt[CNT_VERDICT0 + XDPGPU_REDIRECT] += __popcll(__ballot(fin && !drop));
+		cnt[CNT_L3_BAD] += __popcll(__ballot(fin && l3_bad));
+		cnt[CNT_L4_BAD] += __popcll(__ballot(fin && !l4_ok));
+		cnt[CNT_L4_ABSENT] += __popcll(__ballot(fin && absent));
 		if constexpr (GEN)
 			cnt[CNT_FRAG] += __popcll(__ballot(act && (rv.z & XDPGPU_F_FRAG)));
 	}
@@ -1585,26 +1644,41 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 	fast = shape & (l4 + cl + over <= 64u);
 	bool bulk = shape & !fast & (a.res != nullptr);
 
-	/* V6: untagged IPv6 + UDP with no extension header, the generic
-	 * parse's conditions (parse_ip6hdr, parse_udphdr): the UDP header at
-	 * 54-61 is in the window, the pseudo header's addresses at 22-53;
-	 * csum_ipv6_magic, an odd length zero padded, a stored 0 not absent */
-	bool v6 = false, i6 = false;
-	uint32_t ulen6 = 0;
+	/* V6: IPv6 with no extension header behind 0..2 VLAN tags, in the
+	 * shifted words r (r[j] = frame dword j + nv, zero past the window),
+	 * with the generic parse's conditions (parse_ip6hdr, parse_udphdr,
+	 * parse_tcphdr, parse_icmp6hdr):
+	 *  - UDP behind at most one tag (its length at l4 + 4 in the window),
+	 *    the range its length;
+	 *  - TCP behind at most one tag (both ports in the window), the range
+	 *    the payload length; its data offset lies past the window, so the
+	 *    bulk pass checks it (ABORTED when parse_tcphdr would fail);
+	 *  - ICMPv6 (its type in the window) other than NDP (PASS,
+	 *    af_xdp_kern.c:114-148) and, with the echo responder, echo
+	 *    requests (the exception path's TX rewrite), the range the payload
+	 *    length.
+	 * csum_ipv6_magic, an odd length zero padded, a stored 0 not absent.
+	 * A check word at or past byte 64 (TCP; UDP behind a tag; ICMPv6
+	 * behind two) is "late": the bulk pass reads it, and the data offset,
+	 * from frame bytes [64, 80). */
+	bool v6 = false, i6 = false, t6 = false;
+	uint32_t ulen6 = 0, nh6 = 0;
 	if constexpr (V6) {
-		const uint32_t plen = bswap16(F[4] >> 16);
-		const uint32_t nh6 = F[5] & 0xff;
-		/* ICMPv6 too (its range the payload length), but neither NDP
-		 * (PASS, af_xdp_kern.c:114-148) nor an echo request the echo
-		 * responder answers (the exception path's TX rewrite) */
-		const uint32_t ity = (F[13] >> 16) & 0xff;
+		const uint32_t plen = bswap16(r[4] >> 16);
+		nh6 = r[5] & 0xff;
+		const uint32_t ity = (r[13] >> 16) & 0xff;
+		const bool u6 = nh6 == 17;
+		t6 = nh6 == 6;
 		i6 = (nh6 == 58) & (plen >= 8) & !((ity >= 133) & (ity <= 137)) &
 		     !((a.flags & XDPGPU_CFG_ICMP6_ECHO) && ity == 128);
-		ulen6 = i6 ? plen : bswap16(F[14] >> 16);
-		v6 = (!a.force_generic) & staged & !v1 & ((F[3] & 0xffffu) == 0xdd86u) &
-		     (((F[3] >> 20) & 0xf) == 6) & ((nh6 == 17) | i6) & (len >= 62) &
-		     (54 + plen <= len) & (ulen6 >= 8) & (ulen6 <= plen) & (a.res != nullptr);
+		ulen6 = u6 ? bswap16(r[14] >> 16) : plen;
+		v6 = (!a.force_generic) & staged & ((r[3] & 0xffffu) == 0xdd86u) &
+		     (((r[3] >> 20) & 0xf) == 6) & (l3 + 40 + plen <= len) &
+		     ((u6 & (nv <= 1) & (ulen6 >= 8) & (ulen6 <= plen)) | i6 |
+		      (t6 & (nv <= 1) & (plen >= 20))) &
+		     (a.res != nullptr);
 		i6 = i6 & v6;
+		t6 = t6 & v6;
 		/* always through the bulk pass, which also writes the
 		 * network_tuple (its addresses are not among the words a tile
 		 * keeps for its stores); a payload inside the window is an
@@ -1656,31 +1730,39 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 	uint32_t c3v = c3, c4v = c4, clv = cl, l4v = l4, protov = proto;
 	bool udpv = udp;
 	if constexpr (V6) {
-		/* the v6 frame's terms (selected per lane: branch free) */
-		uint64_t p6 = (uint64_t)__builtin_bswap32(ulen6) + __builtin_bswap32(i6 ? 58u : 17u);
+		/* the v6 frame's terms (selected per lane: branch free), in the
+		 * shifted words: L4 at 54, addresses at 22-53 */
+		uint64_t p6 = (uint64_t)__builtin_bswap32(ulen6) + __builtin_bswap32(nh6);
 #pragma unroll
 		for (int k = 0; k < 4; k++) {
-			const uint32_t sk = (F[5 + k] >> 16) | (F[6 + k] << 16);
-			const uint32_t dk = (F[9 + k] >> 16) | (F[10 + k] << 16);
+			const uint32_t sk = (r[5 + k] >> 16) | (r[6 + k] << 16);
+			const uint32_t dk = (r[9 + k] >> 16) | (r[10 + k] << 16);
 			p6 += (uint64_t)sk + dk;
 			key[k] = v6 ? sk : key[k];
 			key[5 + k] = v6 ? dk : key[5 + k];
 		}
 		const int32_t e6 = (int32_t)(54 + ulen6);
-		/* check word: UDP bytes 60-61, ICMPv6 bytes 56-57 */
-		const uint64_t s46 = p6 + (F[13] & 0xffff0000u) +
-				     (F[14] & first_bytes(e6 - 56) & (i6 ? 0xffff0000u : ~0u)) +
-				     (F[15] & first_bytes(e6 - 60) & (i6 ? ~0u : 0xffff0000u));
-		key[4] = v6 ? (i6 ? 0u : F[13] >> 16) : key[4];
-		key[9] = v6 ? (i6 ? 0u : F[14] & 0xffffu) : key[9];
-		key[10] = v6 ? ((i6 ? 58u : 17u) | (10u << 16)) : key[10];
+		/* L4 bytes [54, 64 - 4 nv) of the window (r is zero past it);
+		 * the check word left out where it lies inside: ICMPv6 at
+		 * 56-57, UDP at 60-61 (TCP's, at 70-71, never does) */
+		const bool u6 = v6 & !i6 & !t6;
+		const uint64_t s46 = p6 + (r[13] & 0xffff0000u) +
+				     (r[14] & first_bytes(e6 - 56) & (i6 ? 0xffff0000u : ~0u)) +
+				     (r[15] & first_bytes(e6 - 60) & (u6 ? 0xffff0000u : ~0u));
+		key[4] = v6 ? (i6 ? 0u : r[13] >> 16) : key[4];
+		key[9] = v6 ? (i6 ? 0u : r[14] & 0xffffu) : key[9];
+		key[10] = v6 ? (nh6 | (10u << 16)) : key[10];
 		s4v = v6 ? s46 : s4v;
 		s3v = v6 ? 0xffffull : s3v;      /* no IPv6 header checksum: l3 ok */
 		c3v = v6 ? 0u : c3v;
-		c4v = v6 ? (i6 ? F[14] & 0xffffu : F[15] & 0xffffu) : c4v;
+		/* the check word where the window holds it (0: late, the bulk
+		 * pass loads it) */
+		c4v = v6 ? (i6 ? (nv <= 1 ? r[14] & 0xffffu : 0u)
+			       : u6 && nv == 0 ? r[15] & 0xffffu : 0u)
+			 : c4v;
 		clv = v6 ? ulen6 : clv;
-		l4v = v6 ? 54u : l4v;
-		protov = v6 ? (i6 ? 58u : 17u) : protov;
+		l4v = v6 ? 54u + 4 * nv : l4v;
+		protov = v6 ? nh6 : protov;
 		udpv = udpv & !v6;               /* a stored 0 is not absent */
 	}
 	const uint32_t l3c = v6 ? 0u : ~fold16(s3v) & 0xffff;

@@ -120,7 +120,8 @@ class PoolSpec(C.Structure):
                 ("vlan_pri", C.c_uint16), ("fill_pattern", C.c_uint32),
                 ("dmac", C.c_uint8 * 6), ("smac", C.c_uint8 * 6),
                 ("saddr", C.c_uint32), ("daddr", C.c_uint32),
-                ("threads", C.c_uint32), ("rsvd", C.c_uint32 * 3)]
+                ("threads", C.c_uint32), ("ppm_v6", C.c_uint32),
+                ("rsvd", C.c_uint32 * 2)]
 
 
 class Nat64Cfg(C.Structure):

@@ -482,7 +482,11 @@ struct xdpgpu_pool_spec {
 	uint32_t saddr;        /* wire order; 0 = the generator's default     */
 	uint32_t daddr;
 	uint32_t threads;      /* 0: hardware concurrency                     */
-	uint32_t rsvd[3];
+	uint32_t ppm_v6;       /* IMIX: per-million IPv6 frames over the whole
+				* pool (300000); the 64 B class
+				* is IPv4-only, so the 570/1500 B classes carry
+				* all of them.  0 in a default spec = 300000  */
+	uint32_t rsvd[2];
 };
 
 /* Bytes of UMEM needed for n frames of this spec. */

@@ -81,9 +81,17 @@ def test_pool_imix_mix():
     assert abs(frac[0] - 7 / 12) < 0.03 and abs(frac[2] - 1 / 12) < 0.02
     live = (v == xdpgpu.REDIRECT)
     f = res["flags"][live]
-    # 30 % of the 570/1500 B classes (5/12 of frames) are IPv6
-    assert 0.10 < np.mean((f & xdpgpu.F_IPV6) > 0) < 0.15
+    # 30 % of the pool IPv6, all in the 570/1500 B classes
+    assert 0.27 < np.mean((f & xdpgpu.F_IPV6) > 0) < 0.33
+    big = descs["len"][live] > 64
+    assert not ((f & xdpgpu.F_IPV6) > 0)[~big].any()
     assert 0.17 < np.mean((f & xdpgpu.F_VLAN) > 0) < 0.27
+    # the round-2 mix (30 % of the 570/1500 B classes) stays available
+    umem, descs, _ = xdpgpu.pool_generate(120000, xdpgpu.POOL_IMIX, 64, 0x5EED0003,
+                                          ppm_v6=125000)
+    v, res, _, _ = oracle.process(umem, descs, 0x5, 0, 2)
+    f = res["flags"][v == xdpgpu.REDIRECT]
+    assert 0.10 < np.mean((f & xdpgpu.F_IPV6) > 0) < 0.15
 
 
 def test_reference_generator_frames():

@@ -366,6 +366,93 @@ def icmp6_frames(seed: int, n: int):
     return umem, descs
 
 
+def v6_late_frames(seed: int, n: int):
+    """IPv6 frames behind 0, 1 or 2 VLAN tags (802.1Q / 802.1ad) with UDP,
+    TCP or ICMPv6 and no extension header: the fast shape's "late" check
+    words (TCP; UDP behind a tag; ICMPv6 behind two) and the shapes just
+    outside it (UDP and TCP behind two tags).  TCP data offsets below 5,
+    past the frame and past the payload length (parse_tcphdr: ABORTED);
+    odd lengths, bad checksums, trailing pad, lengths from the smallest
+    that parse to past 1500 B; 16-byte aligned, the last frame ending at
+    the UMEM end."""
+    import frames as F
+    rng = np.random.default_rng(seed)
+    blobs = []
+    for k in range(n):
+        tags = [[], [(0x8100, 7)], [(0x88A8, 3), (0x8100, 9)]][k % 3]
+        kind = (k // 3) % 4
+        plen = int(rng.integers(0, 40)) if k % 2 else int(rng.integers(0, 1600))
+        pay = rng.integers(0, 256, plen, dtype=np.uint8).tobytes()
+        pad = b""
+        if kind == 0:
+            fr = F.v6_frame(17, F.udp(int(rng.integers(1, 65536)), 53, pay), tags=tags)
+        elif kind == 1:
+            typ = [1, 128, 129, 135, 143][k % 5]
+            fr = F.v6_frame(58, F.icmp(typ, 0, b"\x00\x01\x00\x02" + pay), tags=tags)
+        else:
+            doff = int(rng.integers(5, 16))
+            bad = rng.random()
+            if kind == 3 and bad < 0.3:
+                doff = int(rng.integers(0, 5))            # thl < 20
+            seg = F.tcp(int(rng.integers(1, 65536)), 80, pay, doff=doff,
+                        options=b"\x01" * max(0, doff * 4 - 20))
+            if kind == 3 and 0.3 <= bad < 0.6:
+                # the data offset past the payload length, the frame long
+                # enough to hold it (trailing pad): cl < thl
+                seg = F.tcp(int(rng.integers(1, 65536)), 80, pay[:4], doff=15, options=b"")
+                pad = b"\x00" * 48
+            fr = F.v6_frame(6, seg, tags=tags)
+            if kind == 3 and 0.6 <= bad < 0.75:
+                # the data offset past the frame itself
+                seg = F.tcp(int(rng.integers(1, 65536)), 80, b"", doff=15, options=b"")
+                fr = F.v6_frame(6, seg, tags=tags)
+        if rng.random() < 0.1:
+            b = bytearray(fr)
+            b[-1 - int(rng.integers(0, 8))] ^= 0x5A
+            fr = bytes(b)
+        fr += pad
+        if rng.random() < 0.1:
+            fr += rng.integers(0, 256, int(rng.integers(1, 9)), dtype=np.uint8).tobytes()
+        blobs.append(fr)
+    offs, o = [], 0
+    for fr in blobs:
+        o += 16 * int(rng.integers(0, 3))
+        offs.append(o)
+        o = (o + len(fr) + 15) & ~15
+    umem = np.zeros(offs[-1] + len(blobs[-1]), np.uint8)
+    for off, fr in zip(offs, blobs):
+        umem[off:off + len(fr)] = np.frombuffer(fr, np.uint8)
+    descs = np.zeros(n, xdpgpu.DESC_DTYPE)
+    descs["addr"] = offs
+    descs["len"] = [len(fr) for fr in blobs]
+    return umem, descs
+
+
+def test_v6_late_frames_cover_aborted_tcp():
+    """The generator's TCP cases reach parse_tcphdr's failures (the oracle
+    ABORTs them) and the rest of the shapes verify or drop."""
+    umem, descs = v6_late_frames(41, 3000)
+    v, _, _, st = oracle.process(umem.copy(), descs, 0x5, 0, 2)
+    assert (v == xdpgpu.ABORTED).sum() > 50
+    assert (v == xdpgpu.REDIRECT).sum() > 1500 and (v == xdpgpu.DROP).sum() > 50
+    assert (v == xdpgpu.PASS).sum() > 50          # NDP
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tune", [0, 1 << 21, 4 << 21])
+def test_v6_late_frames_vs_oracle(dev, tune):
+    """Tagged IPv6 and IPv6/TCP through the network_tuple / no-tuple builds
+    (late check words and data offsets in the bulk pass) against the
+    oracle, with and without the echo responder."""
+    umem, descs = v6_late_frames(41, 3000)
+    for flags, iv, fmt in ((0x5, 0, 2), (0x4, 7, 0), (0x7, 0x1234, 2), (0x1, 0, 2)):
+        ou = umem.copy()
+        ov, ores, otup, ost = oracle.process(ou, descs, flags, iv, fmt)
+        v, res, tup, um2, st = run_dev(umem, descs, flags | xdpgpu.CFG_STATS, iv, fmt, 64, tune)
+        assert_same((v, res, tup, um2), (ov, ores, otup, ou), f"late/{flags:#x}/fmt{fmt}")
+        oracle_stats_match(st, ost)
+
+
 @pytest.mark.parametrize("tune", [0, 1 << 15, 1 << 21])
 def test_v6_build_icmp_vs_oracle(dev, golden, tune):
     """The network_tuple / no-tuple builds with and without the echo

@@ -19,13 +19,14 @@
 #   bench                  python bench.py (every leg)
 #   bench:ARGS             python bench.py ARGS (words split on '+')
 #   prof:NAME              rocprofv3 --kernel-trace --stats of a workload
-#                          (config2 1500 imix imix30 nat64 nat64_egress
+#                          (config2 1500 imix imix_r2 nat64 nat64_egress
 #                          nat64_dynamic frags synproxy echo)
 #   pmc:NAME               PMC passes (tools/pmc_profile.sh) on a workload
-#                          (config2 imix imix30 nat64 nat64_egress 1500)
+#                          (config2 imix imix_r2 nat64 nat64_egress 1500)
 #   ab:LIB                 A/B: the in-tree library vs LIB, alternating
 #                          processes (IMIX, 1500 B, config 2)
-#   stamps                 per-wave timeline (build/stamps, tools/stamps.py)
+#   run:LIB:WORKLOAD       one workload (tune_rx timing) with library LIB
+#   stamps[:N+TUNE+KIND+FMT] per-wave timeline (build/stamps, tools/stamps.py)
 #   probe                  tools/order_probe (LDS-DMA / vmcnt ordering)
 #   e2e                    PCIe-inclusive host path (bench.py --e2e)
 #   cli                    xdpsock-gpu over a 16 M-frame pool
@@ -57,7 +58,7 @@ workload() {
 	config2) echo "python3 tools/tune_rx.py --variants 64:0 --rounds 3" ;;
 	1500) echo "python3 tools/tune_rx.py --variants 64:0 --rounds 3 --frames 2097152 --size 1500" ;;
 	imix) echo "python3 tools/tune_rx.py --variants 64:0 --rounds 3 --frames 16777216 --kind 1 --seed 0x5EED0003 --fmt 2" ;;
-	imix30) echo "python3 tools/tune_rx.py --variants 64:0 --rounds 3 --frames 16777216 --kind 4 --seed 0x5EED0003 --fmt 2" ;;
+	imix_r2) echo "python3 tools/tune_rx.py --variants 64:0 --rounds 3 --frames 16777216 --kind 1 --seed 0x5EED0003 --fmt 2 --ppm-v6 125000" ;;
 	nat64) echo "python3 tools/nat64_probe.py --reps 5" ;;
 	nat64_egress) echo "python3 tools/nat64_probe.py --reps 5 --direction 1" ;;
 	nat64_dynamic) echo "python3 tools/nat_dyn_probe.py --frames 16777216 --reps 5" ;;
@@ -109,7 +110,16 @@ for s in "$@"; do
 				step "ab_config2_$tag" 150 env XDPGPU_LIB="$lib" $(workload config2)
 			done
 		done ;;
-	stamps) step stamps 200 env XDPGPU_LIB=build/stamps/libxdpgpu.so python3 -u tools/stamps.py ;;
+	run)
+		lib=${arg%%:*}
+		wl=${arg#*:}
+		# shellcheck disable=SC2046
+		step "run_${wl}_$(basename "$(dirname "$lib")")_$(date +%s)" 200 env XDPGPU_LIB="$lib" \
+			$(workload "$wl") ;;
+	stamps)
+		# shellcheck disable=SC2086
+		step "stamps${arg:+_$(echo "$arg" | tr '+' '_')}" 200 env XDPGPU_LIB=build/stamps/libxdpgpu.so \
+			python3 -u tools/stamps.py ${arg//+/ } ;;
 	probe) step probe 120 tools/order_probe 64 ;;
 	e2e) step e2e 600 python3 bench.py --no-cpu --no-secondary --steps 10 --e2e ;;
 	cli) step cli 300 bpf-examples_amd/apps/xdpsock-gpu --pool 16777216 --pool-kind udp4 \

@@ -27,9 +27,12 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--variants", default="ceil,64:0,64:256,64:512,128:0")
     ap.add_argument("--fmt", type=int, default=xdpgpu.TUPLE_V4)
+    ap.add_argument("--ppm-v6", type=int, default=0,
+                    help="IMIX: IPv6 frames per million (0: the pool's default)")
     args = ap.parse_args()
     n = args.frames
-    umem, descs, expect = xdpgpu.pool_generate(n, args.kind, args.size, args.seed)
+    kw = {"ppm_v6": args.ppm_v6} if args.ppm_v6 else {}
+    umem, descs, expect = xdpgpu.pool_generate(n, args.kind, args.size, args.seed, **kw)
     dev = torch.device("cuda:0")
     d_umem = torch.zeros(umem.nbytes + 64, dtype=torch.uint8, device=dev)
     d_umem[: umem.nbytes].copy_(torch.from_numpy(umem))
