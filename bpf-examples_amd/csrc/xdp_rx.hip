@@ -1035,6 +1035,7 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 
 /* non-temporal 16-byte store (streamed outputs, written once) */
 typedef unsigned int v4u_t __attribute__((ext_vector_type(4)));
+typedef unsigned int v3u_t __attribute__((ext_vector_type(3)));
 __device__ __forceinline__ void st_nt16(void *p, uint4 r)
 {
 	v4u_t v = {r.x, r.y, r.z, r.w};
@@ -1093,68 +1094,49 @@ constexpr bool kTailRecNt = XDP_TAIL_REC_NT != 0;
 #define XDP_TAIL_VERDICT_NT 0
 #endif
 constexpr bool kTailVerdictNt = XDP_TAIL_VERDICT_NT != 0;
-template <int U, bool NT, bool GEN, int G>
-__device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
-					   uint4 *part4, int lane,
-					   const void *list, uint32_t nb,
-					   uint32_t (&cnt)[CNT_FRAG + 1],
-					   uint64_t &my_bytes)
+/* A 44-byte network_tuple at a dword-aligned address: two 16-byte stores
+ * and a 12-byte one (global stores need only dword alignment) */
+__device__ __forceinline__ void store_tuple44(uint8_t *p, const uint32_t (&t)[11])
 {
-	uint32_t *part = reinterpret_cast<uint32_t *>(part4);
+	const v4u_t a0 = {t[0], t[1], t[2], t[3]}, a1 = {t[4], t[5], t[6], t[7]};
+	const v3u_t a2 = {t[8], t[9], t[10]};
+	asm volatile("global_store_dwordx4 %0, %1, off\n\t"
+		     "global_store_dwordx4 %0, %2, off offset:16\n\t"
+		     "global_store_dwordx3 %0, %3, off offset:32\n\t"
+		     "s_nop 2"
+		     :: "v"(p), "v"(a0), "v"(a1), "v"(a2) : "memory");
+}
+
+/* Who stores an IPv6 frame's network_tuple (build knob): 1 the tile
+ * loop, from the window, when it classifies the frame (every tuple sector
+ * written in one pass); 0 the bulk pass, from frame bytes [16, 64) it
+ * loads again */
+#ifndef XDP_TUP6_TILE
+#define XDP_TUP6_TILE 1
+#endif
+constexpr bool kTup6Tile = XDP_TUP6_TILE != 0;
+
+/* Diagnostic builds of the bulk pass (XDP_TAIL_DIAG, never the product):
+ * bit 0: no output stores (record, verdict, tuple); bit 1: no payload
+ * loads (the range summed as zeros) */
+#ifndef XDP_TAIL_DIAG
+#define XDP_TAIL_DIAG 0
+#endif
+/* Batch-adaptive group size (build knob): 1 smaller groups for batches
+ * of short ranges only; 0 always G */
+#ifndef XDP_TAIL_ADAPT
+#define XDP_TAIL_ADAPT 0
+#endif
+constexpr bool kTailAdapt = XDP_TAIL_ADAPT != 0;
+/* The bulk pass's payload streaming, G lanes per frame (dynamic frame
+ * assignment): every listed frame's partial sums into part (16 per frame,
+ * zero-filled for G < 16).  meta: the batch's ranges. */
+template <int G, int U, bool NT>
+__device__ __forceinline__ void stream_groups(const RxArgs &a, const uint4 *meta,
+					      uint32_t *part, int lane, uint32_t nb)
+{
 	static_assert(G == 16 || G == 8 || G == 4, "group of 16, 8 or 4 lanes per frame");
 	const uint32_t sub = lane & (G - 1);
-	const bool act = (uint32_t)lane < nb;
-	uint4 ye = make_uint4(0, 0, 0, 0);
-	uint64_t i;
-	if constexpr (GEN) {
-		ye = reinterpret_cast<const uint4 *>(list)[act ? lane : 0];
-		i = ye.x;
-	} else {
-		i = reinterpret_cast<const uint32_t *>(list)[act ? lane : 0];
-	}
-	if (DBG_BAD(i >= a.n, GEN ? 3 : 2, i))
-		i = 0;
-	const uint4 dv = *reinterpret_cast<const uint4 *>(a.desc + i);
-	uint4 rv = *reinterpret_cast<const uint4 *>(a.res + i);
-	const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
-	const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
-	const uint32_t cl = rv.w >> 16;
-	/* GEN false: the fast shape's records; IPv6/UDP (V6 builds) has its
-	 * L4 header 40 bytes after l3 and no over-read byte */
-	const bool r6 = !GEN && (rv.z & XDPGPU_F_IPV6);
-	/* IPv4 ICMP (V6 builds): no over-read byte either */
-	const bool nov = r6 || ((rv.z >> 8) & 0xff) == 1;
-	const uint32_t l4 = GEN ? (rv.w & 0xffff) : ((rv.z >> 16) & 0xff) + (r6 ? 40u : 20u);
-	const uint32_t rhi = GEN ? (ye.w & 0xffff) : l4 + cl + (nov ? 0u : (cl & 1));
-	uint64_t lim = eff + rhi;
-	lim = lim < a.usize ? lim : a.usize;
-	/* an IPv6/UDP frame's network_tuple words (the tile stored none):
-	 * frame bytes [16, 64), loaded here so that the round trip overlaps
-	 * the payload streaming */
-	const bool tup6 = !GEN && act && r6 && a.tup && a.tuple_fmt == XDPGPU_TUPLE_NET;
-	uint4 h1 = make_uint4(0, 0, 0, 0), h2 = h1, h3 = h1;
-	if (tup6) {
-		h1 = *reinterpret_cast<const uint4 *>(a.umem + eff + 16);
-		h2 = *reinterpret_cast<const uint4 *>(a.umem + eff + 32);
-		h3 = *reinterpret_cast<const uint4 *>(a.umem + eff + 48);
-	}
-	/* a "late" IPv6 frame (fast_tile): its check word (and TCP's data
-	 * offset) lie in frame bytes [64, 80), which the UMEM holds (both
-	 * before l4 + 20 <= len) */
-	const uint32_t p6 = (rv.z >> 8) & 0xff;
-	const uint32_t chk6 = p6 == 6 ? 16u : p6 == 17 ? 6u : 2u;
-	const bool late = r6 && l4 + chk6 >= 64;
-	uint4 x64 = make_uint4(0, 0, 0, 0);
-	if (act && late)
-		x64 = *reinterpret_cast<const uint4 *>(a.umem + eff + 64);
-	/* absolute range [lo, lim), streamed from its 16-byte aligned start */
-	const uint64_t lo = eff + (GEN ? (ye.z & 0xffff) : 64u);
-	const uint64_t lo_al = lo & ~15ull;
-	meta[lane] = make_uint4((uint32_t)lo_al, (uint32_t)(lo_al >> 32),
-				(uint32_t)(lim > lo ? lim - lo_al : 0),
-				(uint32_t)(lo - lo_al));
-	__builtin_amdgcn_wave_barrier();
-
 	/* G-lane group streaming with dynamic frame assignment.  Loads under
 	 * their lane's range only: a branch-free form (every lane loading, the
 	 * chunks outside masked to zero) lets the compiler count loads in
@@ -1173,7 +1155,7 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 		for (int u = 0; u < U; u++) {
 			const uint32_t ou = o + 16 * G * u + 16 * sub;
 			v[u] = make_uint4(0, 0, 0, 0);
-			if (live && ou < fnb)
+			if (!(XDP_TAIL_DIAG & 2) && live && ou < fnb)
 				v[u] = NT ? ld_nt16(a.umem + flo + ou)
 					  : *reinterpret_cast<const uint4 *>(a.umem + flo + ou);
 		}
@@ -1211,11 +1193,94 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 			nxt += (uint32_t)__popcll(dq);
 		}
 	}
+}
+
+template <int U, bool NT, bool GEN, int G>
+__device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
+					   uint4 *part4, int lane,
+					   const void *list, uint32_t nb,
+					   uint32_t (&cnt)[CNT_FRAG + 1],
+					   uint64_t &my_bytes)
+{
+	uint32_t *part = reinterpret_cast<uint32_t *>(part4);
+	const bool act = (uint32_t)lane < nb;
+	uint4 ye = make_uint4(0, 0, 0, 0);
+	uint64_t i;
+	if constexpr (GEN) {
+		ye = reinterpret_cast<const uint4 *>(list)[act ? lane : 0];
+		i = ye.x;
+	} else {
+		i = reinterpret_cast<const uint32_t *>(list)[act ? lane : 0];
+	}
+	if (DBG_BAD(i >= a.n, GEN ? 3 : 2, i))
+		i = 0;
+	const uint4 dv = *reinterpret_cast<const uint4 *>(a.desc + i);
+	uint4 rv = *reinterpret_cast<const uint4 *>(a.res + i);
+	const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
+	const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
+	const uint32_t cl = rv.w >> 16;
+	/* GEN false: the fast shape's records; IPv6/UDP (V6 builds) has its
+	 * L4 header 40 bytes after l3 and no over-read byte */
+	const bool r6 = !GEN && (rv.z & XDPGPU_F_IPV6);
+	/* IPv4 ICMP (V6 builds): no over-read byte either */
+	const bool nov = r6 || ((rv.z >> 8) & 0xff) == 1;
+	const uint32_t l4 = GEN ? (rv.w & 0xffff) : ((rv.z >> 16) & 0xff) + (r6 ? 40u : 20u);
+	const uint32_t rhi = GEN ? (ye.w & 0xffff) : l4 + cl + (nov ? 0u : (cl & 1));
+	uint64_t lim = eff + rhi;
+	lim = lim < a.usize ? lim : a.usize;
+	/* an IPv6/UDP frame's network_tuple words (the tile stored none):
+	 * frame bytes [16, 64), loaded here so that the round trip overlaps
+	 * the payload streaming */
+	const bool net6 = !GEN && act && r6 && a.tup && a.tuple_fmt == XDPGPU_TUPLE_NET;
+	/* the tile stored it (XDP_TUP6_TILE) unless this pass builds it */
+	const bool tup6 = net6 && !kTup6Tile;
+	/* an untagged ICMPv6 frame under the echo responder: its first 64
+	 * bytes, for the type and the rewrite */
+	const bool echo6 = !GEN && act && r6 && (a.flags & XDPGPU_CFG_ICMP6_ECHO) &&
+			   ((rv.z >> 8) & 0xff) == 58 && (rv.z >> 24) == 0;
+	uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0, h2 = h0, h3 = h0;
+	if (tup6 || echo6) {
+		h1 = *reinterpret_cast<const uint4 *>(a.umem + eff + 16);
+		h2 = *reinterpret_cast<const uint4 *>(a.umem + eff + 32);
+		h3 = *reinterpret_cast<const uint4 *>(a.umem + eff + 48);
+	}
+	if (echo6)
+		h0 = *reinterpret_cast<const uint4 *>(a.umem + eff);
+	/* a "late" IPv6 frame (fast_tile): its check word (and TCP's data
+	 * offset) lie in frame bytes [64, 80), which the UMEM holds (both
+	 * before l4 + 20 <= len) */
+	const uint32_t p6 = (rv.z >> 8) & 0xff;
+	const uint32_t chk6 = p6 == 6 ? 16u : p6 == 17 ? 6u : 2u;
+	const bool late = r6 && l4 + chk6 >= 64;
+	uint4 x64 = make_uint4(0, 0, 0, 0);
+	if (act && late)
+		x64 = *reinterpret_cast<const uint4 *>(a.umem + eff + 64);
+	/* absolute range [lo, lim), streamed from its 16-byte aligned start */
+	const uint64_t lo = eff + (GEN ? (ye.z & 0xffff) : 64u);
+	const uint64_t lo_al = lo & ~15ull;
+	uint32_t t = 0;
+	meta[lane] = make_uint4((uint32_t)lo_al, (uint32_t)(lo_al >> 32),
+				(uint32_t)(lim > lo ? lim - lo_al : 0),
+				(uint32_t)(lo - lo_al));
+	__builtin_amdgcn_wave_barrier();
+
+	/* the group size: 16 lanes per frame, fewer when every range of the
+	 * batch is short (the echo leg's 128-byte frames: 4 lanes, 16 frames
+	 * a step instead of 4) */
+	uint32_t mx = act && lim > lo ? (uint32_t)(lim - lo_al) : 0u;
+#pragma unroll
+	for (int d = 1; d < kWave; d <<= 1)
+		mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, kWave));
+	if (kTailAdapt && mx <= 256)
+		stream_groups<4, U, NT>(a, meta, part, lane, nb);
+	else if (kTailAdapt && mx <= 512)
+		stream_groups<8, U, NT>(a, meta, part, lane, nb);
+	else
+		stream_groups<G, U, NT>(a, meta, part, lane, nb);
 	__builtin_amdgcn_wave_barrier();
 
 	/* lane f completes frame f: exact, a range is < 64 KiB + 64 B so
 	 * the raw sum of 16-bit halves fits 32 bits */
-	uint32_t t = 0;
 #pragma unroll
 	for (int j = 0; j < 4; j++) {
 		const uint4 x = part4[4 * lane + ((j + lane) & 3)];
@@ -1259,18 +1324,49 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 	}
 	const bool l4_ok = absent || (~fold16((uint64_t)sum4 + c4) & 0xffff) == 0;
 	const bool drop = (a.flags & XDPGPU_CFG_VERIFY_CSUM) && (l3_bad || !l4_ok);
-	if (act && abort6) {
+	/* process_packet's echo reply (af_xdp_user.c:968-1040) for an echo
+	 * request that was not dropped: MACs and addresses swapped, type 129,
+	 * csum_replace2 of the type word, written over the first 64 bytes as
+	 * whole 16-byte chunks; the record and tuple are the request's */
+	const bool echo_tx = echo6 && ((h3.y >> 16) & 0xff) == 128 && !drop;
+	if (echo_tx && !(XDP_TAIL_DIAG & 1)) {
+		uint32_t d[16] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w,
+				  h2.x, h2.y, h2.z, h2.w, h3.x, h3.y, h3.z, h3.w};
+		uint32_t o[16];
+		auto byte = [&](int b) -> uint32_t { return (d[b >> 2] >> (8 * (b & 3))) & 0xff; };
+		auto src = [&](int b) -> int {
+			return b < 6 ? b + 6 : b < 12 ? b - 6 : (b >= 22 && b < 38) ? b + 16
+			       : (b >= 38 && b < 54) ? b - 16 : b;
+		};
+#pragma unroll
+		for (int w = 0; w < 16; w++)
+			o[w] = byte(src(4 * w)) | (byte(src(4 * w + 1)) << 8) |
+			       (byte(src(4 * w + 2)) << 16) | (byte(src(4 * w + 3)) << 24);
+		/* byte 54: type 129; bytes 56-57: the check word */
+		const uint32_t ck = csum_replace2(d[14] & 0xffff, 0x0080, 0x0081);
+		o[13] = (o[13] & 0xff00ffffu) | (129u << 16);
+		o[14] = (o[14] & 0xffff0000u) | ck;
+		uint4 *fw = reinterpret_cast<uint4 *>(a.umem + eff);
+		fw[0] = make_uint4(o[0], o[1], o[2], o[3]);
+		fw[1] = make_uint4(o[4], o[5], o[6], o[7]);
+		fw[2] = make_uint4(o[8], o[9], o[10], o[11]);
+		fw[3] = make_uint4(o[12], o[13], o[14], o[15]);
+	}
+	if (XDP_TAIL_DIAG & 1) {
+		/* diagnostic: no output stores */
+	} else if (act && abort6) {
 		/* ABORTED frames carry all-zero records and tuples */
 		const uint4 z = make_uint4(0, 0, 0, 0);
 		if constexpr (kTailRecNt)
 			st_nt16(a.res + i, z);
 		else
 			*reinterpret_cast<uint4 *>(a.res + i) = z;
-		if (tup6) {
-			uint32_t *tz = reinterpret_cast<uint32_t *>(a.tup + 44 * i);
-#pragma unroll
-			for (int k = 0; k < 11; k++)
-				tz[k] = 0u;
+		if (net6) {
+			const uint32_t tz[11] = {};
+			store_tuple44(a.tup + 44 * i, tz);
+		} else if (a.tup && a.tuple_fmt == XDPGPU_TUPLE_V4) {
+			/* the tile stored the 16-byte tuple */
+			*reinterpret_cast<uint4 *>(a.tup + 16 * i) = z;
 		}
 		a.verdict[i] = (uint8_t)XDPGPU_ABORTED;
 		my_bytes += dv.z;
@@ -1296,7 +1392,7 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 				w[k] = nv == 0 ? w0[k]
 				     : nv == 1 ? (k + 1 < 12 ? w0[k + 1] : 0u)
 					       : (k + 2 < 12 ? w0[k + 2] : 0u);
-			uint32_t *t = reinterpret_cast<uint32_t *>(a.tup + 44 * i);
+			uint32_t t[11];
 #pragma unroll
 			for (int k = 0; k < 4; k++) {
 				t[k] = (w[1 + k] >> 16) | (w[2 + k] << 16);
@@ -1307,12 +1403,15 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 			t[4] = ports ? w[9] >> 16 : 0u;
 			t[9] = ports ? w[10] & 0xffffu : 0u;
 			t[10] = p6 | (10u << 16);
+			/* three wide stores (the record is dword aligned): eleven
+			 * scattered dword stores cost IMIX 0.5 ms of tail stores */
+			store_tuple44(a.tup + 44 * i, t);
 		}
+		const uint8_t vd = echo_tx ? XDPGPU_TX : drop ? XDPGPU_DROP : XDPGPU_REDIRECT;
 		if constexpr (kTailVerdictNt)
-			__builtin_nontemporal_store((uint8_t)(drop ? XDPGPU_DROP : XDPGPU_REDIRECT),
-						    a.verdict + i);
+			__builtin_nontemporal_store(vd, a.verdict + i);
 		else
-			a.verdict[i] = (uint8_t)(drop ? XDPGPU_DROP : XDPGPU_REDIRECT);
+			a.verdict[i] = vd;
 		my_bytes += dv.z;
 	}
 	if (a.stats) {
@@ -1320,7 +1419,8 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 		cnt[CNT_FRAMES] += __popcll(__ballot(act));
 		cnt[CNT_VERDICT0 + XDPGPU_ABORTED] += __popcll(__ballot(act && abort6));
 		cnt[CNT_VERDICT0 + XDPGPU_DROP] += __popcll(__ballot(fin && drop));
-		cnt[CNT_VERDICT0 + XDPGPU_REDIRECT] += __popcll(__ballot(fin && !drop));
+		cnt[CNT_VERDICT0 + XDPGPU_TX] += __popcll(__ballot(fin && echo_tx));
+		cnt[CNT_VERDICT0 + XDPGPU_REDIRECT] += __popcll(__ballot(fin && !drop && !echo_tx));
 		cnt[CNT_L3_BAD] += __popcll(__ballot(fin && l3_bad));
 		cnt[CNT_L4_BAD] += __popcll(__ballot(fin && !l4_ok));
 		cnt[CNT_L4_ABSENT] += __popcll(__ballot(fin && absent));
@@ -1391,7 +1491,6 @@ __device__ __forceinline__ void st_asm_b128(void *p, uint4 r)
 	asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 2" :: "v"(p), "v"(v) : "memory");
 }
 
-typedef unsigned int v3u_t __attribute__((ext_vector_type(3)));
 __device__ __forceinline__ void st_asm_b96(void *p, uint32_t x, uint32_t y, uint32_t z)
 {
 	const v3u_t v = {x, y, z};
@@ -1507,7 +1606,8 @@ struct TileOut {
 	uint64_t t0;       /* first frame of the tile (wave-uniform)        */
 	uint32_t li;       /* this lane's frame in the tile                 */
 	uint32_t fl;       /* bit 0: verdict store, bit 1: record and tuple,
-			    * bit 2: no tuple (IPv6: the bulk pass's)   */
+			    * bit 2: IPv6 (network_tuple: the bulk
+			    * pass's; 16-byte tuple: stored here)      */
 	uint32_t verdict;
 	uint32_t sa, da, ports, proto, vid;
 	uint4 rec;
@@ -1555,10 +1655,14 @@ __device__ __forceinline__ void store_tile(const RxArgs &a, const TileOut &o)
 	const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
 		tup ? (void *)(a.tup + tb * o.t0) : (void *)a.verdict, 0,
 		tup ? (int)(tb * kWave) : 0, kFmt);
-	const bool tout = out && !(fl & 4);
+	/* an IPv6 frame's network_tuple is the bulk pass's (its addresses
+	 * are not among the words kept here); its 16-byte tuple is stored
+	 * here */
+	const bool tout = out && !((fl & 4) && net);
 	const uint32_t b = tout ? tb * o.li : kOff;
+	const uint32_t ipv = (fl & 4) ? 10u : 2u;
 	const v4u_t w0 = net ? (v4u_t){0u, 0u, 0xffff0000u, o.sa}
-			     : (v4u_t){o.sa, o.da, o.ports, o.proto | (2u << 8) | (o.vid << 16)};
+			     : (v4u_t){o.sa, o.da, o.ports, o.proto | (ipv << 8) | (o.vid << 16)};
 	/* 16-byte tuples: whole lines, streamed (nt).  44-byte tuples: the
 	 * lanes' 16-byte pieces straddle lines that other stores of the tile
 	 * complete, so they stay in L2 to merge there (nt: 2x the loop time on
@@ -1654,9 +1758,10 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 	 *    the payload length; its data offset lies past the window, so the
 	 *    bulk pass checks it (ABORTED when parse_tcphdr would fail);
 	 *  - ICMPv6 (its type in the window) other than NDP (PASS,
-	 *    af_xdp_kern.c:114-148) and, with the echo responder, echo
-	 *    requests (the exception path's TX rewrite), the range the payload
-	 *    length.
+	 *    af_xdp_kern.c:114-148), the range the payload length; with the
+	 *    echo responder, an untagged echo request is answered by the bulk
+	 *    pass once its checksum verifies (process_packet,
+	 *    af_xdp_user.c:968-1040).
 	 * csum_ipv6_magic, an odd length zero padded, a stored 0 not absent.
 	 * A check word at or past byte 64 (TCP; UDP behind a tag; ICMPv6
 	 * behind two) is "late": the bulk pass reads it, and the data offset,
@@ -1669,8 +1774,7 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 		const uint32_t ity = (r[13] >> 16) & 0xff;
 		const bool u6 = nh6 == 17;
 		t6 = nh6 == 6;
-		i6 = (nh6 == 58) & (plen >= 8) & !((ity >= 133) & (ity <= 137)) &
-		     !((a.flags & XDPGPU_CFG_ICMP6_ECHO) && ity == 128);
+		i6 = (nh6 == 58) & (plen >= 8) & !((ity >= 133) & (ity <= 137));
 		ulen6 = u6 ? bswap16(r[14] >> 16) : plen;
 		v6 = (!a.force_generic) & staged & ((r[3] & 0xffffu) == 0xdd86u) &
 		     (((r[3] >> 20) & 0xf) == 6) & (l3 + 40 + plen <= len) &
@@ -1820,12 +1924,20 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 		to->li = (uint32_t)(i - to->t0);
 		to->fl = (fast ? 1u : 0u) | (out ? 2u : 0u) | (v6 ? 4u : 0u);
 		to->verdict = drop ? XDPGPU_DROP : XDPGPU_REDIRECT;
-		to->sa = sa;
-		to->da = da;
-		to->ports = ports;
-		to->proto = proto;
+		/* an IPv6 frame's 16-byte tuple: no addresses, its ports (none
+		 * for ICMPv6), ipv 10 (emit_tuple's layout) */
+		to->sa = v6 ? 0u : sa;
+		to->da = v6 ? 0u : da;
+		to->ports = v6 ? (i6 ? 0u : (r[13] >> 16) | (r[14] << 16)) : ports;
+		to->proto = v6 ? nh6 : proto;
 		to->vid = vid;
 		to->rec = rec;
+		if constexpr (V6 && kTup6Tile) {
+			/* an IPv6 frame's network_tuple now, from the window
+			 * (the deferred stores keep four words of a tuple) */
+			if (v6 && active && a.tup && a.tuple_fmt == XDPGPU_TUPLE_NET)
+				store_tuple44(a.tup + 44 * i, key);
+		}
 	}
 	w.my_bytes += fast ? len : 0;
 	/* counters (wave-uniform: ballots outside divergent code) */
@@ -2842,11 +2954,13 @@ hipError_t launch_rx(const RxArgs &a, uint32_t window, uint32_t max_blocks,
 	if (window != 128 && !(tune & 0x8fffu)) {
 		RxArgs b = a;
 		b.diag = (tune >> 16) & 3;
-		/* untagged IPv6/UDP in the fast shape (IMIX's common IPv6
-		 * frame) for the 44-byte network_tuple and no tuple; bit 18
-		 * turns it off.  The 16-byte IPv4 tuple keeps the IPv4-only
-		 * kernel (config 2), whose registers it would cost. */
-		b.v6 = a.tuple_fmt != XDPGPU_TUPLE_V4 && !((tune >> 18) & 1);
+		/* IPv6 in the fast shape (IMIX's IPv6 frames) for the 44-byte
+		 * network_tuple and no tuple, and with the echo responder
+		 * (its requests are IPv6); bit 18 turns it off.  The 16-byte
+		 * IPv4 tuple otherwise keeps the IPv4-only kernel (config 2),
+		 * whose registers it would cost. */
+		b.v6 = (a.tuple_fmt != XDPGPU_TUPLE_V4 || (a.flags & XDPGPU_CFG_ICMP6_ECHO)) &&
+		       !((tune >> 18) & 1);
 		/* bits 19-20: the tile order (xdp_rx_db_kernel) */
 		b.order = (tune >> 19) & 3;
 		return launch_db(b, max_blocks, stream, ev);

@@ -445,7 +445,8 @@ def test_v6_late_frames_vs_oracle(dev, tune):
     (late check words and data offsets in the bulk pass) against the
     oracle, with and without the echo responder."""
     umem, descs = v6_late_frames(41, 3000)
-    for flags, iv, fmt in ((0x5, 0, 2), (0x4, 7, 0), (0x7, 0x1234, 2), (0x1, 0, 2)):
+    for flags, iv, fmt in ((0x5, 0, 2), (0x4, 7, 0), (0x7, 0x1234, 2), (0x1, 0, 2),
+                           (0x7, 0, 1), (0x3, 5, 0)):
         ou = umem.copy()
         ov, ores, otup, ost = oracle.process(ou, descs, flags, iv, fmt)
         v, res, tup, um2, st = run_dev(umem, descs, flags | xdpgpu.CFG_STATS, iv, fmt, 64, tune)
@@ -455,18 +456,23 @@ def test_v6_late_frames_vs_oracle(dev, tune):
 
 @pytest.mark.parametrize("tune", [0, 1 << 15, 1 << 21])
 def test_v6_build_icmp_vs_oracle(dev, golden, tune):
-    """The network_tuple / no-tuple builds with and without the echo
-    responder: IPv4 ICMP and ICMPv6 other than NDP (and, with the
-    responder, other than echo requests) go through the fast shape and the
-    bulk pass; the golden fixtures, ICMPv6 frames of every type class and
-    the IMIX pool against the oracle."""
+    """The IPv6 builds (network_tuple, no tuple, and any tuple with the echo
+    responder): IPv4 ICMP and ICMPv6 other than NDP go through the fast
+    shape and the bulk pass, which answers untagged echo requests; the
+    golden fixtures, ICMPv6 frames of every type class, the IMIX pool and
+    the echo bench leg's pool against the oracle (UMEM after included)."""
     fx, _ = golden
     cases = [("golden", fx["umem"], fx["descs"].view(xdpgpu.DESC_DTYPE)),
              ("icmp6", *icmp6_frames(31, 2000))]
     um, ds, _ = xdpgpu.pool_generate(300000, xdpgpu.POOL_IMIX, 64, 0x5EED0003)
     cases.append(("imix", um, ds))
+    um, ds, _ = xdpgpu.pool_generate(200000, xdpgpu.POOL_UDP4, 128, 0x5EED0042,
+                                     ppm_echo6=200000)
+    cases.append(("echo-pool", um, ds))
     for name, umem, descs in cases:
-        for flags, iv, fmt in ((0x5, 0, 2), (0x4, 7, 0), (0x7, 0x1234, 2)):
+        # the echo responder with the 16-byte tuple selects the IPv6 build too
+        for flags, iv, fmt in ((0x5, 0, 2), (0x4, 7, 0), (0x7, 0x1234, 2), (0x7, 0, 1),
+                               (0x6, 3, 0)):
             ou = umem.copy()
             ov, ores, otup, ost = oracle.process(ou, descs, flags, iv, fmt)
             v, res, tup, um2, st = run_dev(umem, descs, flags, iv, fmt, 64, tune)
