@@ -1104,6 +1104,12 @@ typedef uint32_t v4u_n __attribute__((ext_vector_type(4)));
 #define XDP_NAT64_WIN_AUX 0
 #endif
 constexpr int kWinAux = XDP_NAT64_WIN_AUX;
+/* the translated frame sectors' stores (build knob for A/B, bit 0
+ * ingress, bit 1 egress): plain or non-temporal.  Egress 1.510 vs 1.617 ms
+ * with non-temporal stores; ingress 0.974 vs 0.971 ms (one box) */
+#ifndef XDP_NAT64_FRAME_NT
+#define XDP_NAT64_FRAME_NT 2
+#endif
 constexpr int kCuBlockN = kCuWavesN * kWaveN;
 
 template <bool EG>
@@ -1299,9 +1305,16 @@ __global__ __launch_bounds__(kCuBlockN, 1) void xdp_nat64_fast_kernel(Nat64Args 
 			const int f = 16 * k + (lane >> 2);
 			const int c = lane & 3;
 			const uint64_t e = otab[f];
-			if (e != ~0ull)
-				*reinterpret_cast<uint4 *>(a.umem + e + 16 * c) =
-					obuf[4 * f + (c ^ ((f >> 2) & 3))];
+			if (e != ~0ull) {
+				const uint4 v = obuf[4 * f + (c ^ ((f >> 2) & 3))];
+				if constexpr (((XDP_NAT64_FRAME_NT >> (EG ? 1 : 0)) & 1) != 0) {
+					const v4u_n v4 = {v.x, v.y, v.z, v.w};
+					__builtin_nontemporal_store(
+						v4, reinterpret_cast<v4u_n *>(a.umem + e + 16 * c));
+				} else {
+					*reinterpret_cast<uint4 *>(a.umem + e + 16 * c) = v;
+				}
+			}
 		}
 		__builtin_amdgcn_wave_barrier();
 		if (active && !slow) {
