@@ -400,8 +400,122 @@ struct Plan {
 	int co;           /* extra 2-byte store (TCP checksum) or -1 */
 };
 
-/* nat64_handle_v6 (nat64_kern.c:741-873) */
-__device__ uint32_t handle_v6(const Row &R, uint32_t len, int l3,
+/* Opt-in XDPGPU_NAT64_F_ICMP_INNER (include/xdpgpu.h; not in the
+ * reference: the FIXMEs at nat64_kern.c:438 and :736).  The IPv6 header
+ * embedded in an ICMPv6 error at frame offset ii becomes h4i, built by the
+ * outer rules of nat64_handle_v6 (:830-850).  v6 is the outer header (its
+ * source maps to src4).  False: not translatable (the frame is dropped).
+ * Rare frames: byte reads through the row, past it from HBM. */
+__device__ bool inner_v6_to_v4(const Row &R, uint32_t len, int ii, uint32_t oplen,
+			       const uint8_t *v6, uint32_t src4, const Nat64Args &a,
+			       const Tables &T, uint8_t (&h4i)[20])
+{
+	if ((uint32_t)ii + 40 > len || oplen < 48 || (R.b(ii) >> 4) != 6)
+		return false;
+	const uint32_t nh = R.b(ii + 6);
+	if (nh == 0 || nh == 43 || nh == 44 || nh == 51 || nh == 60 || nh == 135)
+		return false;
+	int p4[4], pend;
+	if (!v4pos(a.cfg.v6_plen, p4, pend))
+		return false;
+	for (int k = 0; k < 16; k++) {
+		const uint32_t v = k < pend ? R.b(ii + 8 + k) : 0u;
+		if (v != a.cfg.v6_prefix[k])
+			return false;
+	}
+	bool same = true;
+	for (int k = 0; k < 16; k++)
+		same = same && R.b(ii + 24 + k) == v6[8 + k];
+	uint32_t d4 = src4;
+	if (!same) {
+		/* static state only: a dynamic entry is the error's own source */
+		if (T.dyn)
+			return false;
+		uint32_t w[4];
+		for (int k = 0; k < 4; k++)
+			w[k] = R.b(ii + 24 + 4 * k) | R.b(ii + 25 + 4 * k) << 8 |
+			       R.b(ii + 26 + 4 * k) << 16 | R.b(ii + 27 + 4 * k) << 24;
+		bool found;
+		d4 = lookup_v6(T, w, found);
+		if (!found)
+			return false;
+	}
+	h4i[0] = 0x45;
+	h4i[1] = (uint8_t)(((R.b(ii) & 0x0f) << 4) | (R.b(ii + 1) >> 4));
+	const uint32_t tot = R.be16(ii + 4) + 20;
+	h4i[2] = (uint8_t)(tot >> 8);
+	h4i[3] = (uint8_t)tot;
+	h4i[4] = h4i[5] = 0;
+	h4i[6] = 0x40;
+	h4i[7] = 0;
+	h4i[8] = (uint8_t)R.b(ii + 7);
+	h4i[9] = (uint8_t)(nh == 58 ? 1 : nh);
+	h4i[10] = h4i[11] = 0;
+	for (int k = 0; k < 4; k++)
+		h4i[12 + k] = (uint8_t)R.b(ii + 8 + p4[k]);
+	h4i[16] = (uint8_t)(d4 >> 24);
+	h4i[17] = (uint8_t)(d4 >> 16);
+	h4i[18] = (uint8_t)(d4 >> 8);
+	h4i[19] = (uint8_t)d4;
+	uint32_t s = 0;
+	for (int k = 0; k < 20; k += 2)
+		s += h4i[k] | (h4i[k + 1] << 8);
+	s = (s & 0xffff) + (s >> 16);
+	s = (s & 0xffff) + (s >> 16);
+	s = ~s & 0xffff;
+	h4i[10] = (uint8_t)s;
+	h4i[11] = (uint8_t)(s >> 8);
+	return true;
+}
+
+/* The IPv4 header (IHL ihl) embedded in an ICMPv4 error at ii becomes h6i,
+ * by the outer rules of nat64_handle_v4 (:497-519). */
+__device__ bool inner_v4_to_v6(const Row &R, uint32_t len, int ii, uint32_t otot,
+			       const Nat64Args &a, const Tables &T, uint8_t (&h6i)[40],
+			       uint32_t &ihl)
+{
+	if ((uint32_t)ii + 20 > len || (R.b(ii) >> 4) != 4)
+		return false;
+	ihl = (R.b(ii) & 0xf) * 4;
+	if (ihl < 20 || (uint32_t)ii + ihl > len || otot < 28 + ihl)
+		return false;
+	if (R.be16(ii + 6) & ~0x4000u)
+		return false;
+	uint32_t w[4];
+	if (!lookup_v4(T, R.be32(ii + 12), w))
+		return false;
+	int p4[4], pend;
+	if (!v4pos(a.cfg.v6_plen, p4, pend))
+		return false;
+	for (int k = 0; k < 40; k++)
+		h6i[k] = 0;
+	const int keep = a.cfg.v6_plen == 64 ? 8 : pend;
+	for (int k = 0; k < keep; k++)
+		h6i[24 + k] = a.cfg.v6_prefix[k];
+	for (int k = 0; k < 4; k++)
+		h6i[24 + p4[k]] = (uint8_t)R.b(ii + 16 + k);
+	for (int k = 0; k < 4; k++) {
+		h6i[8 + 4 * k] = (uint8_t)w[k];
+		h6i[9 + 4 * k] = (uint8_t)(w[k] >> 8);
+		h6i[10 + 4 * k] = (uint8_t)(w[k] >> 16);
+		h6i[11 + 4 * k] = (uint8_t)(w[k] >> 24);
+	}
+	const uint32_t tos = R.b(ii + 1), proto = R.b(ii + 9);
+	h6i[0] = (uint8_t)(6 << 4 | ((tos & 0x70) >> 4));
+	h6i[1] = (uint8_t)(tos << 4);
+	const uint32_t pl = (R.be16(ii + 2) - ihl) & 0xffff;
+	h6i[4] = (uint8_t)(pl >> 8);
+	h6i[5] = (uint8_t)pl;
+	h6i[6] = (uint8_t)(proto == 1 ? 58 : proto);
+	h6i[7] = (uint8_t)R.b(ii + 8);
+	return true;
+}
+
+/* nat64_handle_v6 (nat64_kern.c:741-873); INNER: the opt-in ICMP-error
+ * inner header (its own instantiation, so the reference build keeps its
+ * registers) */
+template <bool INNER>
+__device__ uint32_t handle_v6(const Row &R, uint32_t len, int l3, uint64_t eff,
 			      const Nat64Args &a, const Tables &T, Plan &P,
 			      int64_t &shift, uint32_t ovv, uint4 &srcw)
 {
@@ -504,13 +618,29 @@ __device__ uint32_t handle_v6(const Row &R, uint32_t len, int l3,
 	const int l4 = l3 + 40;
 	P.co = -1;
 	int l4_end = l4;            /* rewritten L4 bytes [l4, l4_end) */
+	bool inner = false;
+	uint8_t h4i[20];
 	if (nexthdr == 58) {
 		if ((uint32_t)l4 + 8 > len || l4 + 8 > kWinEnd)
+			return XDPGPU_TC_ACT_SHOT;
+		const uint32_t t0 = R.b(l4);
+		inner = INNER && t0 >= 1 && t0 <= 4;
+		if (inner && !inner_v6_to_v4(R, len, l4 + 8, (uint32_t)v6[4] << 8 | v6[5], v6,
+					     src, a, T, h4i))
 			return XDPGPU_TC_ACT_SHOT;
 		if (!rewrite_icmpv6(R, l4, v6))
 			return XDPGPU_TC_ACT_SHOT;
 		h4[9] = 1;
 		l4_end = l4 + 8;
+		if (inner) {
+			/* 40 header bytes out of the ICMP message, 20 in */
+			uint32_t to = 0;
+			for (int k = 0; k < 20; k += 2)
+				to += h4i[k] | (h4i[k + 1] << 8);
+			row_csum(R, l4 + 2, diff_mod(R.words(l4 + 8, 40), mod_ffff(to)), false);
+			h4[2] = v6[4];
+			h4[3] = v6[5];
+		}
 	} else if (nexthdr == 6 || nexthdr == 17) {
 		const int co = l4 + (nexthdr == 6 ? 16 : 6);
 		if ((uint32_t)co + 2 <= len && co + 2 <= kWinEnd) {
@@ -535,6 +665,24 @@ __device__ uint32_t handle_v6(const Row &R, uint32_t len, int l3,
 	s = ~s & 0xffff;
 	h4[10] = (uint8_t)s;
 	h4[11] = (uint8_t)(s >> 8);
+	if (inner) {
+		/* [L2][IPv4][ICMP][inner IPv4] end where the inner IPv6 header
+		 * did: written straight to HBM from the row and registers (the
+		 * frame starts 40 bytes later); nothing left for the row's
+		 * write-back */
+		uint8_t *g = a.umem + eff + 40;
+		for (int k = 0; k < 20; k++)
+			g[l3 + 28 + k] = h4i[k];
+		for (int k = 0; k < 8; k++)
+			g[l3 + 20 + k] = (uint8_t)R.b(l4 + k);
+		for (int k = 0; k < 20; k++)
+			g[l3 + k] = h4[k];
+		for (int k = 0; k < l3; k++)
+			g[k] = k == 12 ? 0x08 : k == 13 ? 0x00 : (uint8_t)R.b(k);
+		P.lo = P.hi = 0;
+		shift = 40;
+		return XDPGPU_TC_ACT_REDIRECT;
+	}
 	/* the L2 header moves 20 bytes forward (back to front: l3 may exceed
 	 * 20), h_proto = 0x0800, then the IPv4 header */
 	for (int k = l3 - 1; k >= 0; k--)
@@ -550,6 +698,7 @@ __device__ uint32_t handle_v6(const Row &R, uint32_t len, int l3,
 }
 
 /* nat64_handle_v4 (nat64_kern.c:443-541) */
+template <bool INNER>
 __device__ uint32_t handle_v4(const Row &R, uint32_t len, int l3, uint64_t eff,
 			      const Nat64Args &a, const Tables &T, Plan &P,
 			      int64_t &shift)
@@ -601,10 +750,47 @@ __device__ uint32_t handle_v4(const Row &R, uint32_t len, int l3, uint64_t eff,
 	if (proto == 1) {
 		if ((uint32_t)l4 + 8 > len || l4 + 8 > kWinEnd)
 			return XDPGPU_TC_ACT_SHOT;
+		const uint32_t t0 = R.b(l4);
+		const bool inner = INNER && (t0 == 3 || t0 == 11 || t0 == 12);
+		uint8_t h6i[40];
+		uint32_t ihl_i = 0, grow = 0;
+		if (inner) {
+			if (!inner_v4_to_v6(R, len, l4 + 8, R.be16(l3 + 2), a, T, h6i, ihl_i))
+				return XDPGPU_TC_ACT_SHOT;
+			grow = 40 - ihl_i;
+			if (eff < 20 + grow)
+				return XDPGPU_TC_ACT_SHOT;
+			/* the pseudo header's length is the new payload_len */
+			const uint32_t pl2 = (pl + grow) & 0xffff;
+			v6[4] = (uint8_t)(pl2 >> 8);
+			v6[5] = (uint8_t)pl2;
+		}
 		if (!rewrite_icmp(R, l4, v6))
 			return XDPGPU_TC_ACT_SHOT;
 		v6[6] = 58;
 		l4_end = l4 + 8;
+		if (inner) {
+			uint32_t to = 0;
+			for (int k = 0; k < 40; k += 2)
+				to += h6i[k] | (h6i[k + 1] << 8);
+			row_csum(R, l4 + 2, diff_mod(R.words(l4 + 8, (int)ihl_i), mod_ffff(to)),
+				 false);
+			/* [L2][IPv6][ICMPv6][inner IPv6] end where the inner
+			 * IPv4 header did: the frame starts 20 + grow earlier */
+			const int sh = 20 + (int)grow;
+			uint8_t *g = a.umem + eff - sh;
+			for (int k = 0; k < l3; k++)
+				g[k] = k == 12 ? 0x86 : k == 13 ? 0xDD : (uint8_t)R.b(k);
+			for (int k = 0; k < 40; k++)
+				g[l3 + k] = v6[k];
+			for (int k = 0; k < 8; k++)
+				g[l3 + 40 + k] = (uint8_t)R.b(l4 + k);
+			for (int k = 0; k < 40; k++)
+				g[l3 + 48 + k] = h6i[k];
+			P.lo = P.hi = 0;
+			shift = -sh;
+			return XDPGPU_TC_ACT_REDIRECT;
+		}
 	} else if (proto == 6 || proto == 17) {
 		const int co = l4 + (proto == 6 ? 16 : 6);
 		if ((uint32_t)co + 2 <= len && co + 2 <= kWinEnd) {
@@ -636,6 +822,7 @@ __device__ uint32_t handle_v4(const Row &R, uint32_t len, int l3, uint64_t eff,
 
 } // namespace
 
+template <bool INNER>
 __global__ __launch_bounds__(kBlockN) void xdp_nat64_kernel(Nat64Args a)
 {
 	__shared__ uint32_t rows_all[kWavesN * kWaveN * kRowDw];
@@ -726,9 +913,9 @@ __global__ __launch_bounds__(kBlockN) void xdp_nat64_kernel(Nat64Args a)
 				l3 += 4;
 			}
 			if (a.cfg.direction == XDPGPU_NAT64_EGRESS && proto == 0x0800)
-				act = handle_v4(R, len, l3, eff, a, T, P, shift);
+				act = handle_v4<INNER>(R, len, l3, eff, a, T, P, shift);
 			else if (a.cfg.direction == XDPGPU_NAT64_INGRESS && proto == 0x86DD)
-				act = handle_v6(R, len, l3, a, T, P, shift, ovv, srcw);
+				act = handle_v6<INNER>(R, len, l3, eff, a, T, P, shift, ovv, srcw);
 		}
 		if (a.dyn && !a.ov)
 			miss_append(a, active && act == XDPGPU_NAT64_NO_STATE, (uint32_t)i, srcw,
@@ -1369,20 +1556,38 @@ uint32_t nat64_grid(uint32_t n, uint32_t max_blocks)
 	return blocks ? (uint32_t)blocks : 1u;
 }
 
+/* the general kernel: the reference's translation, or with
+ * XDPGPU_NAT64_F_ICMP_INNER its own instantiation; blocks 0 = as many as
+ * are resident */
+static hipError_t launch_slow(const Nat64Args &a, uint32_t blocks, uint32_t max_blocks,
+			      uint32_t need, hipStream_t stream)
+{
+	const bool inner = a.cfg.flags & XDPGPU_NAT64_F_ICMP_INNER;
+	if (!blocks) {
+		blocks = inner ? resident_n<xdp_nat64_kernel<true>>()
+			       : resident_n<xdp_nat64_kernel<false>>();
+		if (blocks > max_blocks)
+			blocks = max_blocks;
+		if (blocks > need)
+			blocks = need ? need : 1u;
+	}
+	if (inner)
+		hipLaunchKernelGGL(xdp_nat64_kernel<true>, dim3(blocks), dim3(kBlockN), 0,
+				   stream, a);
+	else
+		hipLaunchKernelGGL(xdp_nat64_kernel<false>, dim3(blocks), dim3(kBlockN), 0,
+				   stream, a);
+	return hipGetLastError();
+}
+
 hipError_t launch_nat64(const Nat64Args &a0, uint32_t max_blocks, hipStream_t stream)
 {
 	Nat64Args a = a0;
 	if (a.ov) {
 		/* the commit pass: the general kernel over the listed frames
 		 * (xlist, one region of xregion entries, its count in xcount) */
-		uint32_t sb = resident_n<xdp_nat64_kernel>();
-		if (sb > max_blocks)
-			sb = max_blocks;
-		const uint32_t need = (a.xregion / kWaveN + kWavesN - 1) / kWavesN;
-		if (sb > need)
-			sb = need ? need : 1u;
-		hipLaunchKernelGGL(xdp_nat64_kernel, dim3(sb), dim3(kBlockN), 0, stream, a);
-		return hipGetLastError();
+		return launch_slow(a, 0, max_blocks,
+				   (a.xregion / kWaveN + kWavesN - 1) / kWavesN, stream);
 	}
 	if (a.fast) {
 		const uint32_t blocks = nat64_grid(a.n, max_blocks);
@@ -1413,11 +1618,7 @@ hipError_t launch_nat64(const Nat64Args &a0, uint32_t max_blocks, hipStream_t st
 		hipError_t e = hipGetLastError();
 		if (e != hipSuccess)
 			return e;
-		uint32_t sb = resident_n<xdp_nat64_kernel>();
-		if (sb > max_blocks)
-			sb = max_blocks;
-		hipLaunchKernelGGL(xdp_nat64_kernel, dim3(sb), dim3(kBlockN), 0, stream, a);
-		return hipGetLastError();
+		return launch_slow(a, 0, max_blocks, ~0u, stream);
 	}
 	a.xlist = nullptr;
 	uint64_t tiles = ((uint64_t)a.n + kWaveN - 1) / kWaveN;
@@ -1426,9 +1627,7 @@ hipError_t launch_nat64(const Nat64Args &a0, uint32_t max_blocks, hipStream_t st
 		blocks = max_blocks;
 	if (!blocks)
 		return hipSuccess;
-	hipLaunchKernelGGL(xdp_nat64_kernel, dim3((uint32_t)blocks), dim3(kBlockN), 0,
-			   stream, a);
-	return hipGetLastError();
+	return launch_slow(a, (uint32_t)blocks, max_blocks, ~0u, stream);
 }
 
 /* The host's dynamic-state commit: changed slots and their buckets' meta

@@ -406,6 +406,201 @@ __device__ __forceinline__ uint32_t sp_frame(const Frame &F, uint32_t &len, uint
 		   : handle_ack(F, ip, v6, tcp, cfg);
 }
 
+/* ------------------------------------------------------------------ */
+/* The common SYN in registers: untagged IPv4 with a 20-byte header, a TCP
+ * SYN to an allowed port with at most 20 option bytes, the growth inside
+ * the row.  The row's first 96 bytes are taken into registers (W), the
+ * checks, checksums, cookie and SYN-ACK of syncookie_handle_syn
+ * (:577-715) are computed at fixed byte positions, and the new bytes go
+ * back to the row as whole dwords; the option walk (tscookie_tcpopt_parse)
+ * stays on the row.  Bit-exact with handle_syn on these frames, in a few
+ * hundred instructions instead of a byte-wise pass over the row. */
+constexpr int kW = 24;                    /* row dwords in registers */
+
+__device__ __forceinline__ uint32_t wb8(const uint32_t (&W)[kW], int i)
+{
+	return (W[i >> 2] >> (8 * (i & 3))) & 0xff;
+}
+
+/* the LE word at byte i (i even) */
+__device__ __forceinline__ uint32_t wle(const uint32_t (&W)[kW], int i)
+{
+	return (i & 3) ? __builtin_amdgcn_alignbyte(W[(i >> 2) + 1], W[i >> 2], i & 3)
+		       : W[i >> 2];
+}
+
+__device__ __forceinline__ uint32_t wbe16(const uint32_t (&W)[kW], int i)
+{
+	return wb8(W, i) << 8 | wb8(W, i + 1);
+}
+
+__device__ __forceinline__ void wput(uint32_t (&O)[kW], int i, uint32_t v)
+{
+	const int s = 8 * (i & 3);
+	O[i >> 2] = (O[i >> 2] & ~(0xffu << s)) | ((v & 0xff) << s);
+}
+
+__device__ __forceinline__ void wput_be16(uint32_t (&O)[kW], int i, uint32_t v)
+{
+	wput(O, i, v >> 8);
+	wput(O, i + 1, v);
+}
+
+__device__ __forceinline__ void wput_be32(uint32_t (&O)[kW], int i, uint32_t v)
+{
+	wput_be16(O, i, v >> 16);
+	wput_be16(O, i + 2, v & 0xffff);
+}
+
+/* is this lane's frame the common SYN (sp_frame's path to handle_syn
+ * with tcp = 34 and nothing past the row)?  room: as sp_frame's */
+__device__ __forceinline__ bool syn_fast_shape(const uint32_t (&W)[kW], uint32_t len0,
+					       uint64_t room, const xdpgpu_synproxy_cfg &cfg)
+{
+	const uint32_t tcp_len = (wb8(W, 46) >> 4) * 4;
+	bool allowed = false, live = true;
+	const uint32_t port = wbe16(W, 36);
+#pragma unroll
+	for (int i = 0; i < 8; i++) {
+		const uint32_t pv = cfg.ports[i];
+		live = live && pv != 0;
+		allowed = allowed || (live && pv == port);
+	}
+	const uint32_t fl = wb8(W, 47);
+	return len0 >= 54 && wbe16(W, 12) == 0x0800 && wb8(W, 14) == 0x45 &&
+	       wb8(W, 23) == 6 && tcp_len >= 20 && tcp_len <= 40 &&
+	       len0 >= 34 + tcp_len && len0 + 60 - tcp_len <= (uint32_t)kRow &&
+	       (wbe16(W, 20) & 0x7fff) == 0x4000 && allowed && (fl & 0x12) == 0x02 &&
+	       60 - tcp_len <= room;
+}
+
+/* handle_syn on the common shape; len in: the grown length */
+__device__ __forceinline__ uint32_t handle_syn_fast(const Frame &F, uint32_t (&W)[kW],
+						    uint32_t &len,
+						    const xdpgpu_synproxy_cfg &cfg,
+						    bool &synack)
+{
+	const uint32_t tcp_len = (wb8(W, 46) >> 4) * 4;
+	const uint32_t fl = wb8(W, 47);
+	if (fl & 0x05)
+		return SP_DROP;
+	uint64_t s = 0;
+#pragma unroll
+	for (int k = 0; k < 5; k++)
+		s += wle(W, 14 + 4 * k);
+	if (fold(s) != 0)
+		return SP_DROP;
+	const uint32_t sa = wle(W, 26), da = wle(W, 30);
+	s = (uint64_t)sa + da + ((uint64_t)(6 + tcp_len) << 8);
+#pragma unroll
+	for (int k = 0; k < 10; k++)
+		s += 4 * k < (int)tcp_len ? wle(W, 34 + 4 * k) : 0u;
+	if (fold(s) != 0)
+		return SP_DROP;
+	const uint32_t count = (uint32_t)(cfg.now_ns / 60000000000ull);
+	const uint32_t seq = (uint32_t)wbe16(W, 38) << 16 | wbe16(W, 40);
+	uint32_t cookie;
+	{
+		/* cookie_hash over (saddr, daddr, ports): jhash2(w, 9, key +
+		 * count) with w[0] = saddr, w[4] = daddr, w[8] = the ports */
+		uint32_t a = 0xdeadbeefu + (9u << 2) + cfg.cookie_key + count, b = a, c = a;
+		a += sa;
+		JH_MIX(a, b, c);
+		b += da;
+		JH_MIX(a, b, c);
+		c += wbe16(W, 34) << 16 | wbe16(W, 36);
+		JH_FINAL(a, b, c);
+		cookie = c + seq;
+	}
+	/* tscookie_init (:274-308), on the row */
+	Opt oc = {34 + 20, len, 0xf, 0, 0, 0};
+	for (int i = 0; i < 42; i++)
+		if (opt_parse(oc, F))
+			break;
+	uint32_t tsval = 0;
+	if (oc.ts) {
+		tsval = (uint32_t)(cfg.now_ns / 1000000ull) & ~0x3fu;
+		tsval |= oc.wscale & 0xf;
+		if (oc.sack)
+			tsval |= 1u << 4;
+		if ((fl & 0x40) && (fl & 0x80))
+			tsval |= 1u << 5;
+	}
+	uint32_t mss, wscale, ttl;
+	if (cfg.values) {
+		mss = (uint32_t)cfg.values & 0xffff;
+		wscale = (uint32_t)(cfg.values >> 16) & 0xf;
+		ttl = (uint32_t)(cfg.values >> 24) & 0xff;
+	} else {
+		mss = 1460;
+		wscale = 7;
+		ttl = 64;
+	}
+	const bool ws = oc.ts && (tsval & 0xf) != 0xf;
+	const uint32_t new_len = oc.ts ? (ws ? 40u : 36u) : 24u;
+
+	/* tcpv4_gen_synack (:533-575), tcp_gen_synack (:512-531),
+	 * tcp_mkoptions (:480-510) */
+	uint32_t O[kW];
+#pragma unroll
+	for (int k = 0; k < kW; k++)
+		O[k] = W[k];
+#pragma unroll
+	for (int i = 0; i < 6; i++) {
+		wput(O, i, wb8(W, 6 + i));
+		wput(O, 6 + i, wb8(W, i));
+	}
+	wput(O, 15, 0);
+	wput_be16(O, 16, 20 + new_len);
+	wput_be16(O, 18, 0);
+	wput(O, 22, ttl);
+	wput_be16(O, 24, 0);
+	O[6] = (O[6] & 0x0000ffffu) | (da << 16);          /* bytes 26-29 */
+	O[7] = (da >> 16) | (sa << 16);                     /* bytes 30-33 */
+	O[8] = (O[8] & 0xffff0000u) | (sa >> 16);
+	wput_be16(O, 34, wbe16(W, 36));
+	wput_be16(O, 36, wbe16(W, 34));
+	wput_be32(O, 38, cookie);
+	wput_be32(O, 42, seq + 1);
+	wput(O, 46, (new_len / 4) << 4);
+	wput(O, 47, 0x12 | ((oc.ts && (tsval & (1u << 5))) ? 0x40 : 0));
+	wput_be32(O, 48, 0);                                /* window, check */
+	wput_be16(O, 52, 0);
+	wput_be32(O, 54, 2u << 24 | 4u << 16 | (mss & 0xffff));
+	if (oc.ts) {
+		wput_be32(O, 58, (tsval & (1u << 4)) ? (4u << 24 | 2u << 16 | 8u << 8 | 10u)
+						     : (1u << 24 | 1u << 16 | 8u << 8 | 10u));
+		wput_be32(O, 62, tsval);
+		wput(O, 66, oc.tsecr);
+		wput(O, 67, oc.tsecr >> 8);
+		wput(O, 68, oc.tsecr >> 16);
+		wput(O, 69, oc.tsecr >> 24);
+		if (ws)
+			wput_be32(O, 70, 1u << 24 | 3u << 16 | 3u << 8 | wscale);
+	}
+	/* checksums (:679-704), stored as computed (LE u16) */
+	s = (uint64_t)sa + da + ((uint64_t)(6 + new_len) << 8);
+#pragma unroll
+	for (int k = 0; k < 10; k++)
+		s += 4 * k < (int)new_len ? wle(O, 34 + 4 * k) : 0u;
+	const uint32_t c = fold(s);
+	wput(O, 50, c);
+	wput(O, 51, c >> 8);
+	s = 0;
+#pragma unroll
+	for (int k = 0; k < 5; k++)
+		s += wle(O, 14 + 4 * k);
+	const uint32_t h = fold(s);
+	wput(O, 24, h);
+	wput(O, 25, h >> 8);
+#pragma unroll
+	for (int k = 0; k < kW; k++)
+		W[k] = O[k];
+	len = 34 + new_len;
+	synack = true;
+	return SP_TX;
+}
+
 /* one tile of kBlockS frames (one wave) from frame t0 on; true: this
  * lane's frame was answered with a SYN-ACK */
 __device__ __forceinline__ bool sp_tile(uint8_t *umem, uint64_t usize, const xdpgpu_desc *desc,
@@ -467,7 +662,24 @@ __device__ __forceinline__ bool sp_tile(uint8_t *umem, uint64_t usize, const xdp
 			room = cfg.tailroom;
 		uint32_t grow = 0;
 		const uint32_t len0 = len;
-		const uint32_t act = sp_frame(F, len, room, cfg, synack, grow);
+		uint32_t act;
+		uint32_t W[kW];
+#pragma unroll
+		for (int k = 0; k < kW; k++)
+			W[k] = rw[k];
+		if (coop && syn_fast_shape(W, len0, room, cfg)) {
+			/* sp_frame's growth (:389-404), then handle_syn */
+			grow = 60 - (wb8(W, 46) >> 4) * 4;
+			len += grow;
+			act = handle_syn_fast(F, W, len, cfg, synack);
+			if (act == SP_TX) {
+#pragma unroll
+				for (int k = 0; k < kW; k++)
+					rw[k] = W[k];
+			}
+		} else {
+			act = sp_frame(F, len, room, cfg, synack, grow);
+		}
 		/* the bytes to write back: the SYN-ACK and the rest of the growth
 		 * (zeros), or the growth of a frame passed or dropped after it */
 		ws = act == SP_TX ? 0u : len0;

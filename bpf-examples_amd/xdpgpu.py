@@ -58,6 +58,7 @@ POOL_NAT64, POOL_NAT64_V4 = 4, 5
 NAT64_INGRESS, NAT64_EGRESS = 0, 1
 TC_ACT_OK, TC_ACT_SHOT, TC_ACT_REDIRECT = 0, 2, 7
 NAT64_NO_STATE = 0x80
+NAT64_F_ICMP_INNER = 0x1   # opt-in: translate the header inside ICMP errors
 NAT64_MAP_DTYPE = np.dtype([("v6", "u1", (16,)), ("v4", "<u4"), ("rsvd", "<u4")])
 NAT64_ENTRY_DTYPE = np.dtype([("v6", "u1", (16,)), ("v4", "<u4"), ("static_conf", "<u4"),
                               ("last_seen", "<u8")])
@@ -129,7 +130,8 @@ class Nat64Cfg(C.Structure):
     _fields_ = [("v6_prefix", C.c_uint8 * 16), ("v6_plen", C.c_uint32),
                 ("v4_prefix", C.c_uint32), ("v4_mask", C.c_uint32),
                 ("allow_plen", C.c_uint32), ("allow_prefix", C.c_uint8 * 16),
-                ("direction", C.c_uint32), ("rsvd", C.c_uint32 * 3)]
+                ("direction", C.c_uint32), ("flags", C.c_uint32),
+                ("rsvd", C.c_uint32 * 2)]
 
 
 class Nat64Dyn(C.Structure):

@@ -335,8 +335,31 @@ struct xdpgpu_nat64_cfg {
 	uint32_t allow_plen;       /* allowed_v6_src LPM entry, 0: none      */
 	uint8_t  allow_prefix[16];
 	uint32_t direction;        /* XDPGPU_NAT64_*                         */
-	uint32_t rsvd[3];
+	uint32_t flags;            /* XDPGPU_NAT64_F_*, 0: the reference     */
+	uint32_t rsvd[2];
 };
+
+/* Opt-in extension (not in the reference, whose rewrite_icmp /
+ * rewrite_icmpv6 leave the embedded header alone: the FIXMEs at
+ * nat64_kern.c:438 and :736).  With this flag an ICMP error (ICMPv6 types
+ * 1-4, ICMPv4 types 3, 11, 12) also has its embedded IP header translated,
+ * RFC 7915 sections 4.3/5.3, with the same field rules the outer header
+ * gets from nat64_handle_v6/_v4:
+ *   ingress: the embedded IPv6 header (no extension header; its source
+ *     inside the pref64, its destination the error's own source or, with
+ *     static state, a v6_state_map entry) becomes a 20-byte IPv4 header;
+ *     the frame starts 40 bytes later and the outer tot_len is the IPv6
+ *     payload_len.
+ *   egress: the embedded IPv4 header (any IHL, not a fragment; its source
+ *     in v4_reversemap) becomes a 40-byte IPv6 header; the frame starts
+ *     60 - IHL bytes earlier (40 for IHL 20: that much UMEM headroom) and
+ *     the outer payload_len grows by 40 - IHL.
+ * The ICMP checksum is updated incrementally for the swapped header (a
+ * frame that arrived with a valid checksum leaves with one); the embedded
+ * transport header and its checksum are left as they are (RFC 7915 allows
+ * it).  An error whose embedded header cannot be translated is
+ * TC_ACT_SHOT. */
+#define XDPGPU_NAT64_F_ICMP_INNER 0x1
 
 /* A static v6_state_map entry (struct v6_addr_state with static_conf,
  * nat64.h:15-19); v4_reversemap is its inverse. */
@@ -369,7 +392,8 @@ int xdpgpu_nat64_dev(struct xdpgpu_ctx *ctx, void *d_umem, uint64_t umem_size,
  * v4 pool (config.next_addr) while prefix + next_addr < (prefix | ~mask) - 1,
  * then reclaimed addresses (reclaim_v4_addr, :563-574: the reclaimed_addrs
  * queue, else one entry whose last_seen is older than now - timeout_ns and
- * not static, found in insertion order), within num_addr = (prefix | ~mask)
+ * not static, found in insertion order: which timed-out entry is taken is
+ * implementation-defined, the kernel walks its hash order), within num_addr = (prefix | ~mask)
  * - prefix - 2 entries (nat64.c:396-401); a hit refreshes last_seen
  * (:821-823).  A failed allocation is TC_ACT_SHOT.  Frames are taken in
  * descriptor order, one batch at one instant: `now_ns`, or CLOCK_MONOTONIC

@@ -588,6 +588,82 @@ static void l4_addr_update(uint8_t *c, int proto, const uint8_t *from, int fn,
 	l4_csum_replace(c, csum_diff_mod(from, fn, to, tn), proto == 17);
 }
 
+/* Opt-in (XDPGPU_NAT64_F_ICMP_INNER, include/xdpgpu.h): the header
+ * embedded in an ICMPv6 error at p + ii, as a new IPv4 header h4i (the
+ * outer construction of nat64_handle_v6, nat64_kern.c:830-850).  outer_src
+ * is the error's own IPv6 source, src4 its IPv4 address.  0 ok, -1 not
+ * translatable.  Not in the reference (FIXME at nat64_kern.c:736). */
+static int inner_v6_to_v4(const uint8_t *p, uint32_t len, uint32_t ii, uint32_t outer_plen,
+			  const uint8_t *outer_src, uint32_t src4,
+			  const struct xdpgpu_nat64_cfg *cfg, const struct tabs *T,
+			  uint8_t h4i[20])
+{
+	if (ii + 40 > len || outer_plen < 48 || (p[ii] >> 4) != 6)
+		return -1;
+	const uint8_t nh = p[ii + 6];
+	if (nh == 0 || nh == 43 || nh == 44 || nh == 51 || nh == 60 || nh == 135)
+		return -1;                 /* an extension header: not handled */
+	uint8_t a4[4], pref[16];
+	if (!oracle_v6addr_to_v4(p + ii + 8, (int)cfg->v6_plen, a4, pref) ||
+	    memcmp(pref, cfg->v6_prefix, 16))
+		return -1;
+	uint32_t d4;
+	if (!memcmp(p + ii + 24, outer_src, 16)) {
+		d4 = src4;
+	} else {
+		/* static state only: a dynamic entry is the error's own source */
+		const struct xdpgpu_nat64_map *m = T->st ? NULL :
+			find_v6(T->map, T->nmap, p + ii + 24);
+		if (!m)
+			return -1;
+		d4 = m->v4;
+	}
+	memset(h4i, 0, 20);
+	h4i[0] = 0x45;
+	h4i[1] = (uint8_t)(((p[ii] & 0x0f) << 4) | (p[ii + 1] >> 4));
+	put_be16(h4i + 2, (uint16_t)(be16(p + ii + 4) + 20));
+	put_be16(h4i + 6, 0x4000);
+	h4i[8] = p[ii + 7];
+	h4i[9] = nh == 58 ? 1 : nh;
+	memcpy(h4i + 12, a4, 4);
+	put_be32(h4i + 16, d4);
+	uint64_t s = 0;
+	for (int i = 0; i < 20; i += 2)
+		s += le16(h4i + i);
+	while (s >> 16)
+		s = (s & 0xffff) + (s >> 16);
+	put_le16(h4i + 10, (uint16_t)~s);
+	return 0;
+}
+
+/* The same for an ICMPv4 error (FIXME at nat64_kern.c:438): the embedded
+ * IPv4 header at p + ii (IHL *ihl) as a new IPv6 header h6i (the outer
+ * construction of nat64_handle_v4, :497-519). */
+static int inner_v4_to_v6(const uint8_t *p, uint32_t len, uint32_t ii, uint32_t outer_tot,
+			  const struct xdpgpu_nat64_cfg *cfg, const struct tabs *T,
+			  uint8_t h6i[40], uint32_t *ihl)
+{
+	if (ii + 20 > len || (p[ii] >> 4) != 4)
+		return -1;
+	*ihl = (p[ii] & 0xf) * 4;
+	if (*ihl < 20 || ii + *ihl > len || outer_tot < 28 + *ihl)
+		return -1;
+	if (be16(p + ii + 6) & ~0x4000u)
+		return -1;                 /* a fragment: not handled */
+	memset(h6i, 0, 40);
+	if (!tab_v4(T, be32(p + ii + 12), h6i + 8))
+		return -1;
+	if (!oracle_v4addr_to_v6(p + ii + 16, h6i + 24, cfg->v6_prefix, (int)cfg->v6_plen))
+		return -1;
+	const uint8_t tos = p[ii + 1], proto = p[ii + 9];
+	h6i[0] = (uint8_t)(6 << 4 | ((tos & 0x70) >> 4));
+	h6i[1] = (uint8_t)(tos << 4);
+	put_be16(h6i + 4, (uint16_t)(be16(p + ii + 2) - *ihl));
+	h6i[6] = proto == 1 ? 58 : proto;
+	h6i[7] = p[ii + 8];
+	return 0;
+}
+
 /* nat64_handle_v6 (nat64_kern.c:741-873) on one frame */
 static int handle_v6(uint8_t *umem, uint64_t eff, uint32_t len, uint32_t l3,
 		     const struct xdpgpu_nat64_cfg *cfg, const struct tabs *T,
@@ -633,9 +709,15 @@ static int handle_v6(uint8_t *umem, uint64_t eff, uint32_t len, uint32_t l3,
 	memcpy(h4 + 16, a4, 4);
 
 	const uint32_t l4 = l3 + 40;
+	int inner = 0;
+	uint8_t h4i[20];
 	switch (nexthdr) {
 	case 58:
 		if (l4 + 8 > len)
+			return XDPGPU_TC_ACT_SHOT;
+		inner = (cfg->flags & XDPGPU_NAT64_F_ICMP_INNER) && p[l4] >= 1 && p[l4] <= 4;
+		if (inner && inner_v6_to_v4(p, len, l4 + 8, be16(p + l3 + 4), p + l3 + 8, src4,
+					    cfg, T, h4i))
 			return XDPGPU_TC_ACT_SHOT;
 		{
 			uint8_t h6[40];
@@ -644,6 +726,12 @@ static int handle_v6(uint8_t *umem, uint64_t eff, uint32_t len, uint32_t l3,
 				return XDPGPU_TC_ACT_SHOT;
 		}
 		h4[9] = 1;
+		if (inner) {
+			/* 40 header bytes out, 20 in; the ICMPv4 message
+			 * is the IPv6 payload less 20 bytes */
+			l4_csum_replace(p + l4 + 2, csum_diff_mod(p + l4 + 8, 40, h4i, 20), 0);
+			put_be16(h4 + 2, be16(p + l3 + 4));
+		}
 		break;
 	case 6: case 17: {
 		const uint32_t co = l4 + (nexthdr == 6 ? 16 : 6);
@@ -663,6 +751,22 @@ static int handle_v6(uint8_t *umem, uint64_t eff, uint32_t len, uint32_t l3,
 		while (s >> 16)
 			s = (s & 0xffff) + (s >> 16);
 		put_le16(h4 + 10, (uint16_t)~s);
+	}
+	if (inner) {
+		/* [L2][IPv4][ICMP][inner IPv4] end where the inner IPv6
+		 * header did: the frame starts 40 bytes later */
+		uint8_t l2[22], icmp[8];
+		memcpy(l2, p, l3);
+		memcpy(icmp, p + l4, 8);
+		uint8_t *q = p + 40;
+		memcpy(q + l3 + 28, h4i, 20);
+		memcpy(q + l3 + 20, icmp, 8);
+		memcpy(q + l3, h4, 20);
+		memcpy(q, l2, l3);
+		q[12] = 0x08; q[13] = 0x00;
+		out->addr = eff + 40;
+		out->len = len - 40;
+		return XDPGPU_TC_ACT_REDIRECT;
 	}
 	/* bpf_skb_change_proto: 20 bytes fewer in front of the network
 	 * header; the L2 header moves, its h_proto becomes 0x0800 */
@@ -711,13 +815,46 @@ static int handle_v4(uint8_t *umem, uint64_t eff, uint32_t len, uint32_t l3,
 	if (eff < 20)
 		return XDPGPU_TC_ACT_SHOT;             /* no headroom to grow */
 	const uint32_t l4 = l3 + 20;
+	int inner = 0;
+	uint8_t h6i[40];
+	uint32_t ihl_i = 0, grow = 0;
 	switch (proto) {
 	case 1:
 		if (l4 + 8 > len)
 			return XDPGPU_TC_ACT_SHOT;
+		inner = (cfg->flags & XDPGPU_NAT64_F_ICMP_INNER) &&
+			(p[l4] == 3 || p[l4] == 11 || p[l4] == 12);
+		if (inner) {
+			if (inner_v4_to_v6(p, len, l4 + 8, be16(p + l3 + 2), cfg, T, h6i, &ihl_i))
+				return XDPGPU_TC_ACT_SHOT;
+			grow = 40 - ihl_i;
+			if (eff < 20 + grow)
+				return XDPGPU_TC_ACT_SHOT;     /* headroom */
+			/* the pseudo header's length is the new payload_len */
+			put_be16(h6 + 4, (uint16_t)(be16(h6 + 4) + grow));
+		}
 		if (rewrite_icmp(p + l4, h6))
 			return XDPGPU_TC_ACT_SHOT;
 		h6[6] = 58;
+		if (inner) {
+			l4_csum_replace(p + l4 + 2,
+					csum_diff_mod(p + l4 + 8, (int)ihl_i, h6i, 40), 0);
+			/* [L2][IPv6][ICMPv6][inner IPv6] end where the inner
+			 * IPv4 header did: the frame starts 20 + grow earlier */
+			const uint32_t sh = 20 + grow;
+			uint8_t l2[22], icmp[8];
+			memcpy(l2, p, l3);
+			memcpy(icmp, p + l4, 8);
+			uint8_t *q = p - sh;
+			memcpy(q, l2, l3);
+			q[12] = 0x86; q[13] = 0xDD;
+			memcpy(q + l3, h6, 40);
+			memcpy(q + l3 + 40, icmp, 8);
+			memcpy(q + l3 + 48, h6i, 40);
+			out->addr = eff - sh;
+			out->len = len + sh;
+			return XDPGPU_TC_ACT_REDIRECT;
+		}
 		break;
 	case 6: case 17: {
 		const uint32_t co = l4 + (proto == 6 ? 16 : 6);

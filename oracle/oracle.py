@@ -35,7 +35,8 @@ class Nat64Cfg(C.Structure):
     _fields_ = [("v6_prefix", C.c_uint8 * 16), ("v6_plen", C.c_uint32),
                 ("v4_prefix", C.c_uint32), ("v4_mask", C.c_uint32),
                 ("allow_plen", C.c_uint32), ("allow_prefix", C.c_uint8 * 16),
-                ("direction", C.c_uint32), ("rsvd", C.c_uint32 * 3)]
+                ("direction", C.c_uint32), ("flags", C.c_uint32),
+                ("rsvd", C.c_uint32 * 2)]
 
 
 class OStats(C.Structure):
