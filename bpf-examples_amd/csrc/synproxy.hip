@@ -11,9 +11,12 @@
  * frame's end as the zeros bpf_xdp_adjust_tail grows it with), and writes
  * back what changed: the SYN-ACK's headers (at most 14 + 40 + 40 bytes, all
  * in the row) or the zeroed growth of a frame the program grew and then
- * passed or dropped.  HBM-bound on the frame's first line and a few stores;
- * the byte-wise parse runs in LDS.  Semantics and what lies outside the
- * transform (conntrack, the kernel's cookie): include/xdpgpu.h.
+ * passed or dropped, as whole 16-byte chunks where the chunk lies in the
+ * frame's buffer (the unchanged bytes from the lane's staged copy).  The
+ * common SYN (untagged IPv4, 20-byte IP header, at most 20 option bytes)
+ * runs in registers (handle_syn_fast); everything else byte-wise on the
+ * row.  Semantics and what lies outside the transform (conntrack, the
+ * kernel's cookie): include/xdpgpu.h.
  */
 #include <hip/hip_runtime.h>
 
@@ -23,8 +26,41 @@
 namespace xdpgpu {
 namespace {
 
-constexpr int kRow = 144;                 /* staged bytes per frame */
+/* staged bytes per frame (build knob for A/B): every byte the program
+ * writes lies below 96 (an IPv6 SYN-ACK ends at 14 + 40 + 40); bytes past
+ * the row are read from the UMEM.  SYN proxy leg, 8 M SYNs at a 128-byte
+ * stride: 96 bytes 0.569 ms, 112 0.617, 128 0.640, 144 0.873 (with the
+ * staging copy of 144 bytes reading into the next frame's line) */
+#ifndef SP_ROW
+#define SP_ROW 96
+#endif
+constexpr int kRow = SP_ROW;
 constexpr int kRowDw = kRow / 4 + 1;      /* odd dword stride: no bank conflicts */
+constexpr int kChunks = kRow / 16;
+static_assert(kRow % 16 == 0 && kRow >= 96, "the row holds whole chunks, every write");
+/* the cooperative write-back (build knob for A/B): 0 = the changed bytes
+ * only (partial chunks by dwords and bytes), 1 = whole 16-byte chunks where
+ * the chunk lies in the frame's buffer (its length plus the tail room it
+ * may grow into), the unchanged bytes from the staged copy, 2 = also the
+ * rest of every 64-byte sector written, so that HBM sees whole sectors.
+ * SYN proxy leg (128-byte rows): 0.733 ms with 0, 0.637 with 1, 0.698
+ * with 2 */
+#ifndef SP_WB
+#define SP_WB 1
+#endif
+constexpr int kWb = SP_WB;
+/* cache policy (build knob for A/B): bit 0 the whole-chunk write-back
+ * stores, bit 1 the verdict and output descriptor stores non-temporal.
+ * No difference on the SYN proxy leg (0.560-0.570 ms either way) */
+#ifndef SP_NT
+#define SP_NT 0
+#endif
+/* 1: a grid of resident waves looping over the tiles, the next tile's
+ * descriptors loaded before this tile's work (build knob for A/B): 1.63 vs
+ * 0.57 ms with one tile per launched wave */
+#ifndef SP_PERSIST
+#define SP_PERSIST 0
+#endif
 constexpr int kBlockS = 64;      /* one wave: LDS rows bound the CU to 15 waves */
 
 enum { SP_ABORTED = 0, SP_DROP = 1, SP_PASS = 2, SP_TX = 3 };
@@ -601,9 +637,17 @@ __device__ __forceinline__ uint32_t handle_syn_fast(const Frame &F, uint32_t (&W
 	return SP_TX;
 }
 
-/* one tile of kBlockS frames (one wave) from frame t0 on; true: this
- * lane's frame was answered with a SYN-ACK */
-__device__ __forceinline__ bool sp_tile(uint8_t *umem, uint64_t usize, const xdpgpu_desc *desc,
+__device__ __forceinline__ void put_verdict(uint8_t *v, uint32_t act)
+{
+	if constexpr ((SP_NT & 2) != 0)
+		__builtin_nontemporal_store((uint8_t)act, v);
+	else
+		*v = (uint8_t)act;
+}
+
+/* one tile of kBlockS frames (one wave) from frame t0 on, dv this lane's
+ * descriptor; true: this lane's frame was answered with a SYN-ACK */
+__device__ __forceinline__ bool sp_tile(uint8_t *umem, uint64_t usize, uint4 dv,
 					uint32_t n, const xdpgpu_synproxy_cfg &cfg,
 					uint8_t *verdict, xdpgpu_desc *out, uint32_t *rows,
 					uint64_t *dtab_all, uint2 *wtab_all, uint64_t t0)
@@ -611,30 +655,34 @@ __device__ __forceinline__ bool sp_tile(uint8_t *umem, uint64_t usize, const xdp
 	const uint64_t i = t0 + threadIdx.x;
 	const bool active = i < n;
 	uint8_t *row = reinterpret_cast<uint8_t *>(rows + threadIdx.x * kRowDw);
-	const uint4 dv = active ? *reinterpret_cast<const uint4 *>(desc + i)
-				: make_uint4(0, 0, 0, 0);
 	const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
 	uint32_t len = dv.z;
 	const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
 	const bool valid = active && (uint64_t)len <= usize && eff <= usize - len;
 	bool synack = false;
 	uint32_t ws = 0, we = 0;   /* the byte range to write back (coop frames) */
+	uint32_t own = 0;          /* the frame's buffer in the row */
 	/* stage [0, kRow) of every lane's frame: 16-byte aligned frames whose
-	 * row lies in the UMEM cooperatively (q = 64 k + lane: chunk q % 9 of
-	 * frame q / 9, nine lanes per frame reading its 144 bytes as whole
-	 * chunks), the others byte by byte; zeros past each frame's end */
+	 * row lies in the UMEM cooperatively (q = 64 k + lane: chunk q % kChunks
+	 * of frame q / kChunks, kChunks lanes per frame reading its kRow bytes
+	 * as whole chunks, each lane keeping the chunks it read for the
+	 * write-back), the others byte by byte; zeros past each frame's end */
 	uint64_t *dtab = dtab_all + (threadIdx.x & ~63u);
 	const int lane = threadIdx.x & 63;
 	const uint64_t us16 = usize & ~15ull;
 	const bool coop = valid && !(eff & 15) && eff + kRow <= us16;
 	dtab[lane] = coop ? eff : ~0ull;
 	__builtin_amdgcn_wave_barrier();
-	for (int k = 0; k < 9; k++) {
+	uint4 orig[kChunks];
+#pragma unroll
+	for (int k = 0; k < kChunks; k++) {
 		const int q = 64 * k + lane;
-		const int f = q / 9, c = q - 9 * (q / 9);
+		const int f = q / kChunks, c = q % kChunks;
 		const uint64_t base = dtab[f];
+		orig[k] = make_uint4(0, 0, 0, 0);
 		if (base != ~0ull) {
 			const uint4 v = *reinterpret_cast<const uint4 *>(umem + base + 16 * c);
+			orig[k] = v;
 			uint32_t *d = rows + ((threadIdx.x & ~63u) + f) * kRowDw + 4 * c;
 			d[0] = v.x;
 			d[1] = v.y;
@@ -697,27 +745,67 @@ __device__ __forceinline__ bool sp_tile(uint8_t *umem, uint64_t usize, const xdp
 				g[k] = row[k];
 			ws = we = 0;
 		}
-		verdict[i] = (uint8_t)act;
+		/* the frame's buffer: its bytes and the room it may grow into */
+		own = (uint32_t)min((uint64_t)len0 + room, (uint64_t)kRow);
+		put_verdict(verdict + i, act);
 	} else if (active) {
-		verdict[i] = SP_ABORTED;
+		put_verdict(verdict + i, SP_ABORTED);
 	}
 	/* cooperative write-back of the 16-byte aligned frames' ranges
-	 * [ws, we) from their rows: whole chunks as 16-byte stores, the
-	 * partial ones by dwords and bytes */
+	 * [ws, we) from their rows: whole chunks as 16-byte stores (kWb >= 1:
+	 * also a partial chunk inside the frame's buffer, its other bytes from
+	 * the staged copy; kWb 2: the whole 64-byte sectors the range touches,
+	 * inside the buffer), the other partial ones by dwords and bytes */
 	uint2 *wtab = wtab_all + (threadIdx.x & ~63u);
+	uint32_t *otab = reinterpret_cast<uint32_t *>(wtab + 64);
 	wtab[lane] = make_uint2(ws, we);
+	otab[lane] = own;
 	__builtin_amdgcn_wave_barrier();
-	for (int k = 0; k < 9; k++) {
+#pragma unroll
+	for (int k = 0; k < kChunks; k++) {
 		const int q = 64 * k + lane;
-		const int f = q / 9, c = q - 9 * (q / 9);
+		const int f = q / kChunks, c = q % kChunks;
 		const uint2 r = wtab[f];
 		const uint32_t lo = 16 * c, hi = lo + 16;
-		if (r.y <= lo || r.x >= hi)
+		if (r.x >= r.y)
+			continue;
+		const uint32_t ob = otab[f] & ~15u;   /* whole chunks of the buffer */
+		uint32_t x0 = r.x, x1 = r.y;          /* the chunks to store */
+		if (kWb >= 2) {
+			x0 = r.x & ~63u;
+			x1 = min((r.y + 63) & ~63u, ob);
+			x1 = x1 > r.y ? x1 : r.y;
+		}
+		if (x1 <= lo || x0 >= hi)
 			continue;
 		const uint64_t base = dtab[f];
 		const uint32_t *src = rows + ((threadIdx.x & ~63u) + f) * kRowDw + 4 * c;
 		uint8_t *dst = umem + base + lo;
-		if (r.x <= lo && r.y >= hi) {
+		if (kWb >= 1 && hi <= ob && lo >= x0) {
+			/* the changed bytes [r.x, r.y) from the row, the rest as
+			 * staged */
+			const uint32_t o4[4] = {orig[k].x, orig[k].y, orig[k].z, orig[k].w};
+			uint32_t v[4];
+#pragma unroll
+			for (int d = 0; d < 4; d++) {
+				uint32_t m = 0;
+#pragma unroll
+				for (int j = 0; j < 4; j++) {
+					const uint32_t b = lo + 4 * d + j;
+					m |= (b >= r.x && b < r.y) ? 0xffu << (8 * j) : 0u;
+				}
+				v[d] = m == ~0u ? src[d] : (m ? (src[d] & m) | (o4[d] & ~m) : o4[d]);
+			}
+			if constexpr ((SP_NT & 1) != 0) {
+				typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+				const v4u x = {v[0], v[1], v[2], v[3]};
+				__builtin_nontemporal_store(x, reinterpret_cast<v4u *>(dst));
+			} else {
+				*reinterpret_cast<uint4 *>(dst) = make_uint4(v[0], v[1], v[2], v[3]);
+			}
+		} else if (r.y <= lo || r.x >= hi) {
+			continue;
+		} else if (r.x <= lo && r.y >= hi) {
 			*reinterpret_cast<uint4 *>(dst) = make_uint4(src[0], src[1], src[2], src[3]);
 		} else {
 			const uint32_t a0 = r.x > lo ? r.x - lo : 0u;
@@ -735,7 +823,13 @@ __device__ __forceinline__ bool sp_tile(uint8_t *umem, uint64_t usize, const xdp
 	if (active) {
 		uint4 od = dv;
 		od.z = len;
-		*reinterpret_cast<uint4 *>(out + i) = od;
+		if constexpr ((SP_NT & 2) != 0) {
+			typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+			const v4u x = {od.x, od.y, od.z, od.w};
+			__builtin_nontemporal_store(x, reinterpret_cast<v4u *>(out + i));
+		} else {
+			*reinterpret_cast<uint4 *>(out + i) = od;
+		}
 	}
 	__builtin_amdgcn_wave_barrier();
 	return synack;
@@ -746,7 +840,12 @@ __device__ __forceinline__ bool sp_tile(uint8_t *umem, uint64_t usize, const xdp
  * atomic per wave on a single word serialised the launch: 1.7 ms per 8 M
  * SYNs), which synproxy_sum_kernel adds to the caller's counter. */
 constexpr int kSpread = 256;
-__global__ __launch_bounds__(kBlockS) void synproxy_kernel(uint8_t *umem, uint64_t usize,
+/* waves per SIMD the register allocation targets (build knob for A/B): 5
+ * or more spill (122 VGPRs at 4) */
+#ifndef SP_MINW
+#define SP_MINW 1
+#endif
+__global__ __launch_bounds__(kBlockS, SP_MINW) void synproxy_kernel(uint8_t *umem, uint64_t usize,
 							   const xdpgpu_desc *desc, uint32_t n,
 							   xdpgpu_synproxy_cfg cfg, uint8_t *verdict,
 							   xdpgpu_desc *out,
@@ -754,12 +853,27 @@ __global__ __launch_bounds__(kBlockS) void synproxy_kernel(uint8_t *umem, uint64
 {
 	__shared__ uint32_t rows[kBlockS * kRowDw];
 	__shared__ uint64_t dtab_all[kBlockS];
-	__shared__ uint2 wtab_all[kBlockS];
-	const bool synack = sp_tile(umem, usize, desc, n, cfg, verdict, out, rows, dtab_all,
-				    wtab_all, (uint64_t)blockIdx.x * kBlockS);
-	const uint64_t m = __ballot(synack);
-	if (spread && m && threadIdx.x == 0)
-		atomicAdd(spread + 16 * (blockIdx.x % kSpread), (unsigned long long)__popcll(m));
+	__shared__ uint2 wtab_all[kBlockS + kBlockS / 2];   /* ranges, then buffers */
+	const uint64_t ntiles = ((uint64_t)n + kBlockS - 1) / kBlockS;
+	auto ld = [&](uint64_t t) -> uint4 {
+		const uint64_t i = t * kBlockS + threadIdx.x;
+		return t < ntiles && i < n ? *reinterpret_cast<const uint4 *>(desc + i)
+					   : make_uint4(0, 0, 0, 0);
+	};
+	uint64_t cnt = 0;
+	uint64_t t = blockIdx.x;
+	uint4 dv = ld(t);
+	while (t < ntiles) {
+		const uint64_t tn = SP_PERSIST ? t + gridDim.x : ntiles;
+		const uint4 dn = SP_PERSIST ? ld(tn) : make_uint4(0, 0, 0, 0);
+		const bool synack = sp_tile(umem, usize, dv, n, cfg, verdict, out, rows, dtab_all,
+					    wtab_all, t * kBlockS);
+		cnt += __popcll(__ballot(synack));
+		dv = dn;
+		t = tn;
+	}
+	if (spread && cnt && threadIdx.x == 0)
+		atomicAdd(spread + 16 * (blockIdx.x % kSpread), (unsigned long long)cnt);
 }
 
 /* the spread counters into the caller's, and cleared for the next launch */
@@ -788,9 +902,13 @@ hipError_t launch_synproxy(uint8_t *umem, uint64_t usize, const xdpgpu_desc *des
 			   xdpgpu_desc *out, unsigned long long *synacks,
 			   unsigned long long *spread, hipStream_t stream)
 {
-	const uint32_t blocks = (n + kBlockS - 1) / kBlockS;
+	uint32_t blocks = (n + kBlockS - 1) / kBlockS;
 	if (!blocks)
 		return hipSuccess;
+	if (SP_PERSIST) {
+		const uint32_t cap = resident_blocks_dev<synproxy_kernel, kBlockS>(8192);
+		blocks = blocks < cap ? blocks : cap;
+	}
 	hipLaunchKernelGGL(synproxy_kernel, dim3(blocks), dim3(kBlockS), 0, stream, umem, usize,
 			   desc, n, cfg, verdict, out, synacks ? spread : nullptr);
 	hipError_t e = hipGetLastError();
