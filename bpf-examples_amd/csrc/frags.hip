@@ -3,9 +3,13 @@
  * frags.hip - multi-buffer packets (XDPGPU_CFG_FRAGS, include/xdpgpu.h).
  *
  * A packet of several descriptors (XDP_PKT_CONTD on all but the last,
- * headers/linux/if_xdp.h:122; IS_EOP_DESC, xdpsock.c:67) cannot be read in
- * place: its bytes are spread over UMEM chunks.  The RX fast kernel skips
- * its descriptors, and these kernels handle it as one frame:
+ * headers/linux/if_xdp.h:122; IS_EOP_DESC, xdpsock.c:67) has its bytes
+ * spread over UMEM chunks.  The RX fast kernel skips its descriptors;
+ * frag_count finishes the broken packets; by default xdp_rx_packet_kernel
+ * (xdp_rx.hip) then reads every complete packet in place (its window from
+ * the first fragment, headers and payload sums across the fragments:
+ * 262 144 x 9000-byte packets in 4096-byte fragments, 0.61 vs 1.66 ms
+ * through the bounce copy).  cfg.tune bit 24 selects the bounce path:
  *  - frag_count: the packets' first descriptors (lane per descriptor) walk
  *    their fragments; complete packets are counted per block with the
  *    bounce bytes they need (frag_scan turns the block totals into

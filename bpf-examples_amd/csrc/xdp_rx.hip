@@ -196,6 +196,27 @@ __device__ __forceinline__ uint32_t jhash_key44(const uint32_t k[11],
 /* ------------------------------------------------------------------ */
 /* frame byte access: LDS window first, global beyond it                */
 
+/* Byte off of the multi-buffer packet whose descriptors are d[head..last]
+ * (the concatenation of its fragments, as frags.hip's oracle sees it; the
+ * byte one past its end is the one after its last fragment in the UMEM,
+ * udp_csum's over-read byte, then zeros).  A walk over the descriptors:
+ * only headers past the first fragment, and short first fragments, come
+ * here. */
+__device__ uint32_t pkt_byte(const uint8_t *umem, uint64_t usize, const xdpgpu_desc *d,
+			     uint64_t head, uint32_t last, uint32_t off)
+{
+	uint64_t end = 0;
+	for (uint64_t j = head; j <= last; j++) {
+		const xdpgpu_desc x = d[j];
+		const uint64_t e = (x.addr & ((1ull << 48) - 1)) + (x.addr >> 48);
+		if (off < x.len)
+			return umem[e + off];
+		off -= x.len;
+		end = e + x.len;
+	}
+	return (off == 0 && end < usize) ? umem[end] : 0u;
+}
+
 template <int WIN, bool DEEP>
 struct FrameView {
 	const uint32_t *w;    /* this lane's LDS row (dword aligned) */
@@ -206,9 +227,17 @@ struct FrameView {
 	 * wanted; the lane is then parsed again with DEEP true, which reads
 	 * such bytes from global memory */
 	uint32_t deep;
+	/* a multi-buffer packet read in place: bytes from flen on are the
+	 * later fragments' (pkt_byte); flen ~0 for a frame */
+	uint32_t flen;
+	uint32_t plast;
+	uint64_t phead;
+	const xdpgpu_desc *pdesc;
 
 	__device__ __forceinline__ uint32_t gbyte(uint32_t off) const
 	{
+		if (off >= flen)
+			return pkt_byte(umem, usize, pdesc, phead, plast, off);
 		const uint64_t at = eff + off;
 		return at < usize ? umem[at] : 0;
 	}
@@ -717,11 +746,95 @@ __device__ __forceinline__ uint32_t ext_sums(const RxArgs &a, bool need,
 }
 
 /*
+ * ext_sums for multi-buffer packets read in place: the range [max(l4, WIN),
+ * rhi) of each lane in `need` (packet head head..last, logical offsets)
+ * streamed by the whole wave fragment by fragment, 4 KiB per wave-step;
+ * a fragment whose UMEM offset and packet offset differ in parity is summed
+ * with its bytes swapped within each 16-bit half, so that every fragment
+ * adds in the packet's own word pairing (exact, the check word removed
+ * there).  The byte past the packet is the one after its last fragment.
+ */
+__device__ __forceinline__ uint32_t swap_in_halves(uint32_t x)
+{
+	return ((x & 0x00ff00ffu) << 8) | ((x >> 8) & 0x00ff00ffu);
+}
+
+template <int WIN>
+__device__ uint32_t pkt_ext_sums(const RxArgs &a, bool need, uint64_t head, uint32_t last,
+				 uint32_t l4, uint32_t rhi, uint32_t chk, uint32_t c4,
+				 int lane)
+{
+	uint64_t mask = __ballot(need);
+	uint32_t out = 0;
+	while (mask) {
+		const int sl = __builtin_ctzll(mask);
+		mask &= mask - 1;
+		const uint64_t first = ((uint64_t)readlane32((uint32_t)(head >> 32), sl) << 32) |
+				       readlane32((uint32_t)head, sl);
+		const uint32_t lst = readlane32(last, sl);
+		const uint32_t sl4 = readlane32(l4, sl);
+		const uint32_t lo = sl4 > (uint32_t)WIN ? sl4 : (uint32_t)WIN;
+		const uint32_t hi = readlane32(rhi, sl);
+		uint32_t acc = 0;
+		uint32_t o = 0;       /* the fragment's packet offset */
+		for (uint64_t j = first; j <= lst && o < hi; j++) {
+			const xdpgpu_desc d = a.desc[j];
+			const uint64_t eff = (d.addr & ((1ull << 48) - 1)) + (d.addr >> 48);
+			const uint32_t fend = o + d.len + (j == lst ? 1u : 0u);
+			const uint32_t x0 = lo > o ? lo : o, x1 = hi < fend ? hi : fend;
+			if (x0 < x1) {
+				const uint64_t p0 = eff + (x0 - o);
+				uint64_t p1 = eff + (x1 - o);
+				p1 = p1 < a.usize ? p1 : a.usize;
+				const bool sw = ((eff - o) & 1) != 0;
+				for (uint64_t b = p0 & ~15ull; b < p1; b += 4 * 16 * kWave) {
+					uint4 v[4];
+					uint64_t q[4];
+#pragma unroll
+					for (int k = 0; k < 4; k++) {
+						q[k] = b + 16ull * (lane + kWave * k);
+						v[k] = make_uint4(0, 0, 0, 0);
+						if (q[k] < p1)
+							v[k] = *reinterpret_cast<const uint4 *>(a.umem + q[k]);
+					}
+#pragma unroll
+					for (int k = 0; k < 4; k++) {
+						if (q[k] < p0 || q[k] + 16 > p1) {
+							const uint4 m = chunk_keep(q[k], p0, p1);
+							v[k].x &= m.x;
+							v[k].y &= m.y;
+							v[k].z &= m.z;
+							v[k].w &= m.w;
+						}
+						if (sw) {
+							v[k].x = swap_in_halves(v[k].x);
+							v[k].y = swap_in_halves(v[k].y);
+							v[k].z = swap_in_halves(v[k].z);
+							v[k].w = swap_in_halves(v[k].w);
+						}
+						acc += halves(v[k].x) + halves(v[k].y) + halves(v[k].z) +
+						       halves(v[k].w);
+					}
+				}
+			}
+			o += d.len;
+		}
+		uint32_t t = wave_sum32(acc);
+		if (readlane32(chk, sl) >= (uint32_t)WIN)
+			t -= readlane32(c4, sl);
+		const uint32_t f = fold16(t);
+		if (lane == sl)
+			out = f;
+	}
+	return out;
+}
+
+/*
  * The generic pipeline on up to 64 frames (one per lane): any descriptor,
  * any alignment, any header stack the oracle knows.  Used for the frames
  * the fast path defers.  Writes verdict, result and tuple of each frame.
  */
-template <int WIN>
+template <int WIN, bool PKT = false>
 __device__ __forceinline__ void generic_batch(const RxArgs &a, uint32_t *win,
 					      uint64_t *dtab, int lane,
 					      uint64_t i, bool active,
@@ -730,13 +843,40 @@ __device__ __forceinline__ void generic_batch(const RxArgs &a, uint32_t *win,
 					      uint64_t &my_bytes)
 {
 	constexpr int SDW = WIN / 4 + 1;
+	/* PKT: lane i is a multi-buffer packet's first descriptor (frags.hip
+	 * finished the broken ones), read in place: len is the packet's,
+	 * flen its first fragment's */
+	uint32_t plast = 0;
+	uint64_t ptotal = 0;
+	if constexpr (PKT) {
+		active = active && (a.desc[i].options & XDPGPU_PKT_CONTD) &&
+			 !(i && (a.desc[i - 1].options & XDPGPU_PKT_CONTD));
+		if (active) {
+			for (uint64_t j = i;; j++) {
+				const uint32_t o = a.desc[j].options;
+				ptotal += a.desc[j].len;
+				if (!(o & XDPGPU_PKT_CONTD) || j + 1 == a.n) {
+					plast = (uint32_t)j;
+					active = !(o & XDPGPU_PKT_CONTD);
+					break;
+				}
+			}
+			for (uint64_t j = i; active && j <= plast; j++) {
+				const xdpgpu_desc x = a.desc[j];
+				const uint64_t e = (x.addr & ((1ull << 48) - 1)) + (x.addr >> 48);
+				active = (uint64_t)x.len <= a.usize && e <= a.usize - x.len;
+			}
+			active = active && ptotal <= 0xffffffffull;
+		}
+	}
 	const uint4 dv = active ? *reinterpret_cast<const uint4 *>(a.desc + i)
 				: make_uint4(0, 0, 0, 0);
 	const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
-	const uint32_t len = dv.z;
+	const uint32_t flen = dv.z;
+	const uint32_t len = PKT ? (uint32_t)ptotal : flen;
 	const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
-	const bool valid = active && (uint64_t)len <= a.usize &&
-			   eff <= a.usize - len;
+	const bool valid = active && (uint64_t)flen <= a.usize &&
+			   eff <= a.usize - flen;
 
 	/* stage the header windows */
 	uint4 cv[WIN / 16];
@@ -750,10 +890,21 @@ __device__ __forceinline__ void generic_batch(const RxArgs &a, uint32_t *win,
 #pragma unroll
 			for (int b = 0; b < 4; b++) {
 				const uint32_t off = 4 * d + b;
-				if (valid && off <= len && eff + off < a.usize)
+				if (valid && off <= flen && eff + off < a.usize)
 					wv |= (uint32_t)a.umem[eff + off] << (8 * b);
 			}
 			win[lane * SDW + d] = wv;
+		}
+	}
+	if constexpr (PKT) {
+		/* a first fragment shorter than the window: the rest of the
+		 * window from the later fragments */
+		if (valid && flen < (uint32_t)WIN) {
+			uint8_t *row = reinterpret_cast<uint8_t *>(win + lane * SDW);
+			for (uint32_t off = flen; off < (uint32_t)WIN; off++)
+				row[off] = off <= len ? (uint8_t)pkt_byte(a.umem, a.usize, a.desc, i,
+									  plast, off)
+						      : 0;
 		}
 	}
 	__builtin_amdgcn_wave_barrier();
@@ -766,6 +917,10 @@ __device__ __forceinline__ void generic_batch(const RxArgs &a, uint32_t *win,
 	F.eff = eff;
 	F.usize = a.usize;
 	F.deep = 0;
+	F.flen = PKT ? flen : ~0u;
+	F.plast = plast;
+	F.phead = i;
+	F.pdesc = a.desc;
 	Lane L = parse_lane<WIN, false>(F, valid ? len : 0u); /* 0: ABORTED */
 	if (__ballot(F.deep)) {
 		if (F.deep) {
@@ -775,22 +930,31 @@ __device__ __forceinline__ void generic_batch(const RxArgs &a, uint32_t *win,
 			G.eff = eff;
 			G.usize = a.usize;
 			G.deep = 0;
+			G.flen = F.flen;
+			G.plast = plast;
+			G.phead = i;
+			G.pdesc = a.desc;
 			L = parse_lane<WIN, true>(G, valid ? len : 0u);
 		}
 	}
 
 	/* a checksum range past the window: the payload sum is deferred to
 	 * the bulk kernel (yl entry), except for echo candidates, whose TX
-	 * verdict needs it here */
+	 * verdict needs it here (and for packets read in place, summed here) */
 	const bool echo_cand = (a.flags & XDPGPU_CFG_ICMP6_ECHO) &&
 			       L.nvlan() == 0 && L.ipv6() && len >= 62 &&
 			       F.b8(20) == 58 && F.b8(54) == 128;
 	const bool need_ext = L.st() == ST_GO && L.has_csum() &&
 			      L.rhi() > (uint32_t)WIN;
-	const bool ydef = need_ext && a.ydefer && a.res && !echo_cand &&
+	const bool ydef = !PKT && need_ext && a.ydefer && a.res && !echo_cand &&
 			  L.rhi() < 65536u;
-	const uint32_t ext_sum = ext_sums<WIN>(a, need_ext && !ydef, eff, L.l4(),
-					       L.rhi(), L.chk(), L.c4(), lane);
+	uint32_t ext_sum;
+	if constexpr (PKT)
+		ext_sum = pkt_ext_sums<WIN>(a, need_ext, i, plast, L.l4(), L.rhi(), L.chk(),
+					    L.c4(), lane);
+	else
+		ext_sum = ext_sums<WIN>(a, need_ext && !ydef, eff, L.l4(), L.rhi(), L.chk(),
+					L.c4(), lane);
 	uint32_t partial = 0;   /* ydef: the L4 sum without the payload part */
 
 	/* checksums, flow key, verdict */
@@ -911,7 +1075,21 @@ __device__ __forceinline__ void generic_batch(const RxArgs &a, uint32_t *win,
 			return rb(j);
 		};
 		uint8_t *g = a.umem + eff;
-		if (!(eff & 3)) {
+		if (PKT && flen < 60) {
+			/* the rewritten bytes spread over the fragments */
+			uint64_t j = i;
+			uint32_t o = 0;
+			for (int b = 0; b < 60; b++) {
+				while (b >= (int)(o + a.desc[j].len)) {
+					o += a.desc[j].len;
+					j++;
+				}
+				const xdpgpu_desc x = a.desc[j];
+				const uint64_t e = (x.addr & ((1ull << 48) - 1)) + (x.addr >> 48);
+				if (b < 12 || b >= 22)
+					a.umem[e + (b - o)] = (uint8_t)nb(b);
+			}
+		} else if (!(eff & 3)) {
 			uint32_t *gw = reinterpret_cast<uint32_t *>(g);
 #pragma unroll
 			for (int d = 0; d < 15; d++) {
@@ -973,6 +1151,23 @@ __device__ __forceinline__ void generic_batch(const RxArgs &a, uint32_t *win,
 #pragma unroll
 				for (int j = 0; j < 11; j++)
 					tp[j] = rec_live ? key[j] : 0u;
+			}
+		}
+	}
+
+	if constexpr (PKT) {
+		/* the packet's other descriptors: its verdict, all-zero
+		 * records and tuples */
+		if (active) {
+			const uint32_t tb = a.tup ? (a.tuple_fmt == XDPGPU_TUPLE_NET ? 44u :
+						     a.tuple_fmt == XDPGPU_TUPLE_V4 ? 16u : 0u)
+						  : 0u;
+			for (uint64_t j = i + 1; j <= plast; j++) {
+				a.verdict[j] = (uint8_t)verdict;
+				if (a.res)
+					*reinterpret_cast<uint4 *>(a.res + j) = make_uint4(0, 0, 0, 0);
+				for (uint32_t b = 0; b < tb; b++)
+					a.tup[j * tb + b] = 0;
 			}
 		}
 	}
@@ -2747,6 +2942,38 @@ __global__ __launch_bounds__(kBlock, 5) void xdp_rx_generic_kernel(RxArgs a)
 	block_stats_flush(a, blk_cnt, cnt, my_bytes, lane);
 }
 
+/* Multi-buffer packets read in place (XDPGPU_CFG_FRAGS, after
+ * frag_count): a lane per descriptor, the packets' first descriptors
+ * through generic_batch<WIN, true>, grid-strided over the batch's tiles. */
+template <int WIN>
+__global__ __launch_bounds__(kBlock, 4) void xdp_rx_packet_kernel(RxArgs a)
+{
+	constexpr int SDW = WIN / 4 + 1;
+	__shared__ uint32_t lds[kWavesPerBlock * kWave * SDW + 8];
+	__shared__ uint64_t dtab_all[kWavesPerBlock * kWave];
+	__shared__ unsigned long long blk_cnt[CNT_SLOT];
+
+	const int lane = threadIdx.x & (kWave - 1);
+	const int wid = threadIdx.x / kWave;
+	uint32_t *win = lds + wid * kWave * SDW;
+	uint64_t *dtab = dtab_all + wid * kWave;
+	if (threadIdx.x < CNT_SLOT)
+		blk_cnt[threadIdx.x] = 0;
+	__syncthreads();
+
+	const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+	const uint64_t ntiles = ((uint64_t)a.n + kWave - 1) / kWave;
+	uint32_t cnt[CNT_FRAG + 1] = {};
+	uint64_t my_bytes = 0;
+	for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + wid; t < ntiles; t += nwaves) {
+		const uint64_t i = t * kWave + lane;
+		generic_batch<WIN, true>(a, win, dtab, lane, i < a.n ? i : 0, i < a.n, nullptr,
+					 nullptr, cnt, my_bytes);
+	}
+
+	block_stats_flush(a, blk_cnt, cnt, my_bytes, lane);
+}
+
 /* Memory ceiling for the RX traffic pattern (diagnostic): the same
  * descriptor, transposed 64-byte window loads and 33 bytes of stores per
  * frame, with no parse.  Its bandwidth is what the RX kernel can approach. */
@@ -2941,6 +3168,20 @@ uint32_t rx_xregion(uint32_t n, uint32_t blocks)
 	const uint64_t ntiles = ((uint64_t)n + kWave - 1) / kWave;
 	const uint64_t nwaves = (uint64_t)blocks * kWavesPerBlock;
 	return (uint32_t)(((ntiles + nwaves - 1) / nwaves) * kWave);
+}
+
+hipError_t launch_rx_packets(const RxArgs &a, uint32_t max_blocks, hipStream_t stream)
+{
+	const uint64_t tiles = ((uint64_t)a.n + kWave - 1) / kWave;
+	uint64_t blocks = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
+	uint32_t cap = resident_blocks<xdp_rx_packet_kernel<64>>();
+	cap = cap < max_blocks ? cap : max_blocks;
+	blocks = blocks < cap ? blocks : cap;
+	if (!blocks)
+		return hipSuccess;
+	hipLaunchKernelGGL(xdp_rx_packet_kernel<64>, dim3((uint32_t)blocks), dim3(kBlock), 0,
+			   stream, a);
+	return hipGetLastError();
 }
 
 hipError_t launch_rx(const RxArgs &a, uint32_t window, uint32_t max_blocks,

@@ -601,9 +601,12 @@ static int enqueue_rx(xdpgpu_ctx *ctx, Slot &s, uint8_t *d_umem, uint64_t usize,
 	 * the device. */
 	FragArgs f;
 	memset(&f, 0, sizeof(f));
+	/* packets read in place, or (cfg.tune bit 24, round 2's path for
+	 * A/B) gathered into a bounce UMEM */
+	const bool bounce = (ctx->cfg.tune >> 24) & 1;
 	const uint64_t mcap = a.frags ? (uint64_t)n / 2 + 1 : 0;
 	if (a.frags) {
-		const uint64_t bytes = usize + 16 * mcap;
+		const uint64_t bytes = bounce ? usize + 16 * mcap : 0;
 		if (!s.d_fc || bytes + 64 > s.bounce_cap || mcap > s.pk_cap) {
 			/* (re)allocation: the slot's earlier launches first */
 			if (s.scr_last)
@@ -645,7 +648,10 @@ static int enqueue_rx(xdpgpu_ctx *ctx, Slot &s, uint8_t *d_umem, uint64_t usize,
 			       ctx->cfg.tune, ev));
 	/* the launch zeroed the other counter set: the next one uses it */
 	s.steal_set ^= 1;
-	if (a.frags) {
+	if (a.frags && !bounce) {
+		/* one frame per packet, its fragments read where they lie */
+		HIP_TRY(ctx, launch_rx_packets(a, ctx->max_blocks, stream));
+	} else if (a.frags) {
 		/* one frame per packet: gathered into the bounce UMEM, the RX
 		 * kernels over the bounce batch, the outputs back to the
 		 * packets' descriptors */

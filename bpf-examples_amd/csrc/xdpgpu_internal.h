@@ -171,6 +171,10 @@ struct RxArgs {
  * each of the fast, exception and bulk kernels (launch order) */
 hipError_t launch_rx(const RxArgs &a, uint32_t window, uint32_t max_blocks,
 		     hipStream_t stream, uint32_t tune, hipEvent_t *ev);
+/* multi-buffer packets read in place (after launch_frag_count): every
+ * complete packet of the batch as one frame, outputs to all its
+ * descriptors */
+hipError_t launch_rx_packets(const RxArgs &a, uint32_t max_blocks, hipStream_t stream);
 hipError_t launch_jhash_words(const uint32_t *words, uint32_t nwords, uint32_t stride,
 			      uint32_t n, uint32_t initval, uint32_t variant,
 			      uint32_t *out, hipStream_t stream);

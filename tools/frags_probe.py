@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--size", type=int, default=9000)
     ap.add_argument("--chunk", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--tune", type=lambda x: int(x, 0), default=0,
+                    help="cfg.tune of the fragments' context (1<<24: bounce copy)")
     args = ap.parse_args()
     u, d, _ = xdpgpu.pool_generate(args.frames, xdpgpu.POOL_UDP4, args.size, 0x5EED0002)
     lens = d["len"].astype(np.int64)
@@ -44,7 +46,7 @@ def main():
         d_desc = torch.from_numpy(descs.view(np.uint8)).to(dev)
         d_v = torch.zeros(n, dtype=torch.uint8, device=dev)
         d_res = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
-        with xdpgpu.XdpGpu(0, flags) as g:
+        with xdpgpu.XdpGpu(0, flags, tune=args.tune if flags & xdpgpu.CFG_FRAGS else 0) as g:
             ms = []
             for r in range(args.reps + 1):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

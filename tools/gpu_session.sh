@@ -63,6 +63,7 @@ workload() {
 	nat64_egress) echo "python3 tools/nat64_probe.py --reps 5 --direction 1" ;;
 	nat64_dynamic) echo "python3 tools/nat_dyn_probe.py --frames 16777216 --reps 5" ;;
 	frags) echo "python3 tools/frags_probe.py --reps 5" ;;
+	frags_bounce) echo "python3 tools/frags_probe.py --reps 5 --tune 0x1000000" ;;
 	synproxy) echo "python3 bench.py --no-cpu --legs synproxy --steps 5 --warmup 2" ;;
 	echo) echo "python3 bench.py --no-cpu --legs echo --steps 5 --warmup 2" ;;
 	bench) echo "python3 bench.py --no-cpu --no-secondary --steps 20" ;;
