@@ -17,11 +17,13 @@ the kernel (xdpgpu_kernel_times), in a second pass of K launches on a
 context with XDPGPU_CFG_TIMING so the events do not perturb the timed
 steps.  traffic is the HBM bytes per launch from the committed rocprofv3
 PMC summary (profiles/r<NN>_pmc.json, tools/pmc_profile.sh).  The CPU baseline
-is the lean CPU leg (oracle/cpu_leg.c: the same outputs as the oracle,
-checked on the sample) on this host's cores, rank 0 at N = 1 only, on a
-bounded sample: one pinned thread, then one thread per CPU of the affinity
-set, with the CPU model and the calibration probe beside the reference
-headers' own routines (oracle/_ref).  Secondary lines: config 2 geometry
+(rank 0 at N = 1 only, on a bounded sample, one pinned thread then one
+thread per CPU the job may use) is the same per-frame work with the
+reference headers' own checksum and jhash routines (oracle/_ref, compiled
+from /root/reference in the container; kind "reference"), when that
+library is present; the lean port (oracle/cpu_leg.c: the same outputs as
+the oracle, checked on the sample) is timed beside it as port_mpps, with
+the CPU model and the calibration probe.  Secondary lines: config 2 geometry
 at 1500 B, config 3 (16 M IMIX, 44 B network_tuple), config 4 (16 M x
 128 B nat64 ingress, static and dynamic state), multi-buffer 9000 B
 packets, the ICMPv6 echo responder and the SYN proxy (8 M SYNs answered
@@ -110,10 +112,12 @@ def cpu_model() -> str:
 
 
 def cpu_baseline(umem, descs, flags, fmt, budget_s: float = 10.0):
-    """The lean CPU leg (oracle/cpu_leg.c) on this host's cores: one pinned
-    thread, then one thread per CPU of the affinity set; its outputs checked
-    against the oracle on part of the sample; the calibration probe (the
-    survey probe's work) beside the reference headers' routines."""
+    """The CPU baseline on this host's cores: the reference headers'
+    routines (oracle/_ref ref_leg_bench, kind "reference") when present,
+    beside the lean port (oracle/cpu_leg.c, port_mpps); one pinned thread,
+    then one thread per CPU the job may use; outputs checked against the
+    oracle on part of the sample; the calibration probe (the survey probe's
+    work) on both."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     oracle.lib()
@@ -188,6 +192,16 @@ def cpu_baseline(umem, descs, flags, fmt, budget_s: float = 10.0):
                       f"1 pinned thread: {len(one)} frames x {reps1} passes"}
     if refleg:
         out.update(refleg)
+        # the reference's own routines are the CPU path north_star names:
+        # they are the baseline; the port (one pass per checksum, 64-bit
+        # sums) stays beside them as port_mpps
+        out["port_mpps"] = out["value"]
+        out["port_sample"] = out["sample"]
+        out["value"] = refleg["reference_mpps"]
+        out["kind"] = "reference"
+        out["gbps"] = round(refleg["reference_mpps"] * 1e6 * BYTES_PER_FRAME / 1e9, 2)
+        out["single_thread_mpps"] = refleg["reference_single_thread_mpps"]
+        out["sample"] = refleg["reference_sample"]
     return out
 
 

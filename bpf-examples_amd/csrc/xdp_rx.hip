@@ -2475,23 +2475,27 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 
 	const bool dma = !a.force_generic && a.usize >= 64;
 	/* the block's k-th tile (a.order): 0: b + k nb; 1: b per + k over a
-	 * contiguous range of per tiles; 2, 3: k nb + (b + k c) mod nb, c = 1,
-	 * 97 (each round of nb tiles still split over the blocks, each block
-	 * moving through the round's positions); ntiles past the block's
-	 * tiles.  Increasing in k. */
+	 * contiguous range of per tiles; 2: k nb + (b + k) mod nb (each round
+	 * of nb tiles still split over the blocks, each block moving through
+	 * the round's positions); 3: pairs, 2 (b + (k / 2) nb) + k mod 2 (the
+	 * two tiles whose 64 verdict bytes share a 128-byte line on one CU,
+	 * and so in one XCD's L2); ntiles past the block's tiles.  Increasing
+	 * in k. */
 	/* the block's own tiles are those below own; the shared ones above
 	 * are claimed after them (a.steal_tiles) */
 	const uint64_t shared = FRAGS || DIAG ? 0 : a.steal_tiles;
 	const uint64_t own = ntiles - shared;
 	const uint64_t per = (own + nb - 1) / nb;
 	const uint32_t order = a.order;
-	const uint64_t rot = order == 3 ? 97 : 1;
+	const uint64_t rot = 1;
 	auto tile_of = [&](uint64_t k) -> uint64_t {
 		uint64_t t, lim = own;
 		if (order == 1) {
 			t = rb * per + k;
 			lim = min(own, rb * per + per);
-		} else if (order >= 2) {
+		} else if (order == 3) {
+			t = 2 * (rb + (k >> 1) * nb) + (k & 1);
+		} else if (order == 2) {
 			t = k * nb + (rb + k * rot) % nb;
 		} else {
 			t = rb + k * nb;
@@ -2653,15 +2657,20 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 				v = atomicAdd(ctr, 1u);
 			return v;
 		};
+		/* the pair order (3): a claim is the adjacent tiles own + 2v
+		 * heads + 2h and the next, on the same XCD as in its own-tile
+		 * order (own is a multiple of 2 heads) */
+		const bool pairs = order == 3;
 		auto first_of = [&](uint32_t v) -> uint64_t {
-			const uint64_t t =
-				own + (uint64_t)__builtin_amdgcn_readfirstlane(v) * 2 * heads + h;
+			const uint64_t t = own + (uint64_t)__builtin_amdgcn_readfirstlane(v) * 2 * heads +
+					   (pairs ? 2 * h : h);
 			return t < ntiles ? t : ntiles;
 		};
 		auto second_of = [&](uint64_t t) -> uint64_t {
-			return t + heads < ntiles ? t + heads : ntiles;
+			const uint64_t u = t + (pairs ? 1 : heads);
+			return u < ntiles ? u : ntiles;
 		};
-		uint64_t c0 = own + h < ntiles ? first_of(claim2()) : ntiles;
+		uint64_t c0 = own + (pairs ? 2 * h : h) < ntiles ? first_of(claim2()) : ntiles;
 		if (c0 < ntiles) {
 			/* per pair: descriptors, windows and the next claim in
 			 * flight, one wait, then the two tiles.  (Pipelined over
@@ -3133,9 +3142,10 @@ static hipError_t launch_db(RxArgs a, uint32_t max_blocks, hipStream_t stream,
 	a.steal_tiles = 0;
 	if (a.steal && a.steal_16ths && !a.frags && !a.ndev && !diag &&
 	    ntiles >= 64 * blocks) {
-		/* own a multiple of the heads (xdp_rx_db_kernel's head order) */
+		/* own a multiple of twice the heads (xdp_rx_db_kernel's head
+		 * orders) */
 		const uint64_t own = (ntiles - ntiles * min(a.steal_16ths, 16u) / 16) &
-				     ~(uint64_t)(kStealHeads - 1);
+				     ~(uint64_t)(2 * kStealHeads - 1);
 		const uint64_t sh = ntiles - own;
 		const uint64_t xr = ((own + blocks - 1) / blocks + steal_cap(sh, blocks)) * kWave;
 		if (xr * blocks <= a.xcap && xr <= 0xffffffffull) {

@@ -25,6 +25,9 @@
 #                          (config2 imix imix_r2 nat64 nat64_egress 1500)
 #   ab:LIB                 A/B: the in-tree library vs LIB, alternating
 #                          processes (IMIX, 1500 B, config 2)
+#   abn:WL+WL:LIB,LIB      the same over named workloads and several LIBs
+#   tune:WL:V,V            tune_rx variants (window:tune) interleaved in one
+#                          process, 7 rounds, on a tune_rx workload
 #   run:LIB:WORKLOAD       one workload (tune_rx timing) with library LIB
 #   stamps[:N+TUNE+KIND+FMT] per-wave timeline (build/stamps, tools/stamps.py)
 #   probe                  tools/order_probe (LDS-DMA / vmcnt ordering)
@@ -111,6 +114,26 @@ for s in "$@"; do
 				step "ab_config2_$tag" 150 env XDPGPU_LIB="$lib" $(workload config2)
 			done
 		done ;;
+	abn)
+		# abn:WL1+WL2:LIB1,LIB2 - two rounds, each workload, in-tree then each LIB
+		wls=${arg%%:*}
+		libs=${arg#*:}
+		for r in 1 2; do
+			for wl in ${wls//+/ }; do
+				for lib in bpf-examples_amd/csrc/libxdpgpu.so ${libs//,/ }; do
+					tag=$(basename "$(dirname "$lib")")_$r
+					# shellcheck disable=SC2046
+					step "abn_${wl}_$tag" 150 env XDPGPU_LIB="$lib" $(workload "$wl")
+				done
+			done
+		done ;;
+	tune)
+		# tune:WL:V1,V2,... - tools/tune_rx.py variants (window:tune) in one
+		# process, interleaved, on a tune_rx workload
+		wl=${arg%%:*}
+		vs=${arg#*:}
+		# shellcheck disable=SC2046
+		step "tune_${wl}_$(date +%s)" 300 $(workload "$wl" | sed "s/--variants 64:0/--variants $vs/; s/--rounds 3/--rounds 7/") ;;
 	run)
 		lib=${arg%%:*}
 		wl=${arg#*:}
