@@ -31,6 +31,7 @@
 #   run:LIB:WORKLOAD       one workload (tune_rx timing) with library LIB
 #   stamps[:N+TUNE+KIND+FMT] per-wave timeline (build/stamps, tools/stamps.py)
 #   probe                  tools/order_probe (LDS-DMA / vmcnt ordering)
+#   hbm[:MODE]             tools/hbm_probe [MODE] (access-shape ceilings)
 #   e2e                    PCIe-inclusive host path (bench.py --e2e)
 #   cli                    xdpsock-gpu over a 16 M-frame pool
 set -u
@@ -145,6 +146,7 @@ for s in "$@"; do
 		step "stamps${arg:+_$(echo "$arg" | tr '+' '_')}" 200 env XDPGPU_LIB=build/stamps/libxdpgpu.so \
 			python3 -u tools/stamps.py ${arg//+/ } ;;
 	probe) step probe 120 tools/order_probe 64 ;;
+	hbm) step "hbm_${arg:-all}" 300 tools/hbm_probe $arg ;;
 	e2e) step e2e 600 python3 bench.py --no-cpu --no-secondary --steps 10 --e2e ;;
 	cli) step cli 300 bpf-examples_amd/apps/xdpsock-gpu --pool 16777216 --pool-kind udp4 \
 		-b 1048576 -C 67108864 --json -Q ;;

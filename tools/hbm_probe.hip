@@ -423,6 +423,33 @@ __global__ __launch_bounds__(256) void k_stride(uint4 *p, size_t nframes, uint32
 		out[0] = x;
 }
 
+/* nat64 egress's shape (config-4 egress pool: 128-byte frames at a
+ * 192-byte stride behind 64 bytes of headroom): per frame, read its first
+ * 64 bytes and write them back with the 20 bytes in front of the frame (a
+ * dword and a 16-byte chunk of the headroom's last sector, FRONT 1), or
+ * with that whole headroom sector (FRONT 2: a measurement of what a
+ * partial sector costs; the translator may not write bytes outside the
+ * frame's -20), or nothing in front (FRONT 0). */
+template <int FRONT>
+__global__ __launch_bounds__(256) void k_egress(uint8_t *p, size_t nframes, uint32_t *out)
+{
+	const size_t n = nframes * 4;
+	for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+		uint8_t *f = p + (i / 4) * 192 + 64;
+		const uint32_t c = i % 4;
+		uint4 *q = reinterpret_cast<uint4 *>(f) + c;
+		uint4 v = *q;
+		v.x += 1;
+		*q = v;
+		if (FRONT == 1 && c == 3) {
+			*reinterpret_cast<uint32_t *>(f - 20) = v.y;
+			*reinterpret_cast<uint4 *>(f - 16) = v;
+		} else if (FRONT == 2) {
+			reinterpret_cast<uint4 *>(f - 64)[c] = v;
+		}
+	}
+}
+
 static int stride_main()
 {
 	const size_t frames = 16ull << 20;
@@ -445,6 +472,29 @@ static int stride_main()
 		{"write128 ", k_stride<8, false, true, false>, 128.0},
 		{"rw128    ", k_stride<8, true, true, false>, 256.0},
 	};
+	/* egress shape: 16 M frames at a 192-byte stride (3 GiB) */
+	uint8_t *pe;
+	CK(hipMalloc(&pe, frames * 192 + 64));
+	CK(hipMemset(pe, 1, frames * 192 + 64));
+	struct E { const char *name; void (*k)(uint8_t *, size_t, uint32_t *); };
+	const E es[] = {{"egress rw64          ", k_egress<0>},
+			{"egress rw64+front20  ", k_egress<1>},
+			{"egress rw64+sector64 ", k_egress<2>}};
+	for (int rep = 0; rep < 2; rep++)
+		for (const E &v : es)
+			for (int grid : {2048, 8192}) {
+				for (int w = 0; w < 2; w++)
+					hipLaunchKernelGGL(v.k, dim3(grid), dim3(256), 0, 0, pe, frames, o);
+				CK(hipEventRecord(e0, 0));
+				for (int r = 0; r < 10; r++)
+					hipLaunchKernelGGL(v.k, dim3(grid), dim3(256), 0, 0, pe, frames, o);
+				CK(hipEventRecord(e1, 0));
+				CK(hipEventSynchronize(e1));
+				float ms;
+				CK(hipEventElapsedTime(&ms, e0, e1));
+				printf("stride %s grid %5d  %.4f ms / 16 M frames\n", v.name, grid, ms / 10);
+			}
+	CK(hipFree(pe));
 	for (int rep = 0; rep < 2; rep++)
 		for (const V &v : vs)
 			for (int grid : {2048, 8192}) {
