@@ -1464,10 +1464,13 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 #pragma unroll
 	for (int d = 1; d < kWave; d <<= 1)
 		mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, kWave));
-	/* frame f's 16 partials, zero but for its group's lanes */
+	/* frame f's 16 partials, zero but for its group's lanes.  The four
+	 * 16-byte slots of a lane rotated by lane / 4: lanes l and l + 4 are
+	 * 256 bytes apart, one bank row, so an unrotated slot j would put them
+	 * on the same banks */
 #pragma unroll
 	for (int j = 0; j < 4; j++)
-		part4[4 * lane + j] = make_uint4(0, 0, 0, 0);
+		part4[4 * lane + ((j + (lane >> 2)) & 3)] = make_uint4(0, 0, 0, 0);
 	__builtin_amdgcn_wave_barrier();
 	if (kTailAdapt && mx <= 64 * U)
 		stream_groups<4, U, NT>(a, meta, part, lane, nb);
@@ -1481,7 +1484,7 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 	 * the raw sum of 16-bit halves fits 32 bits */
 #pragma unroll
 	for (int j = 0; j < 4; j++) {
-		const uint4 x = part4[4 * lane + ((j + lane) & 3)];
+		const uint4 x = part4[4 * lane + ((j + (lane >> 2)) & 3)];
 		t += x.x + x.y + x.z + x.w;
 	}
 	uint32_t c4, sum4;
