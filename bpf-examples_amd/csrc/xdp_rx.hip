@@ -3136,8 +3136,14 @@ static hipError_t launch_db(RxArgs a, uint32_t max_blocks, hipStream_t stream,
 		blocks = max_blocks;
 	if (blocks == 0)
 		blocks = 1;
-	/* list regions per block: its share of the tiles */
-	a.xregion = (uint32_t)(((ntiles + blocks - 1) / blocks) * kWave);
+	/* list regions per block: its share of the tiles (the pair order, 3:
+	 * whole pairs, up to one tile more than an even share) */
+	auto share = [&](uint64_t own) -> uint64_t {
+		if (a.order == 3)
+			return 2 * (((own + 1) / 2 + blocks - 1) / blocks);
+		return (own + blocks - 1) / blocks;
+	};
+	a.xregion = (uint32_t)(share(ntiles) * kWave);
 	a.nregions = (uint32_t)blocks;
 	/* shared tiles (xdp_rx_db_kernel): the last ntiles x steal_16ths / 16,
 	 * for batches of at least 64 tiles per block; a block's region then
@@ -3150,7 +3156,7 @@ static hipError_t launch_db(RxArgs a, uint32_t max_blocks, hipStream_t stream,
 		const uint64_t own = (ntiles - ntiles * min(a.steal_16ths, 16u) / 16) &
 				     ~(uint64_t)(2 * kStealHeads - 1);
 		const uint64_t sh = ntiles - own;
-		const uint64_t xr = ((own + blocks - 1) / blocks + steal_cap(sh, blocks)) * kWave;
+		const uint64_t xr = (share(own) + steal_cap(sh, blocks)) * kWave;
 		if (xr * blocks <= a.xcap && xr <= 0xffffffffull) {
 			a.steal_tiles = (uint32_t)sh;
 			a.xregion = (uint32_t)xr;

@@ -356,6 +356,38 @@ __global__ __launch_bounds__(256) void k_bulkw(const uint8_t *fr, size_t nframes
 		out[0] = x;
 }
 
+/* the same quarter-wave streaming over IMIX's middle class: bytes [64, 570)
+ * of 570-byte frames at a 576-byte stride (every frame), or of every other
+ * frame (SKIP 2: the frames between are not read, as 64-byte frames
+ * between bulk frames are not) */
+template <int U, int SKIP>
+__global__ __launch_bounds__(256) void k_bulk570(const uint8_t *fr, size_t nframes,
+						 uint32_t *out)
+{
+	const int lane = threadIdx.x & 63, q = lane >> 4, sub = lane & 15;
+	const size_t nw = (size_t)gridDim.x * 4;
+	const size_t nb = nframes / SKIP;
+	uint32_t x = 0;
+	for (size_t t = blockIdx.x * 4ull + (threadIdx.x >> 6); t < nb / 64; t += nw) {
+		for (int j = 0; j < 16; j++) {
+			const uint8_t *f = fr + (t * 64 + 4 * j + q) * SKIP * 576ull + 64;
+			uint4 v[U];
+#pragma unroll
+			for (int u = 0; u < U; u++) {
+				const uint32_t ou = 256 * u + 16 * sub;
+				v[u] = make_uint4(0, 0, 0, 0);
+				if (ou < 506)
+					v[u] = ntl((const uint4 *)(f + ou));
+			}
+#pragma unroll
+			for (int u = 0; u < U; u++)
+				x += v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+		}
+	}
+	if (x == 0x12345678u)
+		out[0] = x;
+}
+
 static uint8_t *bulk_buf;
 static size_t bulk_frames = 2ull << 20;
 template <int U, bool NT>
@@ -365,11 +397,26 @@ static void run_bulkw(void *) { hipLaunchKernelGGL((k_bulkw<U, NT>), dim3(C.grid
 template <bool NT>
 static void run_bulkflat(void *) { hipLaunchKernelGGL((k_read<NT>), dim3(C.grid), dim3(256), 0, 0, (const uint4 *)bulk_buf, bulk_frames * 1536 / 16, C.out); }
 
+template <int SKIP>
+static void run_bulk570(void *) { hipLaunchKernelGGL((k_bulk570<4, SKIP>), dim3(C.grid), dim3(256), 0, 0, bulk_buf, bulk_frames * 1536 / 576, C.out); }
+
 static int bulk_main()
 {
 	CK(hipMalloc(&bulk_buf, bulk_frames * 1536));
 	CK(hipMemset(bulk_buf, 3, bulk_frames * 1536));
 	CK(hipMalloc(&C.out, 64));
+	{
+		const size_t n570 = bulk_frames * 1536 / 576;
+		for (int grid : {1024, 2048, 4096}) {
+			C.grid = grid;
+			float t = time_it(run_bulk570<1>, 0, 20);
+			printf("grid %5d b570 all   %7.1f GB/s (of 506 B/frame) %.4f ms\n", grid,
+			       n570 * 506.0 / 1e9 / t * 1e3, t);
+			t = time_it(run_bulk570<2>, 0, 20);
+			printf("grid %5d b570 every2 %7.1f GB/s (of 506 B/frame) %.4f ms\n", grid,
+			       n570 / 2 * 506.0 / 1e9 / t * 1e3, t);
+		}
+	}
 	const double gb = bulk_frames * 1436.0 / 1e9;
 	const int grids[] = {1024, 1536, 2048, 4096};
 	for (int gi = 0; gi < 4; gi++) {
