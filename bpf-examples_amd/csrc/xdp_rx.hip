@@ -1289,6 +1289,12 @@ constexpr bool kTailRecNt = XDP_TAIL_REC_NT != 0;
 #define XDP_TAIL_VERDICT_NT 0
 #endif
 constexpr bool kTailVerdictNt = XDP_TAIL_VERDICT_NT != 0;
+/* bulk frames' provisional verdicts stored by the tile loop, the bulk pass
+ * storing only those that change (fast_tile; build knob) */
+#ifndef XDP_BULK_VERDICT_TILE
+#define XDP_BULK_VERDICT_TILE 1
+#endif
+constexpr bool kBulkVerdictTile = XDP_BULK_VERDICT_TILE != 0;
 /* A 44-byte network_tuple at a dword-aligned address: two 16-byte stores
  * and a 12-byte one (global stores need only dword alignment) */
 __device__ __forceinline__ void store_tuple44(uint8_t *p, const uint32_t (&t)[11])
@@ -1609,10 +1615,15 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 			store_tuple44(a.tup + 44 * i, t);
 		}
 		const uint8_t vd = echo_tx ? XDPGPU_TX : drop ? XDPGPU_DROP : XDPGPU_REDIRECT;
-		if constexpr (kTailVerdictNt)
-			__builtin_nontemporal_store(vd, a.verdict + i);
-		else
-			a.verdict[i] = vd;
+		/* the tile stored the provisional verdict (kBulkVerdictTile) */
+		const uint8_t vprov = (a.flags & XDPGPU_CFG_VERIFY_CSUM) && l3_bad ? XDPGPU_DROP
+										 : XDPGPU_REDIRECT;
+		if (GEN || !kBulkVerdictTile || vd != vprov) {
+			if constexpr (kTailVerdictNt)
+				__builtin_nontemporal_store(vd, a.verdict + i);
+			else
+				a.verdict[i] = vd;
+		}
 		my_bytes += dv.z;
 	}
 	if (a.stats) {
@@ -1842,7 +1853,8 @@ __device__ __forceinline__ void store_tile(const RxArgs &a, const TileOut &o)
 	const __amdgpu_buffer_rsrc_t rv =
 		__builtin_amdgcn_make_buffer_rsrc(a.verdict + o.t0, 0, kWave, kFmt);
 	__builtin_amdgcn_raw_buffer_store_b8((uint8_t)o.verdict, rv,
-					     (fl & 1) ? o.li : kOff, 0, XDP_VERDICT_AUX);
+					     (fl & (kBulkVerdictTile ? 3 : 1)) ? o.li : kOff, 0,
+					     XDP_VERDICT_AUX);
 	const bool out = fl & 2;
 	/* a missing output: a resource of no records over the verdicts */
 	const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
@@ -2089,6 +2101,13 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 		(fast && absent ? XDPGPU_F_L4_ABSENT : 0u) |
 		(protov << 8) | (l3 << 16) | (nv << 24);
 	rec.w = (fast ? l4v : c4v) | (clv << 16);
+	/* the verdict stored with the tile: a fast frame's, and a bulk frame's
+	 * provisional one (DROP for a bad IPv4 header under verification,
+	 * else REDIRECT), which the bulk pass overwrites only when the frame's
+	 * final verdict differs (a bad L4 checksum, an echo reply, ABORTED):
+	 * the tile's verdict bytes are one coalesced store, the bulk pass's
+	 * scattered single bytes partial-line writes (kBulkVerdictTile) */
+	const bool vdrop = fast ? drop : ((a.flags & XDPGPU_CFG_VERIFY_CSUM) && !l3_ok);
 	const uint32_t vid = nv ? (bswap16(F[3] >> 16) & 0x0fff) : 0u;
 	const uint4 tv4 = make_uint4(sa, da, ports, proto | (2u << 8) | (vid << 16));
 	const bool out = fast || bulk;
@@ -2098,9 +2117,9 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 			 * bases, per-lane offsets of at most 64 records */
 			const uint64_t t0 = uniform_u64(i);
 			uint32_t li = (uint32_t)(i - t0);
-			if (fast)
+			if (fast || kBulkVerdictTile)
 				st_asm_sb8(a.verdict + t0, li,
-					   drop ? XDPGPU_DROP : XDPGPU_REDIRECT);
+					   vdrop ? XDPGPU_DROP : XDPGPU_REDIRECT);
 			if (a.res)
 				st_asm_sb128(a.res + t0, 16 * li, rec, true);
 			if (a.tup) {
@@ -2124,7 +2143,7 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 		to->t0 = uniform_u64(i);   /* all lanes active: lane 0 */
 		to->li = (uint32_t)(i - to->t0);
 		to->fl = (fast ? 1u : 0u) | (out ? 2u : 0u) | (v6 ? 4u : 0u);
-		to->verdict = drop ? XDPGPU_DROP : XDPGPU_REDIRECT;
+		to->verdict = vdrop ? XDPGPU_DROP : XDPGPU_REDIRECT;
 		/* an IPv6 frame's 16-byte tuple: no addresses, its ports (none
 		 * for ICMPv6), ipv 10 (emit_tuple's layout) */
 		to->sa = v6 ? 0u : sa;
