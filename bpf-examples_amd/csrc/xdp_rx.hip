@@ -2510,6 +2510,8 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 	const uint64_t per = (own + nb - 1) / nb;
 	const uint32_t order = a.order;
 	const uint64_t rot = 1;
+	/* order 0's XCD shift: block b takes the tiles t = b - xs mod nb */
+	const uint64_t xs = order == 0 ? a.xshift % nb : 0;
 	auto tile_of = [&](uint64_t k) -> uint64_t {
 		uint64_t t, lim = own;
 		if (order == 1) {
@@ -2520,7 +2522,7 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 		} else if (order == 2) {
 			t = k * nb + (rb + k * rot) % nb;
 		} else {
-			t = rb + k * nb;
+			t = (rb + nb - xs) % nb + k * nb;
 		}
 		return t < lim ? t : ntiles;
 	};
@@ -2683,16 +2685,19 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 		 * heads + 2h and the next, on the same XCD as in its own-tile
 		 * order (own is a multiple of 2 heads) */
 		const bool pairs = order == 3;
+		/* with order 0's XCD shift, head h takes the residue h - xs, which
+		 * the shifted own order puts on h's XCD */
+		const uint64_t hr = (h + heads - xs % heads) % heads;
 		auto first_of = [&](uint32_t v) -> uint64_t {
 			const uint64_t t = own + (uint64_t)__builtin_amdgcn_readfirstlane(v) * 2 * heads +
-					   (pairs ? 2 * h : h);
+					   (pairs ? 2 * h : hr);
 			return t < ntiles ? t : ntiles;
 		};
 		auto second_of = [&](uint64_t t) -> uint64_t {
 			const uint64_t u = t + (pairs ? 1 : heads);
 			return u < ntiles ? u : ntiles;
 		};
-		uint64_t c0 = own + (pairs ? 2 * h : h) < ntiles ? first_of(claim2()) : ntiles;
+		uint64_t c0 = own + (pairs ? 2 * h : hr) < ntiles ? first_of(claim2()) : ntiles;
 		if (c0 < ntiles) {
 			/* per pair: descriptors, windows and the next claim in
 			 * flight, one wait, then the two tiles.  (Pipelined over
@@ -3245,6 +3250,8 @@ hipError_t launch_rx(const RxArgs &a, uint32_t window, uint32_t max_blocks,
 		       !((tune >> 18) & 1);
 		/* bits 19-20: the tile order (xdp_rx_db_kernel) */
 		b.order = (tune >> 19) & 3;
+		/* bits 25-27: order 0's XCD shift (diagnostic) */
+		b.xshift = (tune >> 25) & 7;
 		return launch_db(b, max_blocks, stream, ev);
 	}
 	if (window == 128)

@@ -151,6 +151,10 @@ struct RxArgs {
 				    * includes untagged IPv6/UDP           */
 	uint32_t order;            /* set by the launcher: xdp_rx_db_kernel's
 				    * tile order (cfg.tune bits 19-20)     */
+	uint32_t xshift;           /* set by the launcher: order 0's tile t
+				    * to block (t + xshift) mod nb, i.e. to
+				    * XCD (t + xshift) mod 8 (cfg.tune bits
+				    * 25-27; diagnostic)                   */
 	/* xdp_rx_db_kernel's shared tiles: the last steal_tiles tiles of the
 	 * batch are claimed at run time from kStealHeads global counters by
 	 * any block done with its own (set by the launcher; 0: none) */
