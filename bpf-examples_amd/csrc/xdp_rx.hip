@@ -1295,6 +1295,13 @@ constexpr bool kTailVerdictNt = XDP_TAIL_VERDICT_NT != 0;
 #define XDP_BULK_VERDICT_TILE 1
 #endif
 constexpr bool kBulkVerdictTile = XDP_BULK_VERDICT_TILE != 0;
+/* ARP and NDP (PASS) and the common parse failures (ABORTED) decided in the
+ * tile loop (fast_tile's "quick" frames; build knob), so that a pool of
+ * otherwise fast frames leaves the tail no exception batch */
+#ifndef XDP_QUICK
+#define XDP_QUICK 1
+#endif
+constexpr bool kQuick = XDP_QUICK != 0;
 /* A 44-byte network_tuple at a dword-aligned address: two 16-byte stores
  * and a 12-byte one (global stores need only dword alignment) */
 __device__ __forceinline__ void store_tuple44(uint8_t *p, const uint32_t (&t)[11])
@@ -1873,8 +1880,10 @@ __device__ __forceinline__ void store_tile(const RxArgs &a, const TileOut &o)
 	 * here */
 	const bool tout = out && !((fl & 4) && net);
 	const uint32_t b = tout ? tb * o.li : kOff;
-	const uint32_t ipv = (fl & 4) ? 10u : 2u;
-	const v4u_t w0 = net ? (v4u_t){0u, 0u, 0xffff0000u, o.sa}
+	/* a quick frame's tuple (fl bit 3): all zero */
+	const uint32_t zq = (fl & 8) ? 0u : ~0u;
+	const uint32_t ipv = ((fl & 4) ? 10u : 2u) & zq;
+	const v4u_t w0 = net ? (v4u_t){0u, 0u, 0xffff0000u & zq, o.sa}
 			     : (v4u_t){o.sa, o.da, o.ports, o.proto | (ipv << 8) | (o.vid << 16)};
 	/* 16-byte tuples: whole lines, streamed (nt).  44-byte tuples: the
 	 * lanes' 16-byte pieces straddle lines that other stores of the tile
@@ -1885,9 +1894,10 @@ __device__ __forceinline__ void store_tile(const RxArgs &a, const TileOut &o)
 	} else {
 		__builtin_amdgcn_raw_buffer_store_b128(w0, rt, b, 0, XDP_TUP4_AUX);
 	}
-	__builtin_amdgcn_raw_buffer_store_b128((v4u_t){o.ports & 0xffff, 0u, 0u, 0xffff0000u},
+	__builtin_amdgcn_raw_buffer_store_b128((v4u_t){o.ports & 0xffff, 0u, 0u, 0xffff0000u & zq},
 					       rt, net && tout ? b + 16 : kOff, 0, 0);
-	__builtin_amdgcn_raw_buffer_store_b96((v3u_t){o.da, o.ports >> 16, o.proto | (2u << 16)},
+	__builtin_amdgcn_raw_buffer_store_b96((v3u_t){o.da, o.ports >> 16,
+						      o.proto | ((2u << 16) & zq)},
 					      rt, net && tout ? b + 32 : kOff, 0, 0);
 }
 
@@ -2003,13 +2013,58 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 		bulk = bulk | v6;
 	}
 
+	/* Quick frames (kQuick, the per-CU kernel): verdicts parse_lane
+	 * decides from bytes the window holds, with all-zero records and
+	 * tuples (generic_batch's outputs for ABORTED and PASS):
+	 *  - a runt (len < 14: parse_ethhdr_vlan fails, in bounds or not);
+	 *  - for a staged frame of at least 64 bytes (its tags all consumed,
+	 *    every byte read below lies in the frame and the window):
+	 *    ARP behind 0..2 tags (PASS); untagged-or-tagged IPv6 with no
+	 *    extension header and an ICMPv6 type 133..137 (NDP: PASS); IPv6
+	 *    with a version other than 6 (ABORTED); IPv4 whose header
+	 *    fails parse_iphdr (version, ihl, header or tot_len past the
+	 *    frame, tot_len below the header: ABORTED), and with a 20-byte
+	 *    header, not a later fragment, whose UDP length, TCP data offset
+	 *    or ICMP length fails parse_udphdr / parse_tcphdr /
+	 *    parse_icmphdr or runs past tot_len (ABORTED).
+	 * Every other frame the fast shape does not take stays an exception. */
+	bool quick = false;
+	uint32_t qv = XDPGPU_ABORTED;
+	if constexpr (!LQ && kQuick) {
+		const uint32_t et = r[3] & 0xffff;
+		const bool big = (!a.force_generic) & staged & (len >= 64);
+		const bool arp = big & (et == 0x0608u);
+		const uint32_t vihl = (r[3] >> 16) & 0xff, hl = (vihl & 15) * 4;
+		const bool hdr_bad = ((vihl >> 4) != 4) | (hl < 20) | (l3 + hl > len) |
+				     (tot < hl) | (l3 + tot > len);
+		const uint32_t fo = bswap16(r[5] & 0xffff) & 0x3fff;
+		const bool fragb = fo != 0, nonfirst = (fo & 0x1fff) != 0;
+		const uint32_t ulen = bswap16(r[9] >> 16);
+		const bool udp_bad = (proto == 17) & ((ulen < 8) | (!fragb & (l4 + ulen > l3 + tot)));
+		const bool tcp_bad = (proto == 6) &
+				     ((thl < 20) | (l4 + thl > len) | (!fragb & (tot - 20 < thl)));
+		const bool icmp_bad = (proto == 1) & !fragb & (tot - 20 < 8);
+		const bool abort4 = big & (et == 0x0008u) &
+				    (hdr_bad | ((hl == 20) & !nonfirst & (udp_bad | tcp_bad | icmp_bad)));
+		const bool ip6 = big & (et == 0xdd86u);
+		const bool ver6 = ((r[3] >> 20) & 0xf) == 6;
+		const uint32_t ty6 = (r[13] >> 16) & 0xff;
+		const bool ndp = ip6 & ver6 & ((r[5] & 0xff) == 58) & (ty6 >= 133) & (ty6 <= 137) &
+				 (len >= l3 + 48);
+		const bool abort6 = ip6 & !ver6;
+		const bool runt = (!a.force_generic) & (len < 14);
+		quick = active & !fast & !bulk & (runt | arp | ndp | abort4 | abort6);
+		qv = (arp | ndp) ? XDPGPU_PASS : XDPGPU_ABORTED;
+	}
+
 	/* 3. defer the frames of other shapes to the exception list and
 	 * the long ones to the bulk list of this wave */
 	if constexpr (LQ) {
 		defer_append(active && !fast && !bulk, i, w.xq, w.xq_n, w.xl, w.xout, lane);
 		defer_append(bulk, i, w.bq, w.bq_n, w.bl, w.bout, lane);
 	} else {
-		defer_direct(active && !fast && !bulk, i, w.xl, w.lcount, lane, a.xregion);
+		defer_direct(active && !fast && !bulk && !quick, i, w.xl, w.lcount, lane,
+			     a.xregion);
 		defer_direct(bulk, i, w.bl, w.lcount + 1, lane, a.xregion);
 	}
 
@@ -2142,16 +2197,18 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 		/* the outputs, stored by the next step (store_tile) */
 		to->t0 = uniform_u64(i);   /* all lanes active: lane 0 */
 		to->li = (uint32_t)(i - to->t0);
-		to->fl = (fast ? 1u : 0u) | (out ? 2u : 0u) | (v6 ? 4u : 0u);
-		to->verdict = vdrop ? XDPGPU_DROP : XDPGPU_REDIRECT;
+		to->fl = (fast || quick ? 1u : 0u) | (out || quick ? 2u : 0u) | (v6 ? 4u : 0u) |
+			 (quick ? 8u : 0u);
+		to->verdict = quick ? qv : vdrop ? XDPGPU_DROP : XDPGPU_REDIRECT;
 		/* an IPv6 frame's 16-byte tuple: no addresses, its ports (none
-		 * for ICMPv6), ipv 10 (emit_tuple's layout) */
-		to->sa = v6 ? 0u : sa;
-		to->da = v6 ? 0u : da;
-		to->ports = v6 ? (i6 ? 0u : (r[13] >> 16) | (r[14] << 16)) : ports;
-		to->proto = v6 ? nh6 : proto;
-		to->vid = vid;
-		to->rec = rec;
+		 * for ICMPv6), ipv 10 (emit_tuple's layout); a quick frame's:
+		 * zero */
+		to->sa = v6 || quick ? 0u : sa;
+		to->da = v6 || quick ? 0u : da;
+		to->ports = quick ? 0u : v6 ? (i6 ? 0u : (r[13] >> 16) | (r[14] << 16)) : ports;
+		to->proto = quick ? 0u : v6 ? nh6 : proto;
+		to->vid = quick ? 0u : vid;
+		to->rec = quick ? make_uint4(0, 0, 0, 0) : rec;
 		if constexpr (V6 && kTup6Tile) {
 			/* an IPv6 frame's network_tuple now, from the window
 			 * (the deferred stores keep four words of a tuple) */
@@ -2159,10 +2216,15 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 				store_tuple44(a.tup + 44 * i, key);
 		}
 	}
-	w.my_bytes += fast ? len : 0;
+	w.my_bytes += fast || quick ? len : 0;
 	/* counters (wave-uniform: ballots outside divergent code) */
 	if (a.stats) {
-		w.cnt[CNT_FRAMES] += __popcll(__ballot(fast));
+		w.cnt[CNT_FRAMES] += __popcll(__ballot(fast || quick));
+		if constexpr (!LQ && kQuick) {
+			w.cnt[CNT_VERDICT0 + XDPGPU_PASS] += __popcll(__ballot(quick && qv == XDPGPU_PASS));
+			w.cnt[CNT_VERDICT0 + XDPGPU_ABORTED] +=
+				__popcll(__ballot(quick && qv == XDPGPU_ABORTED));
+		}
 		w.cnt[CNT_VERDICT0 + XDPGPU_DROP] += __popcll(__ballot(fast && drop));
 		w.cnt[CNT_VERDICT0 + XDPGPU_REDIRECT] += __popcll(__ballot(fast && !drop));
 		w.cnt[CNT_L3_BAD] += __popcll(__ballot(fast && !l3_ok));
