@@ -96,3 +96,23 @@ def test_reference_routine_leg_vs_oracle(kind, size, n, flags, iv, fmt):
     assert res.tobytes() == ores.tobytes()
     assert tup[: len(otup)].tobytes() == otup.tobytes()
     assert np.array_equal(u, umem)
+
+
+def test_bench_cpu_baseline_is_the_reference_routines():
+    """bench.py's cpu_baseline: with oracle/_ref present (built in this
+    container), the value is the reference headers' routines' rate (kind
+    "reference"), their outputs equal the port's, and the port's rate is
+    reported beside it."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if not os.path.exists(os.path.join(root, "oracle", "_ref", "libref.so")):
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    sys.path.insert(0, root)
+    import bench
+    umem, descs, _ = xdpgpu.pool_generate(1 << 18, xdpgpu.POOL_UDP4, 64, 0x5EED0002)
+    cb = bench.cpu_baseline(umem, descs, xdpgpu.CFG_DEFAULT, xdpgpu.TUPLE_V4, budget_s=0.2)
+    assert cb["kind"] == "reference"
+    assert cb["value"] == cb["reference_mpps"] > 0
+    assert cb["port_mpps"] > 0 and cb["outputs_match_oracle"]
+    assert cb["reference_outputs_match_leg"]
+    json.dumps(cb)
