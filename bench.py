@@ -69,7 +69,10 @@ def to_dev(a: np.ndarray, dev, pad: int = 64) -> torch.Tensor:
 def time_device(ctx, d_umem, usize, d_desc, n, d_v, d_res, d_tup, stream,
                 steps, warmup, world):
     """W untimed + K timed launches between barrier + synchronize; returns
-    wall seconds."""
+    wall seconds.  The launches go to the context's own stream (stream
+    None), as an RX loop over one context does: a caller's stream costs
+    the library an event record per launch (xdpgpu.cpp scratch_leave)."""
+    torch.cuda.synchronize()   # the inputs, made on torch's streams
     for _ in range(warmup):
         ctx.process_dev(d_umem, usize, d_desc, n, d_v, d_res, d_tup, stream)
     torch.cuda.synchronize()
@@ -271,9 +274,9 @@ def side_run(ctx, tctx, dev, stream, n, kind, size, seed, fmt, steps, label, bpf
     g_res = torch.empty(n * 16, dtype=torch.uint8, device=dev)
     g_tup = torch.empty(n * tb, dtype=torch.uint8, device=dev)
     w = time_device(ctx, g_umem, u.nbytes, g_desc, n, g_v, g_res, g_tup,
-                    stream, steps, 2, 1)
+                    None, steps, 2, 1)
     kt = kernel_breakdown(tctx, g_umem, u.nbytes, g_desc, n, g_v, g_res, g_tup,
-                          stream, steps)
+                          None, steps)
     ok = bool(np.array_equal(g_v.cpu().numpy(), ex))
     algo = bpf_fn(ds)
     out = {"workload": label, "frames": n,
@@ -469,7 +472,7 @@ def frags_run(dev, stream, n, steps, local, size=9000, chunk=4096):
     g_tup = torch.empty(m * 16, dtype=torch.uint8, device=dev)
     with xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT | xdpgpu.CFG_FRAGS, 0, xdpgpu.TUPLE_V4,
                        64) as g:
-        w = time_device(g, g_umem, u.nbytes, g_desc, m, g_v, g_res, g_tup, stream, steps, 2, 1)
+        w = time_device(g, g_umem, u.nbytes, g_desc, m, g_v, g_res, g_tup, None, steps, 2, 1)
     ok = bool(np.array_equal(g_v.cpu().numpy(), ex[frame_of]))
     t = w / steps
     out = {"workload": f"{n} x {size}B IPv4/UDP packets in {chunk}B fragments "
@@ -578,9 +581,9 @@ def main():
     stream = torch.cuda.Stream(dev)
 
     wall = time_device(ctx, d_umem, umem.nbytes, d_desc, n, d_v, d_res, d_tup,
-                       stream, args.steps, args.warmup, world)
+                       None, args.steps, args.warmup, world)
     kt = kernel_breakdown(tctx, d_umem, umem.nbytes, d_desc, n, d_v, d_res, d_tup,
-                          stream, args.steps)
+                          None, args.steps)
     kms = kt["total_ms"]
     # correctness spot check of the timed outputs against the generator
     v = d_v.cpu().numpy()

@@ -71,6 +71,7 @@ workload() {
 	synproxy) echo "python3 bench.py --no-cpu --legs synproxy --steps 5 --warmup 2" ;;
 	echo) echo "python3 bench.py --no-cpu --legs echo --steps 5 --warmup 2" ;;
 	bench) echo "python3 bench.py --no-cpu --no-secondary --steps 20" ;;
+	bench50) echo "python3 bench.py --no-cpu --no-secondary --steps 50" ;;
 	*) echo "unknown workload $1" >&2; exit 2 ;;
 	esac
 }
