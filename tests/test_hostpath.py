@@ -250,3 +250,33 @@ def test_queue_stats():
         c.close()
     assert xdpgpu.queue_stats(qa) == a
     assert xdpgpu.queue_stats(qb) == b
+
+
+def test_process_dev_own_and_caller_streams():
+    """Launches alternating between the context's own stream (stream None:
+    the scratch event is recorded only when another stream comes) and two
+    caller streams: every batch's outputs equal the oracle's."""
+    from test_gpu_parity import to_dev
+    pools = [xdpgpu.pool_generate(150000, xdpgpu.POOL_IMIX, 64, s) for s in (43, 44, 45)]
+    want = [oracle.process(u.copy(), d, 0x5, 0, 2)[:3] for u, d, _ in pools]
+    streams = [None, torch.cuda.Stream(), None, torch.cuda.Stream(), None]
+    with xdpgpu.XdpGpu(0, 0x5, 0, xdpgpu.TUPLE_NET) as ctx:
+        bufs = []
+        for u, d, _ in pools:
+            n = len(d)
+            bufs.append((to_dev(u), u.nbytes, to_dev(d, 16), n,
+                         torch.empty(n, dtype=torch.uint8, device="cuda:0"),
+                         torch.empty(n * 16, dtype=torch.uint8, device="cuda:0"),
+                         torch.empty(n * 44, dtype=torch.uint8, device="cuda:0")))
+        torch.cuda.synchronize()
+        for rep in range(10):
+            k = rep % 3
+            du, us, dd, n, dv, dr, dt = bufs[k]
+            ctx.process_dev(du, us, dd, n, dv, dr, dt, stream=streams[rep % len(streams)])
+        torch.cuda.synchronize()
+        for k in range(3):
+            du, us, dd, n, dv, dr, dt = bufs[k]
+            wv, wres, wtup = want[k]
+            np.testing.assert_array_equal(dv.cpu().numpy(), wv)
+            np.testing.assert_array_equal(dr.cpu().numpy(), wres.view(np.uint8).reshape(-1))
+            np.testing.assert_array_equal(dt.cpu().numpy(), wtup)
