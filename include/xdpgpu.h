@@ -217,7 +217,10 @@ void xdpgpu_host_free(void *p);
  * round_up(umem_size, 16) (the kernel loads 16-byte aligned chunks and
  * masks what lies past umem_size).  Launches of one context on different
  * streams are ordered by the context (they share its scratch); launches
- * on one stream run back to back.  Scratch per context slot: deferral
+ * on one stream run back to back (on the context's own stream with no
+ * event between them: back-to-back launches on one caller stream each
+ * record one, as the caller's stream may not outlive the next call).
+ * Scratch per context slot: deferral
  * lists of 3 n + 5.2 M entries (24 bytes each; about 1.3 GB at n = 16 M),
  * grown on first use of a larger n. */
 int xdpgpu_process_dev(struct xdpgpu_ctx *ctx, void *d_umem,
