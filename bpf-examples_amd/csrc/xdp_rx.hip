@@ -2538,7 +2538,7 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 	const uint64_t wgid = rb * kCuWaves + wid;
 
 	if (threadIdx.x == 0) {
-		ctl[0] = ctl[1] = ctl[2] = ctl[3] = ctl[4] = ctl[5] = ctl[6] = 0;
+		ctl[0] = ctl[1] = ctl[2] = ctl[3] = ctl[4] = ctl[5] = ctl[6] = ctl[7] = 0;
 		a.ycount[rb] = 0;      /* filled by the exception pass */
 	}
 	/* the next launch's shared-tile counters (this launch's set was
@@ -2726,71 +2726,91 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 	 * whichever are done first. */
 	if (shared) {
 		const uint64_t heads = min((uint64_t)kStealHeads, nb);
-		const uint64_t h = rb % heads;
-		uint32_t *ctr = a.steal + (a.steal_set * kStealHeads + h) * kStealStride;
 		const uint32_t cap = (uint32_t)steal_cap(shared, nb);
 		lds_dma_landed();   /* the loop's last DMAs into win0/dsl0 */
-		/* A claim v is head h's tiles 2v and 2v + 1, the j-th being
-		 * own + j heads + h, so that a tile goes to the XCD (b mod 8)
-		 * the own-tile order gives it; the launcher makes own a
-		 * multiple of the heads.  (A tile's XCD matters: an order that
-		 * moved the blocks through all positions of each round ran 11 %
-		 * slower.)  claim() reserves two of the block's slots first and
-		 * returns lane 0's claim (no claim over the cap). */
-		auto claim2 = [&]() -> uint32_t {
-			uint32_t v = 0x7fffffffu;
-			if (lds_fetch_add(&ctl[6], 2, lane) + 2 <= cap && lane == 0)
-				v = atomicAdd(ctr, 1u);
-			return v;
-		};
-		/* the pair order (3): a claim is the adjacent tiles own + 2v
-		 * heads + 2h and the next, on the same XCD as in its own-tile
-		 * order (own is a multiple of 2 heads) */
-		const bool pairs = order == 3;
-		/* with order 0's XCD shift, head h takes the residue h - xs, which
-		 * the shifted own order puts on h's XCD */
-		const uint64_t hr = (h + heads - xs % heads) % heads;
-		auto first_of = [&](uint32_t v) -> uint64_t {
-			const uint64_t t = own + (uint64_t)__builtin_amdgcn_readfirstlane(v) * 2 * heads +
-					   (pairs ? 2 * h : hr);
-			return t < ntiles ? t : ntiles;
-		};
-		auto second_of = [&](uint64_t t) -> uint64_t {
-			const uint64_t u = t + (pairs ? 1 : heads);
-			return u < ntiles ? u : ntiles;
-		};
-		uint64_t c0 = own + (pairs ? 2 * h : hr) < ntiles ? first_of(claim2()) : ntiles;
-		if (c0 < ntiles) {
-			/* per pair: descriptors, windows and the next claim in
-			 * flight, one wait, then the two tiles.  (Pipelined over
-			 * pairs, each buffer refilled as soon as read: 0.3361 vs
-			 * 0.3250 ms on config 2, one process.) */
-			for (;;) {
-				const uint64_t c1 = second_of(c0);
-				const uint4 d0 = *reinterpret_cast<const uint4 *>(a.desc + desc_at(c0));
-				const uint4 d1 = *reinterpret_cast<const uint4 *>(a.desc + desc_at(c1));
-				issue_win(d0, true, win0);
-				issue_win(d1, c1 < ntiles, win1);
-				const uint32_t vn = claim2();
-				uint32_t F[18];
-				uint4 dn;
-				lds_dma_landed();
-				read_tile_db<10>(win0, dsl0, lane, F, dn);
-				const uint64_t i0 = c0 * kWave + lane;
-				fast_tile<false, true, V6>(a, F, d0, i0, i0 < nfr, dma, lane, w, &pend);
-				store_tile(a, pend);
-				if (c1 >= ntiles)
-					break;
-				read_tile_db<10>(win1, dsl1, lane, F, dn);
-				const uint64_t i1 = c1 * kWave + lane;
-				fast_tile<false, true, V6>(a, F, d1, i1, i1 < nfr, dma, lane, w, &pend);
-				store_tile(a, pend);
-				c0 = first_of(vn);
-				if (c0 >= ntiles)
-					break;
+		/* a.partner heads in turn: with its own head empty, the wave goes
+		 * on with head h ^ 4, whose blocks run on the XCD 4 away (the
+		 * other half of the chip), until that is empty too (the default,
+		 * 2); with 8, then h ^ 2, h ^ 6, h ^ 1, ... (every XCD's head of
+		 * its set).  The first wave of the block to find a head empty
+		 * tells the others (bit r of ctl[7]).  Within one process the
+		 * two halves of the chip drain their heads 12 us apart, the
+		 * same half last in every launch (which half changes with the
+		 * buffers' placement; tools/stamps.py per_launch); the partner
+		 * head evens them: config 2 0.2969 / 0.2989 vs 0.3007 / 0.3032
+		 * ms without, in one process; every XCD's heads 0.3058 / 0.3079
+		 * (the XCDs of one half drain together, and a move there only
+		 * adds a late pair). */
+		const int rounds = heads % 8 == 0 && a.partner > 1 ? (int)a.partner : 1;
+		for (int round = 0; round < rounds; ++round) {
+			if (round && (__builtin_amdgcn_readfirstlane(ctl[7]) >> round) & 1)
+				continue;
+			const uint64_t h = (rb % heads) ^ ((0x73516240u >> (4 * round)) & 7);
+			uint32_t *ctr = a.steal + (a.steal_set * kStealHeads + h) * kStealStride;
+			/* A claim v is head h's tiles 2v and 2v + 1, the j-th being
+			 * own + j heads + h, so that a tile goes to the XCD (b mod 8)
+			 * the own-tile order gives it; the launcher makes own a
+			 * multiple of the heads.  (A tile's XCD matters: an order that
+			 * moved the blocks through all positions of each round ran 11 %
+			 * slower.)  claim() reserves two of the block's slots first and
+			 * returns lane 0's claim (no claim over the cap). */
+			auto claim2 = [&]() -> uint32_t {
+				uint32_t v = 0x7fffffffu;
+				if (lds_fetch_add(&ctl[6], 2, lane) + 2 <= cap && lane == 0)
+					v = atomicAdd(ctr, 1u);
+				return v;
+			};
+			/* the pair order (3): a claim is the adjacent tiles own + 2v
+			 * heads + 2h and the next, on the same XCD as in its own-tile
+			 * order (own is a multiple of 2 heads) */
+			const bool pairs = order == 3;
+			/* with order 0's XCD shift, head h takes the residue h - xs, which
+			 * the shifted own order puts on h's XCD */
+			const uint64_t hr = (h + heads - xs % heads) % heads;
+			auto first_of = [&](uint32_t v) -> uint64_t {
+				const uint64_t t = own + (uint64_t)__builtin_amdgcn_readfirstlane(v) * 2 * heads +
+						   (pairs ? 2 * h : hr);
+				return t < ntiles ? t : ntiles;
+			};
+			auto second_of = [&](uint64_t t) -> uint64_t {
+				const uint64_t u = t + (pairs ? 1 : heads);
+				return u < ntiles ? u : ntiles;
+			};
+			uint64_t c0 = own + (pairs ? 2 * h : hr) < ntiles ? first_of(claim2()) : ntiles;
+			if (round && c0 >= ntiles && lane == 0)
+				atomicOr(&ctl[7], 1u << round);
+			if (c0 < ntiles) {
+				/* per pair: descriptors, windows and the next claim in
+				 * flight, one wait, then the two tiles.  (Pipelined over
+				 * pairs, each buffer refilled as soon as read: 0.3361 vs
+				 * 0.3250 ms on config 2, one process.) */
+				for (;;) {
+					const uint64_t c1 = second_of(c0);
+					const uint4 d0 = *reinterpret_cast<const uint4 *>(a.desc + desc_at(c0));
+					const uint4 d1 = *reinterpret_cast<const uint4 *>(a.desc + desc_at(c1));
+					issue_win(d0, true, win0);
+					issue_win(d1, c1 < ntiles, win1);
+					const uint32_t vn = claim2();
+					uint32_t F[18];
+					uint4 dn;
+					lds_dma_landed();
+					read_tile_db<10>(win0, dsl0, lane, F, dn);
+					const uint64_t i0 = c0 * kWave + lane;
+					fast_tile<false, true, V6>(a, F, d0, i0, i0 < nfr, dma, lane, w, &pend);
+					store_tile(a, pend);
+					if (c1 >= ntiles)
+						break;
+					read_tile_db<10>(win1, dsl1, lane, F, dn);
+					const uint64_t i1 = c1 * kWave + lane;
+					fast_tile<false, true, V6>(a, F, d1, i1, i1 < nfr, dma, lane, w, &pend);
+					store_tile(a, pend);
+					c0 = first_of(vn);
+					if (c0 >= ntiles)
+						break;
+				}
 			}
+			lds_dma_landed();   /* a claim left outstanding at a break */
 		}
-		lds_dma_landed();   /* a claim left outstanding at a break */
 	}
 	STAMP(wgid, lane, 1);
 
@@ -3314,6 +3334,11 @@ hipError_t launch_rx(const RxArgs &a, uint32_t window, uint32_t max_blocks,
 		b.order = (tune >> 19) & 3;
 		/* bits 25-27: order 0's XCD shift (diagnostic) */
 		b.xshift = (tune >> 25) & 7;
+		/* bits 28-29: after its own head, a wave claims shared tiles of
+		 * 0: the partner head in the other half of the chip (default),
+		 * 1: no other head, 2: the heads of every XCD in turn, 3: as 0 */
+		const uint32_t pm = (tune >> 28) & 3;
+		b.partner = pm == 1 ? 1 : pm == 2 ? 8 : 2;
 		return launch_db(b, max_blocks, stream, ev);
 	}
 	if (window == 128)

@@ -155,6 +155,9 @@ struct RxArgs {
 				    * to block (t + xshift) mod nb, i.e. to
 				    * XCD (t + xshift) mod 8 (cfg.tune bits
 				    * 25-27; diagnostic)                   */
+	uint32_t partner;          /* set by the launcher: the heads a wave
+				    * claims shared tiles from, its own first
+				    * (1, 2 or 8; cfg.tune bits 28-29)     */
 	/* xdp_rx_db_kernel's shared tiles: the last steal_tiles tiles of the
 	 * batch are claimed at run time from kStealHeads global counters by
 	 * any block done with its own (set by the launcher; 0: none) */

@@ -35,7 +35,7 @@ def to_dev(a: np.ndarray, pad: int = 64):
 # (bits 19-20) and shared-tile fractions (bits 21-23: none, 4/16, 8/16, all,
 # 12/16; the default is 12/16), and an XCD shift of the default order (bits
 # 25-27)
-TUNES = [0, 1 << 15, 512, 512 | 256, 6 | (3 << 10), 1 << 10, 1 << 19, 2 << 19, 3 << 19, 1 << 21, 2 << 21, 3 << 21, 4 << 21, 5 << 21, 3 << 25]
+TUNES = [0, 1 << 15, 512, 512 | 256, 6 | (3 << 10), 1 << 10, 1 << 19, 2 << 19, 3 << 19, 1 << 21, 2 << 21, 3 << 21, 4 << 21, 5 << 21, 3 << 25, 1 << 28, 2 << 28]
 
 
 def run_dev(umem, descs, flags=0x5, initval=0, fmt=1, window=64, tune=0):

@@ -32,11 +32,23 @@ d_res = torch.empty(n * 16, dtype=torch.uint8, device=dev)
 d_tup = torch.empty(n * 44, dtype=torch.uint8, device=dev)
 ctx = xdpgpu.XdpGpu(0, xdpgpu.CFG_DEFAULT, 0, fmt, 64, tune=tune)
 st = np.zeros(8 * 8192, np.uint64)
-for rep in range(6):
+reps = int(os.environ.get("STAMPS_REPS", "6"))
+per_rep = []   # per launch: each XCC's median and last loop end (us)
+for rep in range(reps):
     st[:] = 0
     ctx.process_dev(d_umem, umem.nbytes, d_desc, n, d_v, d_res, d_tup)
     torch.cuda.synchronize()
     lib.xdpgpu_stamps_read(st.ctypes.data)
+    r4 = st.reshape(-1, 8)
+    lv = r4[:, 0] > 0
+    rs = r4[lv][:, [0, 1, 2]].astype(np.int64)
+    rt = (rs - rs[:, 0].min()) / 100.0
+    xc = ((r4[lv, 3] >> 32) & 0xF).astype(int)
+    per_rep.append({"xcc_loop_end_median": [round(float(np.median(rt[xc == k, 1])), 1)
+                                            for k in range(8)],
+                    "xcc_loop_end_max": [round(float(rt[xc == k, 1].max()), 1)
+                                         for k in range(8)],
+                    "end_max": round(float(rt[:, 2].max()), 1)})
 s4 = st.reshape(-1, 8)
 live = s4[:, 0] > 0
 hw = s4[live, 3]
@@ -100,4 +112,5 @@ for c in cus:
                 ends_by_age[r].append(v)
 out["loop_end_by_age_on_simd"] = [round(float(np.median(x)), 1) if x else None
                                   for x in ends_by_age]
+out["per_launch"] = per_rep
 print(json.dumps(out))
