@@ -1336,6 +1336,12 @@ constexpr bool kTup6Tile = XDP_TUP6_TILE != 0;
 #define XDP_TAIL_ADAPT 1
 #endif
 constexpr bool kTailAdapt = XDP_TAIL_ADAPT != 0;
+/* Batches of ranges within 64 bytes streamed in one step (stream_short;
+ * build knob) */
+#ifndef XDP_TAIL_SHORT
+#define XDP_TAIL_SHORT 1
+#endif
+constexpr bool kTailShort = XDP_TAIL_SHORT != 0;
 /* The bulk pass's payload streaming, G lanes per frame (dynamic frame
  * assignment): every listed frame's partial sums into part (16 per frame,
  * zero-filled for G < 16).  meta: the batch's ranges. */
@@ -1397,6 +1403,44 @@ __device__ __forceinline__ void stream_groups(const RxArgs &a, const uint4 *meta
 			}
 			nxt += (uint32_t)__popcll(dq);
 		}
+	}
+}
+
+/* A batch whose ranges are all at most 64 bytes from their aligned start
+ * (the 128-byte frames of the echo leg): four lanes per frame, each lane
+ * loading its 16-byte chunk of four frames (g, g + 16, g + 32, g + 48) at
+ * once, so that the whole batch is one round trip; stream_groups<4> would
+ * take four dependent steps of 16 frames.  Same partials as stream_groups
+ * (part[16 f + chunk], the rest left zero). */
+template <bool NT>
+__device__ __forceinline__ void stream_short(const RxArgs &a, const uint4 *meta,
+					     uint32_t *part, int lane, uint32_t nb)
+{
+	const uint32_t sub = lane & 3, g = lane >> 2, ou = 16 * sub;
+	uint4 v[4], m[4];
+#pragma unroll
+	for (int u = 0; u < 4; u++) {
+		const uint32_t f = g + 16 * u;
+		m[u] = meta[f < nb ? f : 0];
+		v[u] = make_uint4(0, 0, 0, 0);
+		const uint64_t flo = ((uint64_t)m[u].y << 32) | m[u].x;
+		if (!(XDP_TAIL_DIAG & 2) && f < nb && ou < m[u].z)
+			v[u] = NT ? ld_nt16(a.umem + flo + ou)
+				  : *reinterpret_cast<const uint4 *>(a.umem + flo + ou);
+	}
+#pragma unroll
+	for (int u = 0; u < 4; u++) {
+		const uint32_t f = g + 16 * u, fnb = m[u].z, fsk = m[u].w;
+		if ((ou + 16 > fnb || ou < fsk) && ou < fnb) {
+			const uint4 mk = chunk_keep(ou, fsk, fnb);
+			v[u].x &= mk.x;
+			v[u].y &= mk.y;
+			v[u].z &= mk.z;
+			v[u].w &= mk.w;
+		}
+		if (f < nb)
+			part[16 * f + sub] = halves(v[u].x) + halves(v[u].y) + halves(v[u].z) +
+					     halves(v[u].w);
 	}
 }
 
@@ -1485,7 +1529,9 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 	for (int j = 0; j < 4; j++)
 		part4[4 * lane + ((j + (lane >> 2)) & 3)] = make_uint4(0, 0, 0, 0);
 	__builtin_amdgcn_wave_barrier();
-	if (kTailAdapt && mx <= 64 * U)
+	if (kTailShort && mx <= 64)
+		stream_short<NT>(a, meta, part, lane, nb);
+	else if (kTailAdapt && mx <= 64 * U)
 		stream_groups<4, U, NT>(a, meta, part, lane, nb);
 	else if (kTailAdapt && mx <= 128 * U)
 		stream_groups<8, U, NT>(a, meta, part, lane, nb);

@@ -144,18 +144,23 @@ def test_pool_vs_oracle(dev, name, kind, size, seed, n, kw, window, tune):
             np.testing.assert_array_equal(v, expect)
 
 
-def bulk_frames(seed: int, n: int):
+def bulk_frames(seed: int, n: int, long_every: int = 3, aligned: bool = True):
     """Fast-shape IPv4 UDP/TCP/ICMP frames of every length class around and past
     the 64-byte header window (0..2 VLAN tags, odd lengths, trailing pad,
     bad and absent checksums), 16-byte aligned with random gaps; the last
     frame ends at the UMEM end with an odd UDP length (over-read past the
-    UMEM reads as zero)."""
+    UMEM reads as zero).  Every long_every-th frame has up to 2960 payload
+    bytes, the rest under 60 (long_every 0: none long, so that whole bulk
+    batches have ranges within 64 bytes); aligned False puts frames at any
+    byte offset (exception frames, whose payload sums the bulk pass adds
+    from unaligned ranges)."""
     import frames as F
     rng = np.random.default_rng(seed)
     blobs = []
     for k in range(n):
         tags = [(0x8100, 5)] * int(rng.integers(0, 3))
-        plen = int(rng.integers(0, 60)) if k % 3 else int(rng.integers(0, 2960))
+        plen = int(rng.integers(0, 60)) if not long_every or k % long_every \
+            else int(rng.integers(0, 2960))
         pay = rng.integers(0, 256, plen, dtype=np.uint8).tobytes()
         if rng.random() < 0.5 or k == n - 1:
             seg = F.udp(int(rng.integers(1, 65536)), 53, pay)
@@ -181,9 +186,9 @@ def bulk_frames(seed: int, n: int):
         blobs[-1] = F.v4_frame(17, seg)
     offs, o = [], 0
     for fr in blobs:
-        o += 16 * int(rng.integers(0, 4))
+        o += 16 * int(rng.integers(0, 4)) if aligned else int(rng.integers(0, 40))
         offs.append(o)
-        o = (o + len(fr) + 15) & ~15
+        o = (o + len(fr) + 15) & ~15 if aligned else o + len(fr)
     size = offs[-1] + len(blobs[-1])
     umem = np.zeros(size, np.uint8)
     for off, fr in zip(offs, blobs):
@@ -205,6 +210,23 @@ def test_bulk_lengths_vs_oracle(dev, tune):
         oracle_stats_match(st, ost)
         if flags == 0x5:
             assert (ov == xdpgpu.REDIRECT).sum() > 2000 and (ov == xdpgpu.DROP).sum() > 100
+
+
+@pytest.mark.parametrize("tune", [0, 1 << 15, 1 << 21])
+@pytest.mark.parametrize("aligned", [True, False])
+def test_short_bulk_vs_oracle(dev, tune, aligned):
+    """Bulk batches whose ranges all end within 64 bytes of the window
+    (stream_short) and batches just past that, fast-shape (aligned) and
+    exception (unaligned) frames."""
+    umem, descs = bulk_frames(23 + aligned, 6000, long_every=0, aligned=aligned)
+    for flags, iv, fmt in ((0x5, 0, 1), (0x4, 0x12345, 2), (0x7, 9, 0)):
+        ou = umem.copy()
+        ov, ores, otup, ost = oracle.process(ou, descs, flags, iv, fmt)
+        v, res, tup, um, st = run_dev(umem, descs, flags, iv, fmt, 64, tune)
+        assert_same((v, res, tup, um), (ov, ores, otup, ou), f"short/{aligned}/{flags:#x}")
+        oracle_stats_match(st, ost)
+        if flags == 0x5:
+            assert (ov == xdpgpu.REDIRECT).sum() > 4000 and (ov == xdpgpu.DROP).sum() > 200
 
 
 def test_unaligned_encoded_descriptors(dev):

@@ -22,7 +22,14 @@ kind = int(sys.argv[3]) if len(sys.argv) > 3 else xdpgpu.POOL_UDP4
 fmt = int(sys.argv[4]) if len(sys.argv) > 4 else xdpgpu.TUPLE_V4
 lib = xdpgpu.load_library()
 lib.xdpgpu_stamps_read.argtypes = [C.c_void_p]
-umem, descs, _ = xdpgpu.pool_generate(n, kind, 64, 0x5EED0002 if kind == 0 else 0x5EED0003)
+# STAMPS_SIZE / STAMPS_ECHO_PPM: the echo leg's pool (bench.py echo_run:
+# 128-byte frames, ICMPv6 echo requests answered, XDPGPU_CFG_ICMP6_ECHO)
+size = int(os.environ.get("STAMPS_SIZE", "64"))
+echo_ppm = int(os.environ.get("STAMPS_ECHO_PPM", "0"))
+kw = {"ppm_echo6": echo_ppm} if echo_ppm else {}
+seed = 0x5EED0042 if echo_ppm else 0x5EED0002 if kind == 0 else 0x5EED0003
+umem, descs, _ = xdpgpu.pool_generate(n, kind, size, seed, **kw)
+flags = xdpgpu.CFG_DEFAULT | (xdpgpu.CFG_ICMP6_ECHO if echo_ppm else 0)
 dev = torch.device("cuda:0")
 d_umem = torch.zeros(umem.nbytes + 64, dtype=torch.uint8, device=dev)
 d_umem[: umem.nbytes].copy_(torch.from_numpy(umem))
@@ -30,12 +37,15 @@ d_desc = torch.from_numpy(descs.view(np.uint8)).to(dev)
 d_v = torch.empty(n, dtype=torch.uint8, device=dev)
 d_res = torch.empty(n * 16, dtype=torch.uint8, device=dev)
 d_tup = torch.empty(n * 44, dtype=torch.uint8, device=dev)
-ctx = xdpgpu.XdpGpu(0, xdpgpu.CFG_DEFAULT, 0, fmt, 64, tune=tune)
+ctx = xdpgpu.XdpGpu(0, flags, 0, fmt, 64, tune=tune)
 st = np.zeros(8 * 8192, np.uint64)
 reps = int(os.environ.get("STAMPS_REPS", "6"))
 per_rep = []   # per launch: each XCC's median and last loop end (us)
 for rep in range(reps):
     st[:] = 0
+    if echo_ppm:   # the responder rewrote the requests: restore them
+        d_umem[: umem.nbytes].copy_(torch.from_numpy(umem))
+        torch.cuda.synchronize()
     ctx.process_dev(d_umem, umem.nbytes, d_desc, n, d_v, d_res, d_tup)
     torch.cuda.synchronize()
     lib.xdpgpu_stamps_read(st.ctypes.data)
