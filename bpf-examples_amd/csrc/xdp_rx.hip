@@ -1337,9 +1337,9 @@ constexpr bool kTup6Tile = XDP_TUP6_TILE != 0;
 #endif
 constexpr bool kTailAdapt = XDP_TAIL_ADAPT != 0;
 /* Batches of ranges within 64 bytes streamed in one step (stream_short;
- * build knob) */
+ * build knob, off: DESIGN.md §5.2) */
 #ifndef XDP_TAIL_SHORT
-#define XDP_TAIL_SHORT 1
+#define XDP_TAIL_SHORT 0
 #endif
 constexpr bool kTailShort = XDP_TAIL_SHORT != 0;
 /* The bulk pass's payload streaming, G lanes per frame (dynamic frame
