@@ -591,22 +591,31 @@ int rx_run(const struct rx_source *src, const struct rx_opts *o,
 
 struct injector {
 	const struct rx_live *lv;
+	const struct xsk_sock *x;    /* the receiving socket (its counters) */
 	const char *ifname;
 	volatile uint64_t received;  /* frames the RX loop has taken */
 	volatile uint64_t sent;
 	volatile uint64_t lost;      /* frames the kernel dropped (no fill
-				      * buffer, RX ring full): given up on  */
+				      * buffer, RX ring full), or given up on */
 	volatile int stop;
-	volatile int done;           /* every frame sent                   */
+	volatile int done;           /* every frame sent, or the injector
+				      * failed (rc)                         */
 	int rc;
 };
 
+/* Frames given up on when the window has not moved for this long and the
+ * kernel reports no drop: far longer than any batch, the first one's code
+ * object load and buffer allocation included. */
+#define INJECT_STALL_NS 5000000000ull
+
 /* Sends the source's frames into the peer, cycling it, keeping at most
  * ring_size / 2 frames ahead of the receiver (no RX-ring overflow: every
- * frame sent is received, so verdicts line up with the source).  A window
- * that does not move for 100 ms means the kernel dropped frames of it (a
- * frame finds no fill buffer when the receiver holds them all): those
- * count as lost and sending goes on. */
+ * frame sent is received, so verdicts line up with the source).  `received`
+ * moves when the RX loop takes frames off the RX ring, before it hands them
+ * to the GPU.  Frames the kernel dropped (a frame finds no fill buffer when
+ * the receiver holds them all; XDP_STATISTICS) count as lost, and so do the
+ * frames of a window that has not moved for INJECT_STALL_NS; any loss is
+ * reported and the per-frame verdict file is then not written. */
 static void *inject_main(void *arg)
 {
 	struct injector *in = arg;
@@ -617,12 +626,19 @@ static void *inject_main(void *arg)
 
 	if (fd < 0) {
 		in->rc = fd;
+		in->done = 1;
 		return NULL;
 	}
 
-	uint64_t lost = 0, last_rx = 0, t_stall = 0;
+	const int64_t drops0 = xsk_rx_drops(in->x);
+	uint64_t given_up = 0, last_rx = 0, t_stall = 0;
 	while (!in->stop && k < in->lv->inject_count) {
 		uint64_t m = in->lv->inject_count - k;
+		const int64_t dr = xsk_rx_drops(in->x);
+		const uint64_t kdrop = dr >= 0 && drops0 >= 0 && dr > drops0 ?
+					       (uint64_t)(dr - drops0) : 0;
+		const uint64_t lost = kdrop + given_up;
+		in->lost = lost;
 		const uint64_t got = in->received + lost;
 		const uint64_t ahead = k > got ? k - got : 0;
 		if (ahead >= window) {
@@ -630,9 +646,8 @@ static void *inject_main(void *arg)
 			if (in->received != last_rx || !t_stall) {
 				last_rx = in->received;
 				t_stall = t;
-			} else if (t - t_stall > 100000000ull) {
-				lost += ahead;
-				in->lost = lost;
+			} else if (t - t_stall > INJECT_STALL_NS) {
+				given_up += ahead;
 				t_stall = 0;
 			}
 			usleep(20);
@@ -798,6 +813,7 @@ int rx_run_live(const struct rx_live *lv, const struct rx_opts *o, struct rx_tot
 
 	if (lv->inject) {
 		in.lv = lv;
+		in.x = &x;
 		in.ifname = lv->veth_peer ? lv->veth_peer : lv->ifname;
 		if (pthread_create(&th, NULL, inject_main, &in)) {
 			rc = -errno;
@@ -833,15 +849,17 @@ int rx_run_live(const struct rx_live *lv, const struct rx_opts *o, struct rx_tot
 				 * in xdpsock's own loop (no verdict compute) */
 				if (o->plumbing)
 					memset(s->v, XDPGPU_REDIRECT, s->n);
-				else
+				s->first = seen;
+				seen += s->n;
+				/* off the RX ring: the injector's window moves now,
+				 * however long the GPU batch takes */
+				in.received = seen;
+				t_last = now_ns();
+				if (!o->plumbing)
 					rc = xdpgpu_submit(ctx, k & 1, s->d, s->n, s->v, NULL, NULL);
 				if (rc)
 					break;
 				s->busy = true;
-				s->first = seen;
-				seen += s->n;
-				in.received = seen;
-				t_last = now_ns();
 			}
 		}
 		/* the previous batch: wait, apply its verdicts to the rings */
@@ -931,7 +949,12 @@ int rx_run_live(const struct rx_live *lv, const struct rx_opts *o, struct rx_tot
 			ctx ? xdpgpu_last_error(ctx) : "");
 	else if (!o->quiet)
 		print_stats(o, out, &st, label, t1);
-	if (!rc && verdicts) {
+	const bool aligned = !in.lost;
+	if (!rc && verdicts && !aligned)
+		fprintf(stderr, "%s: %llu injected frames lost: verdicts no longer line up "
+			"with the source, %s not written\n", o->prog,
+			(unsigned long long)in.lost, o->verdict_out);
+	if (!rc && verdicts && aligned) {
 		FILE *f = fopen(o->verdict_out, "wb");
 		const size_t nv = seen < o->count ? (size_t)seen : (size_t)o->count;
 		if (!f || fwrite(verdicts, 1, nv, f) != nv)
@@ -944,7 +967,8 @@ int rx_run_live(const struct rx_live *lv, const struct rx_opts *o, struct rx_tot
 		printf("{\"prog\": \"%s\", \"live\": \"%s:%u\", \"plumbing\": %s, "
 		       "\"mode\": \"%s\", \"frames\": %llu, \"seconds\": %.6f, "
 		       "\"mpps\": %.3f, \"rx_pkts\": %llu, \"rx_bytes\": %llu, \"tx_pkts\": %llu, "
-		       "\"injected\": %llu, \"lost\": %llu, \"batch\": %u, \"batches\": %llu, "
+		       "\"injected\": %llu, \"lost\": %llu, \"verdicts_aligned\": %s, "
+		       "\"batch\": %u, \"batches\": %llu, "
 		       "\"verdict\": {\"ABORTED\": %llu, \"DROP\": %llu, \"PASS\": %llu, "
 		       "\"TX\": %llu, \"REDIRECT\": %llu}}\n",
 		       o->prog, lv->ifname, lv->queue, o->plumbing ? "true" : "false",
@@ -952,7 +976,8 @@ int rx_run_live(const struct rx_live *lv, const struct rx_opts *o, struct rx_tot
 		       (unsigned long long)out->rx_pkts,
 		       out->seconds, mpps, (unsigned long long)out->rx_pkts,
 		       (unsigned long long)out->rx_bytes, (unsigned long long)out->tx_pkts,
-		       (unsigned long long)in.sent, (unsigned long long)in.lost, o->batch,
+		       (unsigned long long)in.sent, (unsigned long long)in.lost,
+		       aligned ? "true" : "false", o->batch,
 		       (unsigned long long)out->batches,
 		       (unsigned long long)out->verdict[0], (unsigned long long)out->verdict[1],
 		       (unsigned long long)out->verdict[2], (unsigned long long)out->verdict[3],

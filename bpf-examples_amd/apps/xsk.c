@@ -8,6 +8,7 @@
 #include "xsk.h"
 
 #include <errno.h>
+#include <stddef.h>
 #include <net/if.h>
 #include <poll.h>
 #include <stdarg.h>
@@ -141,6 +142,20 @@ int xsk_kick_tx(struct xsk_sock *x)
 			return -errno;
 	}
 	return 0;
+}
+
+int64_t xsk_rx_drops(const struct xsk_sock *x)
+{
+	struct xdp_statistics st;
+	socklen_t len = sizeof(st);
+
+	memset(&st, 0, sizeof(st));
+	if (getsockopt(x->fd, SOL_XDP, XDP_STATISTICS, &st, &len))
+		return -errno;
+	/* rx_ring_full is reported since Linux 5.9 (len says whether it is) */
+	const uint64_t full = len >= offsetof(struct xdp_statistics, rx_ring_full) +
+				     sizeof(st.rx_ring_full) ? st.rx_ring_full : 0;
+	return (int64_t)(st.rx_dropped + full);
 }
 
 uint32_t xsk_complete(struct xsk_sock *x, uint64_t *out, uint32_t max)

@@ -78,6 +78,9 @@ int xsk_kick_tx(struct xsk_sock *x);
 uint32_t xsk_complete(struct xsk_sock *x, uint64_t *out, uint32_t max);
 /* Wake the kernel for RX (poll) when the fill ring asks for it. */
 void xsk_wakeup_rx(struct xsk_sock *x, int timeout_ms);
+/* Frames the kernel dropped on their way to the RX ring (XDP_STATISTICS:
+ * no fill buffer, rx_dropped; RX ring full, rx_ring_full), or -errno. */
+int64_t xsk_rx_drops(const struct xsk_sock *x);
 
 /* Netlink: a veth pair a <-> b, both up.  0 or -errno. */
 int xsk_veth_create(const char *a, const char *b);

@@ -502,7 +502,8 @@ static int ensure_frag_bufs(xdpgpu_ctx *ctx, Slot &s, uint64_t m, uint64_t bytes
 			hipHostMalloc((void **)&s.h_fc, 4 * sizeof(unsigned long long), 0) !=
 				hipSuccess))
 		return set_err(ctx, -ENOMEM, "fragment counters");
-	if (bytes + 64 > s.bounce_cap) {
+	/* bytes 0: packets read in place, no bounce UMEM */
+	if (bytes && bytes + 64 > s.bounce_cap) {
 		(void)hipFree(s.d_bounce);
 		s.d_bounce = nullptr;
 		s.bounce_cap = 0;
@@ -636,7 +637,7 @@ static int enqueue_rx(xdpgpu_ctx *ctx, Slot &s, uint8_t *d_umem, uint64_t usize,
 	const uint64_t mcap = a.frags ? (uint64_t)n / 2 + 1 : 0;
 	if (a.frags) {
 		const uint64_t bytes = bounce ? usize + 16 * mcap : 0;
-		if (!s.d_fc || bytes + 64 > s.bounce_cap || mcap > s.pk_cap) {
+		if (!s.d_fc || (bytes && bytes + 64 > s.bounce_cap) || mcap > s.pk_cap) {
 			/* (re)allocation: the slot's earlier launches first */
 			rc = scratch_sync(ctx, s);
 			if (rc)
@@ -661,8 +662,8 @@ static int enqueue_rx(xdpgpu_ctx *ctx, Slot &s, uint8_t *d_umem, uint64_t usize,
 		f.stats = a.stats;
 		f.fc = s.d_fc;
 		f.blk = s.d_fc + 2;
-		f.bounce = s.d_bounce;
-		f.bounce_cap = s.bounce_cap - 64;
+		f.bounce = bounce ? s.d_bounce : nullptr;
+		f.bounce_cap = bounce ? s.bounce_cap - 64 : 0;
 		f.bdesc = s.d_bdesc;
 		f.bmap = s.d_bmap;
 		f.bverdict = s.d_bverdict;

@@ -17,7 +17,8 @@ from typing import Optional
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-ORACLE_SO = os.path.join(HERE, "liboracle.so")
+# XDPGPU_ORACLE_LIB: another build of the oracle (tools/asan.sh sanitized)
+ORACLE_SO = os.environ.get("XDPGPU_ORACLE_LIB") or os.path.join(HERE, "liboracle.so")
 REF_SO = os.path.join(HERE, "_ref", "libref.so")
 
 DESC_DTYPE = np.dtype([("addr", "<u8"), ("len", "<u4"), ("options", "<u4")])

@@ -16,12 +16,28 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running")
 
 
+_hostreg = None
+
+
 @pytest.fixture(autouse=True)
 def _gpu_drain(request):
     """A GPU test ends with the device drained and a fresh allocation used,
     so that an asynchronously reported device error fails the test whose
     kernels raised it, not the next one."""
+    global _hostreg
+    if os.environ.get("XDPGPU_HOSTREG_PROBE") == "1" and \
+            request.node.get_closest_marker("gpu") is not None:
+        # diagnostic: the runtime's host registrations per test (tests/hostreg.py)
+        if _hostreg is None:
+            import hostreg
+            import test_gpu_parity
+            import xdpgpu
+            hostreg.install(xdpgpu, test_gpu_parity)
+            _hostreg = hostreg
+        _hostreg.current_test = request.node.nodeid
     yield
+    if _hostreg is not None:
+        _hostreg.end_of_test()
     if request.node.get_closest_marker("gpu") is None:
         return
     torch = sys.modules.get("torch")

@@ -22,7 +22,8 @@ import oracle
 import xdpgpu
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
-APPS = os.path.join(ROOT, "bpf-examples_amd", "apps")
+# XDPGPU_APPS: another build of the front-ends (tools/asan.sh)
+APPS = os.environ.get("XDPGPU_APPS") or os.path.join(ROOT, "bpf-examples_amd", "apps")
 XDPSOCK = os.path.join(APPS, "xdpsock-gpu")
 AFXDP = os.path.join(APPS, "af_xdp_user-gpu")
 

@@ -22,7 +22,8 @@ import oracle
 import xdpgpu
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
-APPS = os.path.join(ROOT, "bpf-examples_amd", "apps")
+# XDPGPU_APPS: another build of the front-ends (tools/asan.sh)
+APPS = os.environ.get("XDPGPU_APPS") or os.path.join(ROOT, "bpf-examples_amd", "apps")
 FIXTURE = os.path.join(ROOT, "tests", "golden", "live_capture.npz")
 
 
