@@ -2594,8 +2594,7 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 	lds_dma_landed();
 	__syncthreads();
 
-	const uint32_t nfr = a.ndev ? (uint32_t)min((unsigned long long)a.n, *a.ndev)
-				    : a.n;
+	const uint32_t nfr = a.n;
 	const uint64_t ntiles = ((uint64_t)nfr + kWave - 1) / kWave;
 	FastWave w = {};
 	w.xl = a.xlist + rb * a.xregion;
@@ -2604,35 +2603,17 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 	STAMP(wgid, lane, 0);
 
 	const bool dma = !a.force_generic && a.usize >= 64;
-	/* the block's k-th tile (a.order): 0: b + k nb; 1: b per + k over a
-	 * contiguous range of per tiles; 2: k nb + (b + k) mod nb (each round
-	 * of nb tiles still split over the blocks, each block moving through
-	 * the round's positions); 3: pairs, 2 (b + (k / 2) nb) + k mod 2 (the
-	 * two tiles whose 64 verdict bytes share a 128-byte line on one CU,
-	 * and so in one XCD's L2); ntiles past the block's tiles.  Increasing
-	 * in k. */
-	/* the block's own tiles are those below own; the shared ones above
-	 * are claimed after them (a.steal_tiles) */
+	/* the block's own tiles are those below own, its k-th b + k nb; the
+	 * shared ones above are claimed after them (a.steal_tiles).  (Other
+	 * orders, measured and rejected: a contiguous range per block, 0.3504
+	 * vs 0.3448 ms; each round of nb tiles rotated over the blocks, 11 %
+	 * slower; adjacent pairs per block, 0.3222 vs 0.3179 ms; the order
+	 * shifted by s XCDs, no s ahead: DESIGN.md §5.2) */
 	const uint64_t shared = FRAGS || DIAG ? 0 : a.steal_tiles;
 	const uint64_t own = ntiles - shared;
-	const uint64_t per = (own + nb - 1) / nb;
-	const uint32_t order = a.order;
-	const uint64_t rot = 1;
-	/* order 0's XCD shift: block b takes the tiles t = b - xs mod nb */
-	const uint64_t xs = order == 0 ? a.xshift % nb : 0;
 	auto tile_of = [&](uint64_t k) -> uint64_t {
-		uint64_t t, lim = own;
-		if (order == 1) {
-			t = rb * per + k;
-			lim = min(own, rb * per + per);
-		} else if (order == 3) {
-			t = 2 * (rb + (k >> 1) * nb) + (k & 1);
-		} else if (order == 2) {
-			t = k * nb + (rb + k * rot) % nb;
-		} else {
-			t = (rb + nb - xs) % nb + k * nb;
-		}
-		return t < lim ? t : ntiles;
+		const uint64_t t = rb + k * nb;
+		return t < own ? t : ntiles;
 	};
 	/* the block's next cnt tiles: claim indices k .. k + cnt-1 */
 	auto claim = [&](uint32_t cnt) -> uint64_t {
@@ -2643,7 +2624,7 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 		const uint64_t i = tt * kWave + lane;
 		return i < nfr ? i : nfr - 1;
 	};
-	/* DMA of a tile's 64-byte windows into buf (see xdp_rx_kernel); the
+	/* DMA of a tile's 64-byte windows into buf; the
 	 * frame offsets reach the loading lanes by lane shuffles */
 	auto issue_win = [&](uint4 dv, bool live, uint4 *buf) {
 		const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
@@ -2786,8 +2767,8 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 		 * head evens them: config 2 0.2969 / 0.2989 vs 0.3007 / 0.3032
 		 * ms without, in one process; every XCD's heads 0.3058 / 0.3079
 		 * (the XCDs of one half drain together, and a move there only
-		 * adds a late pair). */
-		const int rounds = heads % 8 == 0 && a.partner > 1 ? (int)a.partner : 1;
+		 * adds a late pair; not kept). */
+		const int rounds = heads % 8 == 0 && a.partner > 1 ? 2 : 1;
 		for (int round = 0; round < rounds; ++round) {
 			if (round && (__builtin_amdgcn_readfirstlane(ctl[7]) >> round) & 1)
 				continue;
@@ -2806,23 +2787,15 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 					v = atomicAdd(ctr, 1u);
 				return v;
 			};
-			/* the pair order (3): a claim is the adjacent tiles own + 2v
-			 * heads + 2h and the next, on the same XCD as in its own-tile
-			 * order (own is a multiple of 2 heads) */
-			const bool pairs = order == 3;
-			/* with order 0's XCD shift, head h takes the residue h - xs, which
-			 * the shifted own order puts on h's XCD */
-			const uint64_t hr = (h + heads - xs % heads) % heads;
 			auto first_of = [&](uint32_t v) -> uint64_t {
-				const uint64_t t = own + (uint64_t)__builtin_amdgcn_readfirstlane(v) * 2 * heads +
-						   (pairs ? 2 * h : hr);
+				const uint64_t t = own + (uint64_t)__builtin_amdgcn_readfirstlane(v) * 2 * heads + h;
 				return t < ntiles ? t : ntiles;
 			};
 			auto second_of = [&](uint64_t t) -> uint64_t {
-				const uint64_t u = t + (pairs ? 1 : heads);
+				const uint64_t u = t + heads;
 				return u < ntiles ? u : ntiles;
 			};
-			uint64_t c0 = own + (pairs ? 2 * h : hr) < ntiles ? first_of(claim2()) : ntiles;
+			uint64_t c0 = own + h < ntiles ? first_of(claim2()) : ntiles;
 			if (round && c0 >= ntiles && lane == 0)
 				atomicOr(&ctl[7], 1u << round);
 			if (c0 < ntiles) {
@@ -2883,227 +2856,6 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 		}
 	}
 	STAMP(wgid, lane, 2);
-}
-
-/* Per-wave LDS of the fast kernel, in uint4: the tile loop's window buffer
- * (256), descriptor table (32) and two deferral queues (32 each); the tail
- * phase reuses the same bytes for the exception pass's windows (272) and
- * table (32), then the bulk pass's meta (64) and partial sums (256). */
-constexpr int kRxLdsWave = 256 + 32 + 32 + 32;
-static_assert(kRxLdsWave >= 64 * 17 / 4 + 32 && kRxLdsWave >= 64 + 256,
-	      "tail phases fit the loop's LDS");
-
-template <int MINW, bool FRAGS>
-__global__ __launch_bounds__(kBlock, MINW) void xdp_rx_kernel(RxArgs a)
-{
-	constexpr int XQ = 2 * kWave;      /* deferral queues per wave */
-	__shared__ uint4 lds_all[kWavesPerBlock * kRxLdsWave];
-	__shared__ unsigned long long blk_cnt[CNT_SLOT];
-
-	const int lane = threadIdx.x & (kWave - 1);
-	const int wid = threadIdx.x / kWave;
-	uint4 *wlds = lds_all + wid * kRxLdsWave;
-	uint4 *buf = wlds;
-	uint64_t *dtab = reinterpret_cast<uint64_t *>(wlds + 4 * kWave);
-	uint32_t *xq = reinterpret_cast<uint32_t *>(wlds + 4 * kWave + 32);
-	uint32_t *bq = xq + XQ;
-
-	if (threadIdx.x < CNT_SLOT)
-		blk_cnt[threadIdx.x] = 0;
-	__syncthreads();
-
-	/* frames: a.n, or the device count it bounds (the bounce batch of
-	 * multi-buffer packets, frags.hip) */
-	const uint32_t nfr = a.ndev ? (uint32_t)min((unsigned long long)a.n, *a.ndev)
-				    : a.n;
-	const uint64_t ntiles = ((uint64_t)nfr + kWave - 1) / kWave;
-	const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
-	const uint64_t wgid = (uint64_t)blockIdx.x * kWavesPerBlock + wid;
-	uint32_t *xl = a.xlist + wgid * a.xregion;
-	uint32_t *bl = a.blist + wgid * a.xregion;
-	FastWave w = {};
-	w.xq = xq;
-	w.bq = bq;
-	w.xl = xl;
-	w.bl = bl;
-
-	/* the DMA of an invalid frame reads the UMEM's first 64 bytes */
-	const bool dma = !a.force_generic && a.usize >= 64;
-	/* descriptor of frame t*64+lane, index clamped to the batch so the
-	 * prefetch is an unconditional load (lanes past the end are inactive) */
-	auto ld_desc = [&](uint64_t tt) -> uint4 {
-		uint64_t i = tt * kWave + lane;
-		i = i < nfr ? i : nfr - 1;
-		return *reinterpret_cast<const uint4 *>(a.desc + i);
-	};
-	/* DMA the 64-byte windows of a tile into buf: frames that are not
-	 * valid, 16-byte aligned and whole inside the UMEM, and every frame of
-	 * a tile past the end (live false), load the UMEM's first 64 bytes
-	 * instead (one cached line; their lanes are deferred or inactive).
-	 * Issued unconditionally so that no wait for it is placed early. */
-	auto issue = [&](uint4 dv, bool live) {
-		const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
-		const uint32_t len = dv.z;
-		const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
-		const bool ok = live & dma & (len >= 14) & ((uint64_t)len <= a.usize) &
-				(eff <= a.usize - len) & !(eff & 15) &
-				(eff + 64 <= ((a.usize + 15) & ~15ull));
-		dtab[lane] = ok ? eff : 0ull;
-		__builtin_amdgcn_wave_barrier();
-#pragma unroll
-		for (int k = 0; k < 4; k++) {
-			const int f = 16 * k + (lane >> 2);
-			const int c = (lane & 3) ^ ((f >> 2) & 3);
-			__builtin_amdgcn_global_load_lds(
-				(const void *)(a.umem + dtab[f] + 16 * c),
-				(lds_void_t *)(buf + kWave * k), 16, 0, 2 /* nt */);
-		}
-	};
-
-	uint64_t t = wgid;
-	uint4 dcur = make_uint4(0, 0, 0, 0), dnext = dcur;
-	if (t < ntiles) {
-		dcur = ld_desc(t);
-		dnext = ld_desc(t + nwaves);
-		issue(dcur, true);
-	}
-	for (; t < ntiles; t += nwaves) {
-		const uint64_t i = t * kWave + lane;
-		const uint4 dv = dcur;
-		/* multi-buffer mode (a variant of its own, so that the plain
-		 * kernel is untouched): the descriptors of packets of several
-		 * fragments are the fragment kernels' (frags.hip) */
-		bool skip = false;
-		if constexpr (FRAGS) {
-			const uint32_t contd = dv.w & XDPGPU_PKT_CONTD;
-			uint32_t prev = (uint32_t)__shfl_up((int)contd, 1, kWave);
-			if (lane == 0)
-				prev = t ? a.desc[t * kWave - 1].options & XDPGPU_PKT_CONTD : 0u;
-			skip = (contd | prev) != 0;
-		}
-		const bool active = (i < nfr) & !skip;
-
-		/* 1. this lane's window out of LDS (4 conflict-free b128 reads),
-		 * then the next tile's DMA and descriptors */
-		uint32_t F[18];
-		lds_dma_landed();
-		{
-			const int sw = (lane >> 2) & 3;
-#pragma unroll
-			for (int c = 0; c < 4; c++) {
-				const uint4 v = buf[4 * lane + (c ^ sw)];
-				F[4 * c] = v.x;
-				F[4 * c + 1] = v.y;
-				F[4 * c + 2] = v.z;
-				F[4 * c + 3] = v.w;
-			}
-			F[16] = F[17] = 0;
-		}
-		lds_reads_done();
-		__builtin_amdgcn_wave_barrier();
-		dcur = dnext;
-		issue(dcur, t + nwaves < ntiles);
-		dnext = ld_desc(t + 2 * nwaves);
-
-		fast_tile<true>(a, F, dv, i, active, dma, lane, w);
-	}
-	rx_flush_lists(a, w, wgid, lane);
-
-	block_stats_flush(a, blk_cnt, w.cnt, w.my_bytes, lane);
-}
-
-
-/* Assignment of the fast kernel's wave regions to the waves of a
- * follow-up kernel: with at least as many waves as regions, m = W / R waves
- * share a region and take its batches round robin; otherwise waves stride
- * over regions.  Each wave reads a region's count once. */
-struct RegionWalk {
-	uint32_t first, rstep, bfirst, bstep;
-	__device__ RegionWalk(uint32_t regions, uint32_t waves, uint32_t w)
-	{
-		const uint32_t m = waves >= regions ? waves / regions : 1;
-		first = w / m;
-		rstep = waves / m;
-		bfirst = (w % m) * kWave;
-		bstep = m * kWave;
-	}
-};
-
-/* Bulk kernel: the bulk pass as a kernel of its own (cfg.tune bit 8). */
-template <int MINW, int U, bool NT, int G = 16>
-__global__ __launch_bounds__(kBlock, MINW) void xdp_rx_bulk_kernel(RxArgs a)
-{
-	__shared__ uint4 meta_all[kWavesPerBlock * kWave];
-	__shared__ uint4 part_all[kWavesPerBlock * kWave * 4];
-	__shared__ unsigned long long blk_cnt[CNT_SLOT];
-
-	const int lane = threadIdx.x & (kWave - 1);
-	const int wid = threadIdx.x / kWave;
-	uint4 *meta = meta_all + wid * kWave;
-	uint4 *part4 = part_all + wid * kWave * 4;
-	if (threadIdx.x < CNT_SLOT)
-		blk_cnt[threadIdx.x] = 0;
-	__syncthreads();
-
-	const uint32_t nwaves = gridDim.x * kWavesPerBlock;
-	uint32_t cnt[CNT_FRAG + 1] = {};
-	uint64_t my_bytes = 0;
-	const RegionWalk w(a.nregions, nwaves, blockIdx.x * kWavesPerBlock + wid);
-	for (uint32_t r = w.first; r < a.nregions; r += w.rstep) {
-		const uint32_t count = a.bcount[r];
-		const uint32_t *bl = a.blist + (uint64_t)r * a.xregion;
-		for (uint32_t b = w.bfirst; b < count; b += w.bstep)
-			bulk_batch<U, NT, false, G>(a, meta, part4, lane, bl + b,
-						 count - b < (uint32_t)kWave ? count - b : kWave,
-						 cnt, my_bytes);
-		const uint32_t ycount = a.ycount[r];
-		const uint4 *yl = a.ylist + (uint64_t)r * a.xregion;
-		for (uint32_t b = w.bfirst; b < ycount; b += w.bstep)
-			bulk_batch<U, NT, true, G>(a, meta, part4, lane, yl + b,
-						ycount - b < (uint32_t)kWave ? ycount - b : kWave,
-						cnt, my_bytes);
-	}
-	block_stats_flush(a, blk_cnt, cnt, my_bytes, lane);
-}
-
-/* Exception kernel: the generic pipeline on the frames the fast kernel
- * deferred, one wave per fast-kernel wave region, 64 frames per batch. */
-/* held to 96 VGPRs (5 waves/SIMD, a few spilled registers): the kernel is
- * latency-bound, and on IMIX it ran 0.30-0.31 ms against 0.34-0.36 ms at
- * the compiler's 3 waves (same process, tools/tune_rx.py) */
-template <int WIN>
-__global__ __launch_bounds__(kBlock, 5) void xdp_rx_generic_kernel(RxArgs a)
-{
-	constexpr int SDW = WIN / 4 + 1;
-	__shared__ uint32_t lds[kWavesPerBlock * kWave * SDW + 8];
-	__shared__ uint64_t dtab_all[kWavesPerBlock * kWave];
-	__shared__ unsigned long long blk_cnt[CNT_SLOT];
-
-	const int lane = threadIdx.x & (kWave - 1);
-	const int wid = threadIdx.x / kWave;
-	uint32_t *win = lds + wid * kWave * SDW;
-	uint64_t *dtab = dtab_all + wid * kWave;
-	if (threadIdx.x < CNT_SLOT)
-		blk_cnt[threadIdx.x] = 0;
-	__syncthreads();
-
-	const uint32_t nwaves = gridDim.x * kWavesPerBlock;
-	uint32_t cnt[CNT_FRAG + 1] = {};
-	uint64_t my_bytes = 0;
-	const RegionWalk w(a.nregions, nwaves, blockIdx.x * kWavesPerBlock + wid);
-	for (uint32_t r = w.first; r < a.nregions; r += w.rstep) {
-		const uint32_t count = a.xcount[r];
-		const uint32_t *xl = a.xlist + (uint64_t)r * a.xregion;
-		for (uint32_t b = w.bfirst; b < count; b += w.bstep) {
-			const bool act = b + lane < count;
-			const uint64_t i = act ? xl[b + lane] : 0;
-			generic_batch<WIN>(a, win, dtab, lane, i, act,
-					   a.ylist + (uint64_t)r * a.xregion,
-					   a.ycount + r, cnt, my_bytes);
-		}
-	}
-
-	block_stats_flush(a, blk_cnt, cnt, my_bytes, lane);
 }
 
 /* Multi-buffer packets read in place (XDPGPU_CFG_FRAGS, after
@@ -3193,82 +2945,11 @@ uint32_t rx_grid_blocks(uint32_t n, uint32_t max_blocks)
 	return (uint32_t)blocks;
 }
 
-/* Kernel variants selectable by cfg.tune (diagnostic A/B): bits 0-7 =
- * waves per SIMD the fast kernel's register allocation is held to (0:
- * compiler's choice, 6, 8), bit 9 = every frame through the exception
- * kernel (bulk pass off for it), bits 10-11 = bulk-kernel variant. */
 /* Blocks of a kernel resident at once on the device (occupancy x CUs). */
 template <auto KERN>
 static uint32_t resident_blocks()
 {
 	return resident_blocks_dev<KERN, kBlock>(kMaxRxBlocks);
-}
-
-/* Launch the fast kernel on a grid of resident blocks (no partial second
- * round), then the bulk and exception kernels, each on its own resident
- * grid, over the fast kernel's wave regions.  a.xlist and a.blist must each
- * hold blocks * kWavesPerBlock * rx_xregion(a.n, blocks) entries. */
-template <auto KERN>
-static hipError_t launch_resident(const RxArgs &a, uint32_t cap,
-				  hipStream_t stream)
-{
-	uint32_t blocks = resident_blocks<KERN>();
-	if (blocks > cap)
-		blocks = cap;
-	hipLaunchKernelGGL(KERN, dim3(blocks), dim3(kBlock), 0, stream, a);
-	return hipGetLastError();
-}
-
-template <int WIN, int MINW>
-static hipError_t launch_sized(RxArgs a, uint32_t max_blocks,
-			       hipStream_t stream, uint32_t bulk_variant,
-			       hipEvent_t *ev)
-{
-	uint32_t cap = resident_blocks<xdp_rx_kernel<MINW, false>>();
-	if (cap < max_blocks)
-		max_blocks = cap;
-	const uint32_t blocks = rx_grid_blocks(a.n, max_blocks);
-	a.xregion = rx_xregion(a.n, blocks);
-	a.nregions = blocks * kWavesPerBlock;
-	if (ev)
-		(void)hipEventRecord(ev[0], stream);
-	if (a.frags)
-		hipLaunchKernelGGL((xdp_rx_kernel<MINW, true>), dim3(blocks),
-				   dim3(kBlock), 0, stream, a);
-	else
-		hipLaunchKernelGGL((xdp_rx_kernel<MINW, false>), dim3(blocks),
-				   dim3(kBlock), 0, stream, a);
-	hipError_t e = hipGetLastError();
-	if (e != hipSuccess)
-		return e;
-	if (ev)
-		(void)hipEventRecord(ev[1], stream);
-	/* at most one wave per (region, batch) */
-	const uint64_t items = (uint64_t)a.nregions * (a.xregion / kWave);
-	const uint32_t icap = (uint32_t)((items + kWavesPerBlock - 1) / kWavesPerBlock);
-	e = launch_resident<xdp_rx_generic_kernel<WIN>>(a, icap, stream);
-	if (e != hipSuccess)
-		return e;
-	if (ev)
-		(void)hipEventRecord(ev[2], stream);
-	switch (bulk_variant) {
-	case 1:
-		e = launch_resident<xdp_rx_bulk_kernel<8, 4, true, 8>>(a, icap, stream);
-		break;
-	case 2:
-		e = launch_resident<xdp_rx_bulk_kernel<8, 2, true>>(a, icap, stream);
-		break;
-	case 3:
-		e = launch_resident<xdp_rx_bulk_kernel<8, 4, false>>(a, icap, stream);
-		break;
-	default:
-		/* 4 non-temporal loads per lane and step: 1500 B 3-4 % faster
-		 * than 2 in one process, IMIX and config 2 unchanged */
-		e = launch_resident<xdp_rx_bulk_kernel<8, 4, true>>(a, icap, stream);
-	}
-	if (ev && e == hipSuccess)
-		(void)hipEventRecord(ev[3], stream);
-	return e;
 }
 
 /* The default RX launch: one double-buffered fast kernel with its tail
@@ -3288,20 +2969,15 @@ static hipError_t launch_db(RxArgs a, uint32_t max_blocks, hipStream_t stream,
 		blocks = max_blocks;
 	if (blocks == 0)
 		blocks = 1;
-	/* list regions per block: its share of the tiles (the pair order, 3:
-	 * whole pairs, up to one tile more than an even share) */
-	auto share = [&](uint64_t own) -> uint64_t {
-		if (a.order == 3)
-			return 2 * (((own + 1) / 2 + blocks - 1) / blocks);
-		return (own + blocks - 1) / blocks;
-	};
+	/* list regions per block: its share of the tiles */
+	auto share = [&](uint64_t own) -> uint64_t { return (own + blocks - 1) / blocks; };
 	a.xregion = (uint32_t)(share(ntiles) * kWave);
 	a.nregions = (uint32_t)blocks;
 	/* shared tiles (xdp_rx_db_kernel): the last ntiles x steal_16ths / 16,
 	 * for batches of at least 64 tiles per block; a block's region then
 	 * holds its own tiles and up to steal_cap() shared ones */
 	a.steal_tiles = 0;
-	if (a.steal && a.steal_16ths && !a.frags && !a.ndev && !diag &&
+	if (a.steal && a.steal_16ths && !a.frags && !diag &&
 	    ntiles >= 64 * blocks) {
 		/* own a multiple of twice the heads (xdp_rx_db_kernel's head
 		 * orders) */
@@ -3355,45 +3031,24 @@ hipError_t launch_rx_packets(const RxArgs &a, uint32_t max_blocks, hipStream_t s
 	return hipGetLastError();
 }
 
-hipError_t launch_rx(const RxArgs &a, uint32_t window, uint32_t max_blocks,
-		     hipStream_t stream, uint32_t tune, hipEvent_t *ev)
+hipError_t launch_rx(const RxArgs &a, uint32_t max_blocks, hipStream_t stream, uint32_t tune,
+		     hipEvent_t *ev)
 {
-	const uint32_t waves = tune & 0xff;
-	/* bits 10-11: bulk-kernel loads per lane and step (0: 4 non-temporal,
-	 * 1: 4 non-temporal in 8-lane groups, 2: 2 non-temporal, 3: 4) */
-	const uint32_t bu = (tune >> 10) & 3;
-	/* default: one double-buffered launch; the three-kernel form for the
-	 * 128-byte exception window and the diagnostic variants (bit 15
-	 * forces it); bits 16-17: the double-buffered kernel's diagnostic
-	 * variants (no compute, no stores) */
-	if (window != 128 && !(tune & 0x8fffu)) {
-		RxArgs b = a;
-		b.diag = (tune >> 16) & 3;
-		/* IPv6 in the fast shape (IMIX's IPv6 frames) for the 44-byte
-		 * network_tuple and no tuple, and with the echo responder
-		 * (its requests are IPv6); bit 18 turns it off.  The 16-byte
-		 * IPv4 tuple otherwise keeps the IPv4-only kernel (config 2),
-		 * whose registers it would cost. */
-		b.v6 = (a.tuple_fmt != XDPGPU_TUPLE_V4 || (a.flags & XDPGPU_CFG_ICMP6_ECHO)) &&
-		       !((tune >> 18) & 1);
-		/* bits 19-20: the tile order (xdp_rx_db_kernel) */
-		b.order = (tune >> 19) & 3;
-		/* bits 25-27: order 0's XCD shift (diagnostic) */
-		b.xshift = (tune >> 25) & 7;
-		/* bits 28-29: after its own head, a wave claims shared tiles of
-		 * 0: the partner head in the other half of the chip (default),
-		 * 1: no other head, 2: the heads of every XCD in turn, 3: as 0 */
-		const uint32_t pm = (tune >> 28) & 3;
-		b.partner = pm == 1 ? 1 : pm == 2 ? 8 : 2;
-		return launch_db(b, max_blocks, stream, ev);
-	}
-	if (window == 128)
-		return launch_sized<128, 1>(a, max_blocks, stream, bu, ev);
-	if (waves == 6)
-		return launch_sized<64, 6>(a, max_blocks, stream, bu, ev);
-	if (waves == 8)
-		return launch_sized<64, 8>(a, max_blocks, stream, bu, ev);
-	return launch_sized<64, 1>(a, max_blocks, stream, bu, ev);
+	RxArgs b = a;
+	/* bits 16-17: diagnostic variants (no compute, no stores) */
+	b.diag = (tune >> 16) & 3;
+	/* IPv6 in the fast shape (IMIX's IPv6 frames) for the 44-byte
+	 * network_tuple and no tuple, and with the echo responder (its
+	 * requests are IPv6); bit 18 turns it off.  The 16-byte IPv4 tuple
+	 * otherwise keeps the IPv4-only kernel (config 2), whose registers it
+	 * would cost. */
+	b.v6 = (a.tuple_fmt != XDPGPU_TUPLE_V4 || (a.flags & XDPGPU_CFG_ICMP6_ECHO)) &&
+	       !((tune >> 18) & 1);
+	/* bit 28: after its own head, a wave claims no shared tiles of the
+	 * partner head (the default goes on with the head in the other half
+	 * of the chip) */
+	b.partner = (tune >> 28) & 1 ? 1 : 2;
+	return launch_db(b, max_blocks, stream, ev);
 }
 
 /* ------------------------------------------------------------------ */

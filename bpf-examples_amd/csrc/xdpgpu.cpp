@@ -52,18 +52,6 @@ struct Slot {
 	 * sets, the next launch's zeroed by the current one */
 	uint32_t *d_steal = nullptr;
 	uint32_t steal_set = 0;
-	/* multi-buffer packets (XDPGPU_CFG_FRAGS) */
-	unsigned long long *d_fc = nullptr;   /* fragment kernels' counters:
-					       * 2 totals, then 2 per block */
-	unsigned long long *h_fc = nullptr;   /* pinned host copy           */
-	uint8_t *d_bounce = nullptr;          /* bounce UMEM                */
-	uint64_t bounce_cap = 0;
-	xdpgpu_desc *d_bdesc = nullptr;       /* per packet                 */
-	uint2 *d_bmap = nullptr;
-	uint8_t *d_bverdict = nullptr;
-	xdpgpu_result *d_bres = nullptr;
-	uint8_t *d_btup = nullptr;
-	uint64_t pk_cap = 0;
 	/* host path: this slot's device mirror of the registered UMEM (one
 	 * per slot, so two batches in flight never share mirror bytes) */
 	uint8_t *d_mirror = nullptr;
@@ -189,15 +177,6 @@ static void free_slot(Slot &s)
 		(void)hipFree(s.d_steal);
 	if (s.d_ylist)
 		(void)hipFree(s.d_ylist);
-	if (s.h_fc)
-		(void)hipHostFree(s.h_fc);
-	(void)hipFree(s.d_fc);
-	(void)hipFree(s.d_bounce);
-	(void)hipFree(s.d_bdesc);
-	(void)hipFree(s.d_bmap);
-	(void)hipFree(s.d_bverdict);
-	(void)hipFree(s.d_bres);
-	(void)hipFree(s.d_btup);
 	(void)hipFree(s.d_mirror);
 	(void)hipFree(s.d_erec);
 	(void)hipFree(s.d_ecnt);
@@ -293,7 +272,7 @@ int xdpgpu_init(const xdpgpu_cfg *cfg, xdpgpu_ctx **out)
 {
 	if (!cfg || !out)
 		return -EINVAL;
-	if (cfg->window != 0 && cfg->window != 64 && cfg->window != 128)
+	if (cfg->window != 0 && cfg->window != 64)
 		return -EINVAL;
 	if (cfg->tuple_fmt > XDPGPU_TUPLE_NET)
 		return -EINVAL;
@@ -492,53 +471,6 @@ static int ensure_xlist(xdpgpu_ctx *ctx, Slot &s, uint32_t n)
 	return 0;
 }
 
-/* Fragment scratch of a slot (XDPGPU_CFG_FRAGS): the counters, and the
- * bounce UMEM and per-packet arrays for m packets of `bytes` bounce bytes.
- * Called with the slot's stream idle. */
-static int ensure_frag_bufs(xdpgpu_ctx *ctx, Slot &s, uint64_t m, uint64_t bytes)
-{
-	if (!s.d_fc && (hipMalloc(&s.d_fc, (2 + 2 * 1024) * sizeof(unsigned long long)) !=
-				hipSuccess ||
-			hipHostMalloc((void **)&s.h_fc, 4 * sizeof(unsigned long long), 0) !=
-				hipSuccess))
-		return set_err(ctx, -ENOMEM, "fragment counters");
-	/* bytes 0: packets read in place, no bounce UMEM */
-	if (bytes && bytes + 64 > s.bounce_cap) {
-		(void)hipFree(s.d_bounce);
-		s.d_bounce = nullptr;
-		s.bounce_cap = 0;
-		const uint64_t cap = std::max<uint64_t>(bytes + 64, 1ull << 20);
-		if (hipMalloc(&s.d_bounce, cap) != hipSuccess)
-			return set_err(ctx, -ENOMEM, "bounce UMEM of %llu bytes",
-				       (unsigned long long)cap);
-		s.bounce_cap = cap;
-	}
-	if (m > s.pk_cap) {
-		(void)hipFree(s.d_bdesc);
-		(void)hipFree(s.d_bmap);
-		(void)hipFree(s.d_bverdict);
-		(void)hipFree(s.d_bres);
-		(void)hipFree(s.d_btup);
-		s.d_bdesc = nullptr;
-		s.d_bmap = nullptr;
-		s.d_bverdict = nullptr;
-		s.d_bres = nullptr;
-		s.d_btup = nullptr;
-		s.pk_cap = 0;
-		const uint64_t cap = std::max<uint64_t>(m, 4096);
-		const uint32_t tb = tuple_bytes(ctx->cfg.tuple_fmt);
-		if (hipMalloc(&s.d_bdesc, cap * sizeof(xdpgpu_desc)) != hipSuccess ||
-		    hipMalloc(&s.d_bmap, cap * sizeof(uint2)) != hipSuccess ||
-		    hipMalloc(&s.d_bverdict, cap) != hipSuccess ||
-		    hipMalloc(&s.d_bres, cap * sizeof(xdpgpu_result)) != hipSuccess ||
-		    (tb && hipMalloc(&s.d_btup, cap * tb) != hipSuccess))
-			return set_err(ctx, -ENOMEM, "fragment arrays for %llu packets",
-				       (unsigned long long)cap);
-		s.pk_cap = cap;
-	}
-	return 0;
-}
-
 /* A launch on `stream` that uses slot s's scratch waits for the previous
  * launch that used it when that one went to another stream (a caller's
  * stream for xdpgpu_process_dev / xdpgpu_nat64_dev, the slot's own for
@@ -614,43 +546,23 @@ static int enqueue_rx(xdpgpu_ctx *ctx, Slot &s, uint8_t *d_umem, uint64_t usize,
 	a.xcap = s.xcap;
 	a.steal = s.d_steal;
 	a.steal_set = s.steal_set;
-	/* shared tiles, in 16ths of the batch (cfg.tune bits 21-23): 0 =
-	 * 12, 1 = none, 2 = 4, 3 = 8, 4 = 16 (all), 5 = 12, 6 = 2, 7 = 14.
+	/* shared tiles, in 16ths of the batch (cfg.tune bit 21: none).
 	 * Config 2, one box, one process: none 0.3435 ms, 8 0.3284, 12
 	 * 0.3226, 14 0.3227, 16 0.331 (tools/gpu_ab_steal.sh) */
-	{
-		static const uint32_t k16ths[8] = {12, 0, 4, 8, 16, 12, 2, 14};
-		a.steal_16ths = k16ths[(ctx->cfg.tune >> 21) & 7];
-	}
+	a.steal_16ths = (ctx->cfg.tune >> 21) & 1 ? 0u : 12u;
 
-	/* Multi-buffer packets.  No host round trip: the bounce arrays are
-	 * sized from bounds known here (a packet has at least two
-	 * descriptors; its bounce bytes are its own bytes plus at most 16 of
-	 * padding, and the fragments of distinct packets are distinct UMEM
-	 * bytes), and the kernels after the count read the packet count from
-	 * the device. */
-	FragArgs f;
-	memset(&f, 0, sizeof(f));
-	/* packets read in place, or (cfg.tune bit 24, round 2's path for
-	 * A/B) gathered into a bounce UMEM */
-	const bool bounce = (ctx->cfg.tune >> 24) & 1;
-	const uint64_t mcap = a.frags ? (uint64_t)n / 2 + 1 : 0;
-	if (a.frags) {
-		const uint64_t bytes = bounce ? usize + 16 * mcap : 0;
-		if (!s.d_fc || (bytes && bytes + 64 > s.bounce_cap) || mcap > s.pk_cap) {
-			/* (re)allocation: the slot's earlier launches first */
-			rc = scratch_sync(ctx, s);
-			if (rc)
-				return rc;
-			rc = ensure_frag_bufs(ctx, s, mcap, bytes);
-			if (rc)
-				return rc;
-		}
-	}
 	rc = scratch_enter(ctx, s, stream);
 	if (rc)
 		return rc;
+	hipEvent_t *ev = nullptr;
+	if (ctx->tev && ctx->tn < XDPGPU_TIMING_MAX)
+		ev = ctx->tev + 4 * ctx->tn++;
 	if (a.frags) {
+		/* multi-buffer packets: the broken ones finished first, then
+		 * (after the RX kernel, which skips their descriptors) every
+		 * complete packet read in place as one frame */
+		FragArgs f;
+		memset(&f, 0, sizeof(f));
 		f.umem = d_umem;
 		f.usize = usize;
 		f.desc = d_desc;
@@ -660,47 +572,13 @@ static int enqueue_rx(xdpgpu_ctx *ctx, Slot &s, uint8_t *d_umem, uint64_t usize,
 		f.tup = d_tup;
 		f.tb = d_tup ? tuple_bytes(ctx->cfg.tuple_fmt) : 0;
 		f.stats = a.stats;
-		f.fc = s.d_fc;
-		f.blk = s.d_fc + 2;
-		f.bounce = bounce ? s.d_bounce : nullptr;
-		f.bounce_cap = bounce ? s.bounce_cap - 64 : 0;
-		f.bdesc = s.d_bdesc;
-		f.bmap = s.d_bmap;
-		f.bverdict = s.d_bverdict;
-		f.bres = s.d_bres;
-		f.btup = s.d_btup;
-		f.m = (uint32_t)mcap;
 		HIP_TRY(ctx, launch_frag_count(f, stream));
 	}
-	hipEvent_t *ev = nullptr;
-	if (ctx->tev && ctx->tn < XDPGPU_TIMING_MAX)
-		ev = ctx->tev + 4 * ctx->tn++;
-	HIP_TRY(ctx, launch_rx(a, ctx->cfg.window, ctx->max_blocks, stream,
-			       ctx->cfg.tune, ev));
+	HIP_TRY(ctx, launch_rx(a, ctx->max_blocks, stream, ctx->cfg.tune, ev));
 	/* the launch zeroed the other counter set: the next one uses it */
 	s.steal_set ^= 1;
-	if (a.frags && !bounce) {
-		/* one frame per packet, its fragments read where they lie */
+	if (a.frags)
 		HIP_TRY(ctx, launch_rx_packets(a, ctx->max_blocks, stream));
-	} else if (a.frags) {
-		/* one frame per packet: gathered into the bounce UMEM, the RX
-		 * kernels over the bounce batch, the outputs back to the
-		 * packets' descriptors */
-		HIP_TRY(ctx, launch_frag_gather(f, stream));
-		RxArgs b = a;
-		b.umem = s.d_bounce;
-		b.usize = f.bounce_cap;
-		b.desc = s.d_bdesc;
-		b.n = (uint32_t)mcap;
-		b.ndev = s.d_fc;
-		b.verdict = s.d_bverdict;
-		b.res = d_res ? s.d_bres : nullptr;
-		b.tup = d_tup ? s.d_btup : nullptr;
-		b.frags = 0;
-		HIP_TRY(ctx, launch_rx(b, ctx->cfg.window, ctx->max_blocks, stream,
-				       ctx->cfg.tune, nullptr));
-		HIP_TRY(ctx, launch_frag_scatter(f, stream));
-	}
 	return scratch_leave(ctx, s, stream);
 }
 

@@ -149,15 +149,10 @@ struct RxArgs {
 				    * (diagnostic kernel variants)          */
 	uint32_t v6;               /* set by the launcher: the fast shape
 				    * includes untagged IPv6/UDP           */
-	uint32_t order;            /* set by the launcher: xdp_rx_db_kernel's
-				    * tile order (cfg.tune bits 19-20)     */
-	uint32_t xshift;           /* set by the launcher: order 0's tile t
-				    * to block (t + xshift) mod nb, i.e. to
-				    * XCD (t + xshift) mod 8 (cfg.tune bits
-				    * 25-27; diagnostic)                   */
-	uint32_t partner;          /* set by the launcher: the heads a wave
-				    * claims shared tiles from, its own first
-				    * (1, 2 or 8; cfg.tune bits 28-29)     */
+	uint32_t partner;          /* set by the launcher: 2 a wave claims
+				    * shared tiles of its own head, then of
+				    * the partner head h ^ 4 (default); 1
+				    * its own head only (cfg.tune bit 28)  */
 	/* xdp_rx_db_kernel's shared tiles: the last steal_tiles tiles of the
 	 * batch are claimed at run time from kStealHeads global counters by
 	 * any block done with its own (set by the launcher; 0: none) */
@@ -169,15 +164,13 @@ struct RxArgs {
 				    * (0: none)                            */
 	uint32_t steal_tiles;      /* set by the launcher                  */
 	uint64_t xcap;             /* entries of each deferral list        */
-	const unsigned long long *ndev; /* nullable: the frame count lives on
-				    * the device (the bounce batch of
-				    * frags.hip); n is then its upper bound */
 };
 
-/* ev (nullable): four events recorded before the fast kernel and after
- * each of the fast, exception and bulk kernels (launch order) */
-hipError_t launch_rx(const RxArgs &a, uint32_t window, uint32_t max_blocks,
-		     hipStream_t stream, uint32_t tune, hipEvent_t *ev);
+/* The RX launch (xdp_rx_db_kernel).  ev (nullable): four events, the
+ * first before the kernel, the other three after it (the round-1 form timed
+ * three kernels in these slots). */
+hipError_t launch_rx(const RxArgs &a, uint32_t max_blocks, hipStream_t stream, uint32_t tune,
+		     hipEvent_t *ev);
 /* multi-buffer packets read in place (after launch_frag_count): every
  * complete packet of the batch as one frame, outputs to all its
  * descriptors */
@@ -189,9 +182,8 @@ uint32_t rx_grid_blocks(uint32_t n, uint32_t max_blocks);
 uint32_t rx_xregion(uint32_t n, uint32_t blocks);
 hipError_t launch_ceiling(const RxArgs &a, uint32_t blocks, hipStream_t stream);
 
-/* Multi-buffer packets (XDPGPU_CFG_FRAGS, frags.hip): count the packets of
- * several descriptors (and finish the broken ones), gather them into a
- * bounce UMEM as one frame each, scatter the bounce batch's outputs back. */
+/* Multi-buffer packets (XDPGPU_CFG_FRAGS, frags.hip): finish the packets
+ * the batch cannot complete as ABORTED (before launch_rx_packets). */
 struct FragArgs {
 	uint8_t *umem;
 	uint64_t usize;
@@ -202,21 +194,8 @@ struct FragArgs {
 	uint8_t *tup;              /* nullable */
 	uint32_t tb;               /* tuple bytes, 0 without tuples         */
 	unsigned long long *stats; /* block 0's counter slot, or null       */
-	unsigned long long *fc;    /* [0] packets, [1] bounce bytes         */
-	unsigned long long *blk;   /* per count/gather block: packets and
-				    * bounce bytes, then their prefixes     */
-	uint8_t *bounce;           /* gather, scatter */
-	uint64_t bounce_cap;       /* bytes; a packet past it is ABORTED    */
-	xdpgpu_desc *bdesc;        /* one per packet  */
-	uint2 *bmap;               /* first descriptor, descriptors         */
-	uint8_t *bverdict;
-	xdpgpu_result *bres;
-	uint8_t *btup;
-	uint32_t m;                /* upper bound of the packets (fc[0])    */
 };
 hipError_t launch_frag_count(const FragArgs &a, hipStream_t stream);
-hipError_t launch_frag_gather(const FragArgs &a, hipStream_t stream);
-hipError_t launch_frag_scatter(const FragArgs &a, hipStream_t stream);
 
 /* Host path write-back of ICMPv6 echo replies (xdpgpu_submit): for every
  * descriptor of the batch with verdict TX, bytes [0, min(len, 64)) of its

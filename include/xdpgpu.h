@@ -134,15 +134,19 @@ struct xdpgpu_cfg {
 	uint32_t max_batch;     /* max descriptors per host-path call (0: 2^20) */
 	uint32_t jhash_initval; /* initval of jhash (CLI option, default 0)    */
 	uint32_t tuple_fmt;     /* XDPGPU_TUPLE_*                              */
-	uint32_t window;        /* header bytes the exception path stages in
-				 * LDS: 64 or 128 (0: 64) */
-	uint32_t tune;          /* kernel variant (diagnostic): bits 0-7 waves per
-				 * SIMD, bit 8 exception kernel keeps its
-				 * payload sums, bit 9 exception path only,
-				 * bits 10-11 bulk-kernel variant, bit 14
-				 * host path without the mapped UMEM (span
-				 * copies, compact echo records);
-				 * 0 = default */
+	uint32_t window;        /* header bytes staged per frame: 64 (0: 64;
+				 * any other value is -EINVAL) */
+	uint32_t tune;          /* kernel variant (diagnostic, 0 = default):
+				 * bit 8 the exception pass keeps its payload
+				 * sums, bit 9 every frame through the
+				 * exception pass, bit 14 host path without
+				 * the mapped UMEM (span copies, compact echo
+				 * records), bits 16-17 no-compute / no-store
+				 * timing variants, bit 18 no IPv6 in the
+				 * fast shape, bit 21 no shared tiles, bit 28
+				 * no partner head; nat64: bits 12-13 no map
+				 * probe / no frame stores, bit 14 no shared
+				 * tiles */
 	uint32_t queue_id;      /* the RX queue this context serves (the XDP
 				 * program's ctx->rx_queue_index): its
 				 * counters add into that queue's

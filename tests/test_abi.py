@@ -33,7 +33,7 @@ def test_library_exports_every_header_symbol():
 def test_library_contains_gfx950_code_object():
     blob = open(xdpgpu.LIB_PATH, "rb").read()
     assert b"gfx950" in blob
-    assert b"xdp_rx_kernel" in blob
+    assert b"xdp_rx_db_kernel" in blob
 
 
 def test_abi_version_and_struct_sizes():

@@ -27,15 +27,11 @@ def to_dev(a: np.ndarray, pad: int = 64):
     return t
 
 
-# kernel variants (cfg.tune): default (one fused launch); the three-kernel
-# form (bit 15); every frame through the exception
-# kernel (its long payload sums deferred to the bulk kernel); the same with
-# the exception kernel keeping its payload sums; 6-wave fast kernel with the
-# 4-load plain bulk kernel; the fused launch with its other tile orders
-# (bits 19-20) and shared-tile fractions (bits 21-23: none, 4/16, 8/16, all,
-# 12/16; the default is 12/16), and an XCD shift of the default order (bits
-# 25-27)
-TUNES = [0, 1 << 15, 512, 512 | 256, 6 | (3 << 10), 1 << 10, 1 << 19, 2 << 19, 3 << 19, 1 << 21, 2 << 21, 3 << 21, 4 << 21, 5 << 21, 3 << 25, 1 << 28, 2 << 28]
+# kernel variants (cfg.tune): default (one fused launch); every frame through
+# the exception pipeline of the launch's tail (bit 9); the same with the
+# exception pass keeping its payload sums (bit 8); no shared tiles (bit 21);
+# shared tiles without the partner head (bit 28)
+TUNES = [0, 512, 512 | 256, 1 << 21, 1 << 28]
 
 
 def run_dev(umem, descs, flags=0x5, initval=0, fmt=1, window=64, tune=0):
@@ -87,16 +83,15 @@ def oracle_stats_match(st, ost):
 
 # ---------------------------------------------------------------- golden
 @pytest.mark.parametrize("tune", TUNES)
-@pytest.mark.parametrize("window", [64, 128])
 @pytest.mark.parametrize("cfg", ["verify", "echo_net", "noverify"])
-def test_golden_fixtures_device(dev, golden, cfg, window, tune):
+def test_golden_fixtures_device(dev, golden, cfg, tune):
     fx, meta = golden
     flags, iv, fmt = meta["cfgs"][cfg]
     descs = fx["descs"].view(xdpgpu.DESC_DTYPE)
-    v, res, tup, um, st = run_dev(fx["umem"], descs, flags, iv, fmt, window, tune)
+    v, res, tup, um, st = run_dev(fx["umem"], descs, flags, iv, fmt, 64, tune)
     want = (fx[f"{cfg}_verdict"], fx[f"{cfg}_res"].view(xdpgpu.RESULT_DTYPE),
             fx[f"{cfg}_tup"], fx[f"{cfg}_umem_after"])
-    assert_same((v, res, tup, um), want, f"golden/{cfg}/w{window}")
+    assert_same((v, res, tup, um), want, f"golden/{cfg}")
     ws = fx[f"{cfg}_stats"]
     assert st["frames"] == ws[0] and st["bytes"] == ws[1]
     assert [st["verdict"][n] for n in xdpgpu.VERDICT_NAMES] == list(ws[2:7])
@@ -130,15 +125,14 @@ POOLS = [
 
 
 @pytest.mark.parametrize("tune", TUNES)
-@pytest.mark.parametrize("window", [64, 128])
 @pytest.mark.parametrize("name,kind,size,seed,n,kw", POOLS, ids=[p[0] for p in POOLS])
-def test_pool_vs_oracle(dev, name, kind, size, seed, n, kw, window, tune):
+def test_pool_vs_oracle(dev, name, kind, size, seed, n, kw, tune):
     umem, descs, expect = xdpgpu.pool_generate(n, kind, size, seed, **kw)
     for flags, iv, fmt in ((0x5, 0, 1), (0x7, 0x9E3779B9, 2)):
         ou = umem.copy()
         ov, ores, otup, ost = oracle.process(ou, descs, flags, iv, fmt)
-        v, res, tup, um, st = run_dev(umem, descs, flags, iv, fmt, window, tune)
-        assert_same((v, res, tup, um), (ov, ores, otup, ou), f"{name}/w{window}/{flags:#x}")
+        v, res, tup, um, st = run_dev(umem, descs, flags, iv, fmt, 64, tune)
+        assert_same((v, res, tup, um), (ov, ores, otup, ou), f"{name}/{flags:#x}")
         oracle_stats_match(st, ost)
         if flags == 0x5:
             np.testing.assert_array_equal(v, expect)
@@ -212,7 +206,7 @@ def test_bulk_lengths_vs_oracle(dev, tune):
             assert (ov == xdpgpu.REDIRECT).sum() > 2000 and (ov == xdpgpu.DROP).sum() > 100
 
 
-@pytest.mark.parametrize("tune", [0, 1 << 15, 1 << 21])
+@pytest.mark.parametrize("tune", [0, 512, 1 << 21])
 @pytest.mark.parametrize("aligned", [True, False])
 def test_short_bulk_vs_oracle(dev, tune, aligned):
     """Bulk batches whose ranges all end within 64 bytes of the window
@@ -462,7 +456,7 @@ def test_v6_late_frames_cover_aborted_tcp():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tune", [0, 1 << 21, 4 << 21])
+@pytest.mark.parametrize("tune", [0, 512, 1 << 21])
 def test_v6_late_frames_vs_oracle(dev, tune):
     """Tagged IPv6 and IPv6/TCP through the network_tuple / no-tuple builds
     (late check words and data offsets in the bulk pass) against the
@@ -477,7 +471,7 @@ def test_v6_late_frames_vs_oracle(dev, tune):
         oracle_stats_match(st, ost)
 
 
-@pytest.mark.parametrize("tune", [0, 1 << 15, 1 << 21])
+@pytest.mark.parametrize("tune", [0, 512, 1 << 21])
 def test_v6_build_icmp_vs_oracle(dev, golden, tune):
     """The IPv6 builds (network_tuple, no tuple, and any tuple with the echo
     responder): IPv4 ICMP and ICMPv6 other than NDP go through the fast
