@@ -302,8 +302,9 @@ def side_run(ctx, tctx, dev, stream, n, kind, size, seed, fmt, steps, label, bpf
            "ms_per_launch": round(w / steps * 1e3, 4),
            "gbps": round(algo / w * steps / 1e9, 1),
            "roofline_frac": round(algo / w * steps / 1e9 / HBM_PEAK_GBS, 4),
-           "roofline_frac_kernel": round(algo / (kt["total_ms"] / max(kt["launches"], 1) *
-                                                 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           # the same bytes over the HIP-event launch time (kernel_times()
+           # averages over its launches)
+           "roofline_frac_kernel": round(algo / (kt["total_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
            "kernel_ms": kt_round(kt), "verdicts_ok": ok}
     del g_umem, g_desc, g_v, g_res, g_tup
     torch.cuda.empty_cache()

@@ -2558,6 +2558,10 @@ constexpr int kCuBlock = kCuWaves * kWave;
 #ifndef XDP_DESC_AUX
 #define XDP_DESC_AUX 0
 #endif
+/* cache policy of the tile loop's window DMA (build knob for A/B): nt */
+#ifndef XDP_WIN_AUX
+#define XDP_WIN_AUX 2
+#endif
 template <bool FRAGS, int DIAG = 0, bool V6 = false>
 __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 {
@@ -2645,7 +2649,7 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 				ef = 0;
 			__builtin_amdgcn_global_load_lds(
 				(const void *)(a.umem + ef + 16 * c),
-				(lds_void_t *)(buf + kWave * k), 16, 0, 2 /* nt */);
+				(lds_void_t *)(buf + kWave * k), 16, 0, XDP_WIN_AUX);
 		}
 	};
 	/* DMA of a tile's 64 descriptors into a slot (lane l: descriptor l) */

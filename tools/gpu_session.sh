@@ -68,10 +68,10 @@ workload() {
 	nat64_dynamic) echo "python3 tools/nat_dyn_probe.py --frames 16777216 --reps 5" ;;
 	frags) echo "python3 tools/frags_probe.py --reps 5" ;;
 	frags_bounce) echo "python3 tools/frags_probe.py --reps 5 --tune 0x1000000" ;;
-	synproxy) echo "python3 bench.py --no-cpu --legs synproxy --steps 5 --warmup 2" ;;
-	echo) echo "python3 bench.py --no-cpu --legs echo --steps 5 --warmup 2" ;;
-	bench) echo "python3 bench.py --no-cpu --no-secondary --steps 20" ;;
-	bench50) echo "python3 bench.py --no-cpu --no-secondary --steps 50" ;;
+	synproxy) echo "python3 bench.py --no-cpu --no-e2e --legs synproxy --steps 5 --warmup 2" ;;
+	echo) echo "python3 bench.py --no-cpu --no-e2e --legs echo --steps 5 --warmup 2" ;;
+	bench) echo "python3 bench.py --no-cpu --no-secondary --no-e2e --steps 20" ;;
+	bench50) echo "python3 bench.py --no-cpu --no-secondary --no-e2e --steps 50" ;;
 	*) echo "unknown workload $1" >&2; exit 2 ;;
 	esac
 }
@@ -148,7 +148,7 @@ for s in "$@"; do
 			python3 -u tools/stamps.py ${arg//+/ } ;;
 	probe) step probe 120 tools/order_probe 64 ;;
 	hbm) step "hbm_${arg:-all}" 300 tools/hbm_probe $arg ;;
-	e2e) step e2e 600 python3 bench.py --no-cpu --no-secondary --steps 10 --e2e ;;
+	e2e) step e2e 600 python3 bench.py --no-cpu --no-secondary --steps 10 ;;
 	cli) step cli 300 bpf-examples_amd/apps/xdpsock-gpu --pool 16777216 --pool-kind udp4 \
 		-b 1048576 -C 67108864 --json -Q ;;
 	*) echo "unknown step $s"; exit 2 ;;
