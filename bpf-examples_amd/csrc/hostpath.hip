@@ -9,12 +9,10 @@
  * of the UMEM belongs to the application and the kernel (fill ring frames
  * the NIC may be filling), SURVEY §8b.  So for every descriptor of the
  * batch whose verdict is TX this kernel copies bytes [0, min(len, 64)) of
- * its frame, and nothing else:
- *  - straight into the host UMEM through its mapped pinned pointer (the
- *    writes cross PCIe as posted writes; they are visible to the host once
- *    the slot's completion event has fired), or
- *  - as compact 80-byte records (EchoRec) that xdpgpu_wait scatters, when
- *    the UMEM is not mapped.
+ * its frame, and nothing else, as compact 80-byte records (EchoRec) that
+ * xdpgpu_wait scatters on the host.  (Until round 4 the kernel could also
+ * write them straight into the mapped pinned UMEM; no kernel touches host
+ * memory any more)
  * Multi-buffer packets: each fragment of a TX packet has verdict TX, and
  * packet byte p < 64 lies at offset <= p of its fragment, so the fragments'
  * first 64 bytes cover the rewrite.
@@ -56,11 +54,9 @@ __global__ __launch_bounds__(kEchoBlock) void echo_writeback_kernel(EchoArgs a)
 	if (!m)
 		return;
 	uint32_t base = 0;
-	if (!a.host) {
-		if (lane == 0)
-			base = atomicAdd(a.nrec, (uint32_t)__popcll(m));
-		base = __builtin_amdgcn_readfirstlane(base);
-	}
+	if (lane == 0)
+		base = atomicAdd(a.nrec, (uint32_t)__popcll(m));
+	base = __builtin_amdgcn_readfirstlane(base);
 	uint32_t r = 0;
 	for (uint64_t k = m; k; k &= k - 1, r++) {
 		const int src = __builtin_ctzll(k);
@@ -68,17 +64,12 @@ __global__ __launch_bounds__(kEchoBlock) void echo_writeback_kernel(EchoArgs a)
 				    rl32((uint32_t)eff, src);
 		const uint32_t sw = rl32(w, src);
 		const uint8_t b = (uint32_t)lane < sw ? a.mirror[se + lane] : 0;
-		if (a.host) {
-			if ((uint32_t)lane < sw)
-				a.host[se + lane] = b;
-		} else {
-			EchoRec *rec = a.rec + base + r;
-			rec->b[lane] = b;
-			if (lane == 0) {
-				rec->eff = se;
-				rec->len = sw;
-				rec->rsvd = 0;
-			}
+		EchoRec *rec = a.rec + base + r;
+		rec->b[lane] = b;
+		if (lane == 0) {
+			rec->eff = se;
+			rec->len = sw;
+			rec->rsvd = 0;
 		}
 	}
 }

@@ -4,8 +4,8 @@
  *
  * A context owns one device, two HIP streams (two in-flight RX batches), a
  * device mirror of the registered host UMEM and per-block counter slots.
- * The host path copies the UMEM span a batch touches (or, for a sparse
- * batch, lets the kernel read the pinned UMEM in place), the descriptors,
+ * The host path copies the UMEM runs a batch touches into the slot's device
+ * mirror (no kernel ever reads or writes host memory), the descriptors,
  * launches the RX kernel and copies verdicts/results/tuples back.
  */
 #include <hip/hip_runtime.h>
@@ -87,7 +87,9 @@ struct xdpgpu_ctx {
 	uint8_t *h_umem = nullptr;
 	uint64_t umem_size = 0;
 	bool pinned = false;
-	uint8_t *d_umem_mapped = nullptr; /* device view of pinned host UMEM */
+	/* the last device UMEM a *_dev call was checked for (device memory
+	 * only: no kernel of the library dereferences host memory) */
+	const void *dev_ok = nullptr;
 	/* XDPGPU_CFG_TIMING: 4 events per recorded launch */
 	hipEvent_t *tev = nullptr;
 	/* nat64 translator (xdpgpu_nat64_setup) */
@@ -354,7 +356,6 @@ static void release_umem(xdpgpu_ctx *ctx)
 	ctx->pinned = false;
 	ctx->h_umem = nullptr;
 	ctx->umem_size = 0;
-	ctx->d_umem_mapped = nullptr;
 }
 
 /* A slot's device mirror of the registered UMEM (+64: 16-byte loads of a
@@ -391,16 +392,16 @@ int xdpgpu_register_umem(xdpgpu_ctx *ctx, void *base, uint64_t size,
 	release_umem(ctx);
 	ctx->h_umem = (uint8_t *)base;
 	ctx->umem_size = size;
-	/* pin (and map) the caller's UMEM; pageable memory still works,
-	 * only slower */
-	if (hipHostRegister(base, size, hipHostRegisterMapped) == hipSuccess) {
+	/* pin the caller's UMEM for the copy engines (pageable memory still
+	 * works, only slower).  No kernel reads or writes it: every batch's
+	 * frames are copied into the slot's device mirror and the echo
+	 * replies come back as compact records (the host
+	 * memory faults of rounds 2-3 all followed kernels that dereferenced
+	 * this UMEM through its GPU mapping) */
+	if (hipHostRegister(base, size, hipHostRegisterDefault) == hipSuccess)
 		ctx->pinned = true;
-		void *dp = nullptr;
-		if (hipHostGetDevicePointer(&dp, base, 0) == hipSuccess)
-			ctx->d_umem_mapped = (uint8_t *)dp;
-	} else {
+	else
 		(void)hipGetLastError();
-	}
 	/* slot 0's mirror now, so that a size the device cannot hold fails
 	 * here; slot 1's on its first batch */
 	const int rc = ensure_mirror(ctx, ctx->slot[0]);
@@ -607,6 +608,28 @@ int xdpgpu_kernel_times(xdpgpu_ctx *ctx, xdpgpu_ktimes *out)
 	return 0;
 }
 
+/* The UMEM of a *_dev call must be device memory: no kernel of the
+ * library dereferences host memory (pinned or mapped host memory read or
+ * written through its GPU mapping is what the host-memory faults of
+ * rounds 2-3 had in common).  One pointer query per new
+ * UMEM (the last one checked is remembered). */
+static int check_dev_umem(xdpgpu_ctx *ctx, const void *p)
+{
+	if (p == ctx->dev_ok)
+		return 0;
+	hipPointerAttribute_t at;
+	memset(&at, 0, sizeof(at));
+	if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+		(void)hipGetLastError();
+		return set_err(ctx, -EINVAL, "UMEM %p is not device memory", p);
+	}
+	if (at.type != hipMemoryTypeDevice && !at.isManaged)
+		return set_err(ctx, -EINVAL, "UMEM %p is host memory (type %d): the kernels "
+			       "read device memory only", p, (int)at.type);
+	ctx->dev_ok = p;
+	return 0;
+}
+
 int xdpgpu_process_dev(xdpgpu_ctx *ctx, void *d_umem, uint64_t umem_size,
 		       const xdpgpu_desc *d_descs, uint32_t n,
 		       uint8_t *d_verdict, xdpgpu_result *d_res, void *d_tuples,
@@ -616,6 +639,9 @@ int xdpgpu_process_dev(xdpgpu_ctx *ctx, void *d_umem, uint64_t umem_size,
 		return -EINVAL;
 	if (n == 0)
 		return 0;
+	int rc = check_dev_umem(ctx, d_umem);
+	if (rc)
+		return rc;
 	hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
 	return enqueue_rx(ctx, ctx->slot[0], (uint8_t *)d_umem, umem_size,
 			  d_descs, n, d_verdict, d_res, (uint8_t *)d_tuples, st);
@@ -855,6 +881,8 @@ int xdpgpu_nat64_dev(xdpgpu_ctx *ctx, void *d_umem, uint64_t umem_size,
 		return set_err(ctx, -EINVAL, "xdpgpu_nat64_setup not called");
 	if (n == 0)
 		return 0;
+	if (int rc0 = check_dev_umem(ctx, d_umem))
+		return rc0;
 	Nat64Args a;
 	memset(&a, 0, sizeof(a));
 	a.umem = (uint8_t *)d_umem;
@@ -960,6 +988,8 @@ int xdpgpu_synproxy_dev(xdpgpu_ctx *ctx, void *d_umem, uint64_t umem_size,
 	if (n == 0)
 		return 0;
 	HIP_TRY(ctx, hipSetDevice(ctx->cfg.device));
+	if (int rc0 = check_dev_umem(ctx, d_umem))
+		return rc0;
 	hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
 	if (d_synacks && !ctx->d_spread) {
 		/* the SYN-ACK counters, zeroed once: each launch's sum kernel
@@ -1002,11 +1032,14 @@ int xdpgpu_ceiling_dev(xdpgpu_ctx *ctx, const void *d_umem, uint64_t umem_size,
 	return 0;
 }
 
-/* The UMEM bytes a batch reads, as runs of nearby frames (gaps up to
- * kRunGap bytes are copied along): one run for a batch of consecutive
- * frames, two for a batch that wraps round a cyclic fill ring.  More than
- * kMaxRuns runs: the batch is scattered over the UMEM, and runs is left
- * empty.  [lo, hi) is the span of all of them; used the bytes the
+/* The UMEM bytes a batch reads, as at most kMaxRuns runs of nearby frames
+ * (gaps up to kRunGap bytes are copied along): one run for a batch of
+ * consecutive frames, two for a batch that wraps round a cyclic fill ring,
+ * found in descriptor order.  A batch scattered over the UMEM (more runs
+ * than that in descriptor order: a recycled fill ring) is sorted by
+ * address and merged with the smallest gap (kRunGap, x4, ...) that leaves
+ * at most kMaxRuns runs, so that its copies stay few and close to the
+ * bytes it names.  [lo, hi) is the span of all of them; used the bytes the
  * descriptors name.  +1 byte per frame: udp_csum's odd over-read. */
 struct Run {
 	uint64_t lo, hi;
@@ -1043,10 +1076,32 @@ static void batch_runs(const xdpgpu_ctx *ctx, const xdpgpu_desc *descs,
 		}
 		if (runs.size() == kMaxRuns) {
 			scattered = true;
-			runs.clear();
 			continue;
 		}
 		runs.push_back({eff, end});
+	}
+	if (!scattered)
+		return;
+	std::vector<Run> fr;
+	fr.reserve(n);
+	for (uint32_t i = 0; i < n; i++) {
+		const uint64_t eff = (descs[i].addr & ((1ull << 48) - 1)) +
+				     (descs[i].addr >> 48);
+		if (eff < ctx->umem_size)
+			fr.push_back({eff, std::min<uint64_t>(eff + descs[i].len + 1,
+							     ctx->umem_size)});
+	}
+	std::sort(fr.begin(), fr.end(), [](const Run &x, const Run &y) { return x.lo < y.lo; });
+	for (uint64_t gap = kRunGap;; gap *= 4) {
+		runs.clear();
+		for (const Run &r : fr) {
+			if (!runs.empty() && r.lo <= runs.back().hi + gap)
+				runs.back().hi = std::max(runs.back().hi, r.hi);
+			else
+				runs.push_back(r);
+		}
+		if (runs.size() <= kMaxRuns)
+			return;
 	}
 }
 
@@ -1078,44 +1133,19 @@ int xdpgpu_submit(xdpgpu_ctx *ctx, uint32_t slot, const xdpgpu_desc *descs,
 	uint64_t lo, hi, used;
 	batch_runs(ctx, descs, n, runs, lo, hi, used);
 	const bool echo = ctx->cfg.flags & XDPGPU_CFG_ICMP6_ECHO;
-	const bool mapped_ok = ctx->d_umem_mapped && !(ctx->umem_size & 15) &&
-			       !((ctx->cfg.tune >> 14) & 1);
-	uint8_t *kumem = s.d_mirror;
-	bool zero_copy = false;
-	if (hi > lo) {
-		uint64_t copy = 0;
-		for (const Run &r : runs)
-			copy += r.hi - r.lo;
-		if (runs.empty())
-			copy = hi - lo;
-		/* sparse batch over pinned memory: the kernels read the frames
-		 * in place (and an echo rewrite lands in the host UMEM) */
-		if (mapped_ok && copy > 4 * used + (1u << 20)) {
-			kumem = ctx->d_umem_mapped;
-			zero_copy = true;
-		} else if (runs.empty()) {
-			HIP_TRY(ctx, hipMemcpyAsync(s.d_mirror + lo, ctx->h_umem + lo,
-						    hi - lo, hipMemcpyHostToDevice,
-						    s.stream));
-		} else {
-			for (const Run &r : runs)
-				HIP_TRY(ctx, hipMemcpyAsync(s.d_mirror + r.lo,
-							    ctx->h_umem + r.lo,
-							    r.hi - r.lo,
-							    hipMemcpyHostToDevice,
-							    s.stream));
-		}
-	}
+	for (const Run &r : runs)
+		HIP_TRY(ctx, hipMemcpyAsync(s.d_mirror + r.lo, ctx->h_umem + r.lo, r.hi - r.lo,
+					    hipMemcpyHostToDevice, s.stream));
 	HIP_TRY(ctx, hipMemcpyAsync(s.d_desc, descs, (size_t)n * sizeof(*descs),
 				    hipMemcpyHostToDevice, s.stream));
 	uint8_t *d_tup = (tuples && ctx->cfg.tuple_fmt) ? s.d_tup : nullptr;
-	rc = enqueue_rx(ctx, s, kumem, ctx->umem_size, s.d_desc, n, s.d_verdict,
+	rc = enqueue_rx(ctx, s, s.d_mirror, ctx->umem_size, s.d_desc, n, s.d_verdict,
 			res ? s.d_res : nullptr, d_tup, s.stream);
 	if (rc)
 		return rc;
 	/* echo replies were written in the mirror: only the TX frames' first
 	 * bytes go back to the host UMEM (SURVEY §8b ownership) */
-	if (echo && !zero_copy) {
+	if (echo) {
 		EchoArgs e;
 		memset(&e, 0, sizeof(e));
 		e.mirror = s.d_mirror;
@@ -1123,9 +1153,7 @@ int xdpgpu_submit(xdpgpu_ctx *ctx, uint32_t slot, const xdpgpu_desc *descs,
 		e.desc = s.d_desc;
 		e.verdict = s.d_verdict;
 		e.n = n;
-		if (ctx->d_umem_mapped && !((ctx->cfg.tune >> 14) & 1)) {
-			e.host = ctx->d_umem_mapped;
-		} else {
+		{
 			if (s.erec_cap < n) {
 				HIP_TRY(ctx, hipStreamSynchronize(s.stream));
 				(void)hipFree(s.d_erec);
@@ -1326,6 +1354,8 @@ int xdpgpu_hints_dev(xdpgpu_ctx *ctx, const void *d_umem, uint64_t umem_size,
 		return -EINVAL;
 	if (n == 0)
 		return 0;
+	if (int rc0 = check_dev_umem(ctx, d_umem))
+		return rc0;
 	hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
 	HIP_TRY(ctx, launch_hints((const uint8_t *)d_umem, umem_size, d_descs, n,
 				  rx_time_btf_id, mark_btf_id, d_out, st));

@@ -149,6 +149,9 @@ struct RxArgs {
 				    * (diagnostic kernel variants)          */
 	uint32_t v6;               /* set by the launcher: the fast shape
 				    * includes untagged IPv6/UDP           */
+	uint32_t inlb;             /* set by the launcher: bulk frames
+				    * finished inline in the tile loop
+				    * (xdp_rx_db_kernel INLB)              */
 	uint32_t partner;          /* set by the launcher: 2 a wave claims
 				    * shared tiles of its own head, then of
 				    * the partner head h ^ 4 (default); 1
@@ -200,10 +203,9 @@ hipError_t launch_frag_count(const FragArgs &a, hipStream_t stream);
 /* Host path write-back of ICMPv6 echo replies (xdpgpu_submit): for every
  * descriptor of the batch with verdict TX, bytes [0, min(len, 64)) of its
  * frame (the rewrite of process_packet, af_xdp_user.c:990-1037, touches
- * bytes 0-57) go from the slot's device mirror to the host UMEM: straight
- * through the mapped pinned UMEM (host non-null), or as compact records
- * the host scatters after xdpgpu_wait.  Nothing else of the UMEM is
- * written. */
+ * bytes 0-57) go from the slot's device mirror to the host UMEM as compact
+ * records the host scatters after xdpgpu_wait (no kernel writes host
+ * memory).  Nothing else of the UMEM is written. */
 constexpr uint32_t kEchoBytes = 64;
 struct EchoRec {
 	uint64_t eff;              /* frame's UMEM offset                   */
@@ -214,12 +216,11 @@ struct EchoRec {
 static_assert(sizeof(EchoRec) == 80, "echo record layout");
 struct EchoArgs {
 	const uint8_t *mirror;
-	uint8_t *host;             /* mapped host UMEM or null              */
 	uint64_t usize;
 	const xdpgpu_desc *desc;
 	const uint8_t *verdict;
 	uint32_t n;
-	EchoRec *rec;              /* host null: one record per TX frame    */
+	EchoRec *rec;              /* one record per TX frame               */
 	uint32_t *nrec;
 };
 hipError_t launch_echo_writeback(const EchoArgs &a, hipStream_t stream);

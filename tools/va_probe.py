@@ -74,3 +74,44 @@ for nbytes in (2 << 20, 71 << 20):
     rec["hsa_host_after"] = hostreg.scan(hp, 1)
     res.setdefault("registered", []).append(rec)
 print(json.dumps(res, indent=1))
+
+# -- a device allocation freed back to the runtime: does its VA leave the
+# process's maps and the runtime's table together?  (No kernel touches
+# anything below; registration is driver bookkeeping.)
+import mmap as _mm  # noqa: E402
+
+libc = C.CDLL("libc.so.6", use_errno=True)
+libc.mmap.restype = C.c_void_p
+libc.mmap.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_int, C.c_long]
+libc.munmap.argtypes = [C.c_void_p, C.c_size_t]
+MAP_FIXED_NOREPLACE = 0x100000
+freed = []
+for nbytes in (66 << 20, 8 << 20):
+    t = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    p = t.data_ptr()
+    before = {"cpu_maps": covering(maps(), p, p + nbytes), "hsa": hostreg.scan(p, 1)}
+    del t
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    torch.cuda.synchronize()
+    after = {"cpu_maps": covering(maps(), p, p + nbytes), "hsa": hostreg.scan(p, 1)}
+    rec = {"ptr": hex(p), "bytes": nbytes, "live": before, "after_free": after}
+    # a host mapping at exactly that VA, if the CPU side is free
+    q = libc.mmap(p, nbytes, 3, 0x22 | MAP_FIXED_NOREPLACE, -1, 0)   # RW, PRIVATE|ANON
+    rec["host_mmap_at_freed_va"] = hex(q) if q and q != C.c_void_p(-1).value else \
+        f"failed errno {C.get_errno()}"
+    if q == p:
+        rec["hsa_over_host_mapping"] = hostreg.scan(p, 1)
+        rc = hip.hipHostRegister(p, nbytes, 1)
+        dp = C.c_void_p()
+        rc2 = hip.hipHostGetDevicePointer(C.byref(dp), p, 0)
+        rec["register"] = {"rc": rc, "devptr_rc": rc2, "devptr": hex(dp.value or 0),
+                           "hsa": hostreg.scan(p, 1)}
+        rec["unregister_rc"] = hip.hipHostUnregister(p)
+        rec["hsa_after_unregister"] = hostreg.scan(p, 1)
+        libc.munmap(p, nbytes)
+    t2 = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    rec["next_alloc_same_size"] = hex(t2.data_ptr())
+    del t2
+    freed.append(rec)
+print(json.dumps({"freed_device_va": freed}, indent=1))
