@@ -505,7 +505,7 @@ def frags_run(dev, stream, n, steps, local, size=9000, chunk=4096):
     return out
 
 
-def echo_run(dev, stream, n, steps, local, size=128, ppm=200000):
+def echo_run(dev, stream, n, steps, local, size=128, ppm=200000, tune=0):
     """The ICMPv6 echo responder (af_xdp_user.c:968-1040) as a throughput
     mode: n frames of which ppm / 1e6 are echo requests, rewritten in place
     into replies (TX).  The rewrite changes the UMEM, so every step
@@ -526,7 +526,7 @@ def echo_run(dev, stream, n, steps, local, size=128, ppm=200000):
     d_tup = torch.empty(n * 16, dtype=torch.uint8, device=dev)
     ms = []
     with xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT | xdpgpu.CFG_ICMP6_ECHO, 0,
-                       xdpgpu.TUPLE_V4, 64) as g:
+                       xdpgpu.TUPLE_V4, 64, tune=tune) as g:
         for k in range(steps + 2):
             with torch.cuda.stream(stream):
                 work.copy_(pristine, non_blocking=True)
@@ -567,6 +567,8 @@ def main():
                     help="secondary workloads: comma list of 1500, imix, nat64, frags, echo")
     ap.add_argument("--imix-frames", type=int, default=16 << 20)
     ap.add_argument("--nat64-frames", type=int, default=16 << 20)
+    ap.add_argument("--tune", type=lambda x: int(x, 0), default=0,
+                    help="cfg.tune of the secondary legs' contexts (diagnostic A/B)")
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the end-to-end host path (pinned H2D + kernel + D2H)")
     args = ap.parse_args()
@@ -650,7 +652,8 @@ def main():
         if "frags" in legs:
             secondary["multibuffer_9000B"] = frags_run(dev, stream, 1 << 16, steps2, local)
         if "echo" in legs:
-            secondary["icmp6_echo"] = echo_run(dev, stream, 8 << 20, steps2, local)
+            secondary["icmp6_echo"] = echo_run(dev, stream, 8 << 20, steps2, local,
+                                               tune=args.tune)
         if "synproxy" in legs:
             secondary["synproxy"] = synproxy_run(dev, stream, 8 << 20, steps2, local)
 

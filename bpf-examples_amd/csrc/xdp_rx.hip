@@ -1303,7 +1303,8 @@ constexpr bool kBulkVerdictTile = XDP_BULK_VERDICT_TILE != 0;
 #endif
 constexpr bool kQuick = XDP_QUICK != 0;
 /* tiles with no tagged frame skip the tag shift of the window words
- * (fast_tile; build knob) */
+ * (fast_tile; build knob): config 2 0.3185 / 0.3315 vs 0.3344 / 0.3406 ms
+ * per step without, alternating processes (profiles/r04_ab_untagged.txt) */
 #ifndef XDP_UNTAGGED_TILES
 #define XDP_UNTAGGED_TILES 1
 #endif
@@ -1342,11 +1343,6 @@ constexpr bool kTup6Tile = XDP_TUP6_TILE != 0;
 #define XDP_TAIL_ADAPT 1
 #endif
 constexpr bool kTailAdapt = XDP_TAIL_ADAPT != 0;
-/* group sizes of the inline batches (build knob): 2 = 4, 8 or 16 lanes
- * by the batch's longest range, 1 = 4 or 16, 0 = 16 only */
-#ifndef XDP_INL_ADAPT
-#define XDP_INL_ADAPT 2
-#endif
 /* Batches of ranges within 64 bytes streamed in one step (stream_short;
  * build knob, off: DESIGN.md §5.2) */
 #ifndef XDP_TAIL_SHORT
@@ -1455,88 +1451,12 @@ __device__ __forceinline__ void stream_short(const RxArgs &a, const uint4 *meta,
 	}
 }
 
-/* stream_groups for a batch whose ranges live in registers, one frame per
- * lane (ml/mh: the range's 16-byte aligned start, mz its bytes from there,
- * mw the bytes skipped at the start), with no LDS but 64 words: a group
- * reduces its partial sums across its G lanes when it finishes a frame
- * and its first lane writes the frame's sum to psum[k] (the inline bulk
- * batches of the tile loop, whose LDS the DMA pipeline owns). */
-template <int G, int U, bool NT>
-__device__ __forceinline__ void stream_groups_inl(const RxArgs &a, uint32_t ml, uint32_t mh,
-						  uint32_t mz, uint32_t mw, uint32_t *psum,
-						  int lane, uint32_t nb)
-{
-	static_assert(G == 16 || G == 8 || G == 4, "group of 16, 8 or 4 lanes per frame");
-	const uint32_t sub = lane & (G - 1);
-	uint32_t k = lane / G;
-	uint32_t nxt = kWave / G;
-	bool live = k < nb;
-	auto fetch = [&](uint32_t kk, uint64_t &flo, uint32_t &fnb, uint32_t &fsk) {
-		const int src = (int)(kk < nb ? kk : 0);
-		flo = ((uint64_t)(uint32_t)__shfl((int)mh, src, kWave) << 32) |
-		      (uint32_t)__shfl((int)ml, src, kWave);
-		fnb = (uint32_t)__shfl((int)mz, src, kWave);
-		fsk = (uint32_t)__shfl((int)mw, src, kWave);
-	};
-	uint64_t flo;
-	uint32_t fnb, fsk, o = 0, acc = 0;
-	fetch(k, flo, fnb, fsk);
-	while (__ballot(live)) {
-		uint4 v[U];
-#pragma unroll
-		for (int u = 0; u < U; u++) {
-			const uint32_t ou = o + 16 * G * u + 16 * sub;
-			v[u] = make_uint4(0, 0, 0, 0);
-			if (live && ou < fnb)
-				v[u] = NT ? ld_nt16(a.umem + flo + ou)
-					  : *reinterpret_cast<const uint4 *>(a.umem + flo + ou);
-		}
-#pragma unroll
-		for (int u = 0; u < U; u++) {
-			const uint32_t ou = o + 16 * G * u + 16 * sub;
-			if ((ou + 16 > fnb || ou < fsk) && ou < fnb) {
-				const uint4 mk = chunk_keep(ou, fsk, fnb);
-				v[u].x &= mk.x;
-				v[u].y &= mk.y;
-				v[u].z &= mk.z;
-				v[u].w &= mk.w;
-			}
-			acc += halves(v[u].x) + halves(v[u].y) + halves(v[u].z) + halves(v[u].w);
-		}
-		o += 16 * G * U;
-		const bool done = live && o >= fnb;
-		const uint64_t dq = __ballot(done && sub == 0);
-		if (dq) {
-			/* every lane takes part in the group sums (no divergent
-			 * shuffles); the finished groups' first lanes publish */
-			uint32_t red = acc;
-#pragma unroll
-			for (int m = G / 2; m >= 1; m >>= 1)
-				red += (uint32_t)__shfl_xor((int)red, m, kWave);
-			if (done) {
-				if (sub == 0)
-					psum[k] = red;
-				acc = 0;
-				k = nxt + (uint32_t)__popcll(dq & ((1ull << (lane & ~(G - 1))) - 1));
-				live = k < nb;
-				o = 0;
-			}
-			fetch(k, flo, fnb, fsk);
-			nxt += (uint32_t)__popcll(dq);
-		}
-	}
-}
-
-/* INL: the tile loop's inline batch (xdp_rx_db_kernel's INLB builds): the
- * lane's frame index is inl_i, the ranges stay in registers and the sums
- * go through psum (64 words of LDS) instead of meta and part4. */
-template <int U, bool NT, bool GEN, int G, bool INL = false>
+template <int U, bool NT, bool GEN, int G>
 __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 					   uint4 *part4, int lane,
 					   const void *list, uint32_t nb,
 					   uint32_t (&cnt)[CNT_FRAG + 1],
-					   uint64_t &my_bytes, uint32_t inl_i = 0,
-					   uint32_t *psum = nullptr)
+					   uint64_t &my_bytes)
 {
 	uint32_t *part = reinterpret_cast<uint32_t *>(part4);
 	const bool act = (uint32_t)lane < nb;
@@ -1545,8 +1465,6 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 	if constexpr (GEN) {
 		ye = reinterpret_cast<const uint4 *>(list)[act ? lane : 0];
 		i = ye.x;
-	} else if constexpr (INL) {
-		i = act ? inl_i : 0;
 	} else {
 		i = reinterpret_cast<const uint32_t *>(list)[act ? lane : 0];
 	}
@@ -1574,7 +1492,7 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 	const bool tup6 = net6 && !kTup6Tile;
 	/* an untagged ICMPv6 frame under the echo responder: its first 64
 	 * bytes, for the type and the rewrite */
-	const bool echo6 = !GEN && !INL && act && r6 && (a.flags & XDPGPU_CFG_ICMP6_ECHO) &&
+	const bool echo6 = !GEN && act && r6 && (a.flags & XDPGPU_CFG_ICMP6_ECHO) &&
 			   ((rv.z >> 8) & 0xff) == 58 && (rv.z >> 24) == 0;
 	uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0, h2 = h0, h3 = h0;
 	if (tup6 || echo6) {
@@ -1597,12 +1515,10 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 	const uint64_t lo = eff + (GEN ? (ye.z & 0xffff) : 64u);
 	const uint64_t lo_al = lo & ~15ull;
 	uint32_t t = 0;
-	const uint4 me = make_uint4((uint32_t)lo_al, (uint32_t)(lo_al >> 32),
-				    (uint32_t)(lim > lo ? lim - lo_al : 0), (uint32_t)(lo - lo_al));
-	if constexpr (!INL) {
-		meta[lane] = me;
-		__builtin_amdgcn_wave_barrier();
-	}
+	meta[lane] = make_uint4((uint32_t)lo_al, (uint32_t)(lo_al >> 32),
+				(uint32_t)(lim > lo ? lim - lo_al : 0),
+				(uint32_t)(lo - lo_al));
+	__builtin_amdgcn_wave_barrier();
 
 	/* the group size: 16 lanes per frame, fewer when every range of the
 	 * batch is short (the echo leg's 128-byte frames: 4 lanes, 16 frames
@@ -1612,42 +1528,30 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 #pragma unroll
 	for (int d = 1; d < kWave; d <<= 1)
 		mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, kWave));
-	if constexpr (INL) {
-		if (XDP_INL_ADAPT && mx <= 64 * U)
-			stream_groups_inl<4, U, NT>(a, me.x, me.y, me.z, me.w, psum, lane, nb);
-		else if (XDP_INL_ADAPT > 1 && mx <= 128 * U)
-			stream_groups_inl<8, U, NT>(a, me.x, me.y, me.z, me.w, psum, lane, nb);
-		else
-			stream_groups_inl<G, U, NT>(a, me.x, me.y, me.z, me.w, psum, lane, nb);
-		__builtin_amdgcn_wave_barrier();
-		/* lane f completes frame f (its group's sum; exact as below) */
-		t = act ? psum[lane] : 0u;
-	} else {
-		/* frame f's 16 partials, zero but for its group's lanes.  The
-		 * four 16-byte slots of a lane rotated by lane / 4: lanes l and
-		 * l + 4 are 256 bytes apart, one bank row, so an unrotated slot
-		 * j would put them on the same banks */
+	/* frame f's 16 partials, zero but for its group's lanes.  The four
+	 * 16-byte slots of a lane rotated by lane / 4: lanes l and l + 4 are
+	 * 256 bytes apart, one bank row, so an unrotated slot j would put them
+	 * on the same banks */
 #pragma unroll
-		for (int j = 0; j < 4; j++)
-			part4[4 * lane + ((j + (lane >> 2)) & 3)] = make_uint4(0, 0, 0, 0);
-		__builtin_amdgcn_wave_barrier();
-		if (kTailShort && mx <= 64)
-			stream_short<NT>(a, meta, part, lane, nb);
-		else if (kTailAdapt && mx <= 64 * U)
-			stream_groups<4, U, NT>(a, meta, part, lane, nb);
-		else if (kTailAdapt && mx <= 128 * U)
-			stream_groups<8, U, NT>(a, meta, part, lane, nb);
-		else
-			stream_groups<G, U, NT>(a, meta, part, lane, nb);
-		__builtin_amdgcn_wave_barrier();
+	for (int j = 0; j < 4; j++)
+		part4[4 * lane + ((j + (lane >> 2)) & 3)] = make_uint4(0, 0, 0, 0);
+	__builtin_amdgcn_wave_barrier();
+	if (kTailShort && mx <= 64)
+		stream_short<NT>(a, meta, part, lane, nb);
+	else if (kTailAdapt && mx <= 64 * U)
+		stream_groups<4, U, NT>(a, meta, part, lane, nb);
+	else if (kTailAdapt && mx <= 128 * U)
+		stream_groups<8, U, NT>(a, meta, part, lane, nb);
+	else
+		stream_groups<G, U, NT>(a, meta, part, lane, nb);
+	__builtin_amdgcn_wave_barrier();
 
-		/* lane f completes frame f: exact, a range is < 64 KiB + 64 B
-		 * so the raw sum of 16-bit halves fits 32 bits */
+	/* lane f completes frame f: exact, a range is < 64 KiB + 64 B so
+	 * the raw sum of 16-bit halves fits 32 bits */
 #pragma unroll
-		for (int j = 0; j < 4; j++) {
-			const uint4 x = part4[4 * lane + ((j + (lane >> 2)) & 3)];
-			t += x.x + x.y + x.z + x.w;
-		}
+	for (int j = 0; j < 4; j++) {
+		const uint4 x = part4[4 * lane + ((j + (lane >> 2)) & 3)];
+		t += x.x + x.y + x.z + x.w;
 	}
 	uint32_t c4, sum4;
 	bool absent, l3_bad;
@@ -1975,9 +1879,7 @@ struct TileOut {
 	uint32_t li;       /* this lane's frame in the tile                 */
 	uint32_t fl;       /* bit 0: verdict store, bit 1: record and tuple,
 			    * bit 2: IPv6 (network_tuple: the bulk
-			    * pass's; 16-byte tuple: stored here), bit 3:
-			    * quick frame, bit 4: a bulk frame for the
-			    * wave's inline queue (INLB)               */
+			    * pass's; 16-byte tuple: stored here)      */
 	uint32_t verdict;
 	uint32_t sa, da, ports, proto, vid;
 	uint4 rec;
@@ -2069,7 +1971,7 @@ __device__ __forceinline__ void defer_direct(bool want, uint64_t i, uint32_t *gl
 		st_asm_sb32(uniform_ptr(gl), (base + rank) * 4u, (uint32_t)i);
 }
 
-template <bool LQ, bool ST = true, bool V6 = false, bool INLB = false>
+template <bool LQ, bool ST = true, bool V6 = false>
 __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[18],
 					  uint4 dv, uint64_t i, bool active,
 					  bool dma, int lane, FastWave &w,
@@ -2216,8 +2118,6 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 		qv = (arp | ndp) ? XDPGPU_PASS : XDPGPU_ABORTED;
 	}
 
-	const bool inlq = INLB && bulk &&
-			  !(v6 && (a.flags & XDPGPU_CFG_ICMP6_ECHO) && nh6 == 58 && nv == 0);
 	/* 3. defer the frames of other shapes to the exception list and
 	 * the long ones to the bulk list of this wave */
 	if constexpr (LQ) {
@@ -2226,11 +2126,7 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 	} else {
 		defer_direct(active && !fast && !bulk && !quick, i, w.xl, w.lcount, lane,
 			     a.xregion);
-		/* INLB: bulk frames go to the wave's own queue once their
-		 * tile's outputs are stored (xdp_rx_db_kernel, TileOut bit 4),
-		 * but for untagged ICMPv6 under the echo responder, whose
-		 * rewrite stays with the tail's bulk pass */
-		defer_direct(bulk && !inlq, i, w.bl, w.lcount + 1, lane, a.xregion);
+		defer_direct(bulk, i, w.bl, w.lcount + 1, lane, a.xregion);
 	}
 
 	/* 4. fast frames: flow key, hash, tuple, checksums, verdict */
@@ -2363,7 +2259,7 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 		to->t0 = uniform_u64(i);   /* all lanes active: lane 0 */
 		to->li = (uint32_t)(i - to->t0);
 		to->fl = (fast || quick ? 1u : 0u) | (out || quick ? 2u : 0u) | (v6 ? 4u : 0u) |
-			 (quick ? 8u : 0u) | (inlq ? 16u : 0u);
+			 (quick ? 8u : 0u);
 		to->verdict = quick ? qv : vdrop ? XDPGPU_DROP : XDPGPU_REDIRECT;
 		/* an IPv6 frame's 16-byte tuple: no addresses, its ports (none
 		 * for ICMPv6), ipv 10 (emit_tuple's layout); a quick frame's:
@@ -2459,12 +2355,6 @@ __device__ __forceinline__ void wave_stats_to_lds(const RxArgs &a,
 #define XDP_TAIL_U 4
 #endif
 constexpr int kTailG = XDP_TAIL_G, kTailU = XDP_TAIL_U;
-/* loads per lane and step of the inline bulk batches (registers: the tile
- * loop's state is live around them) */
-#ifndef XDP_INL_U
-#define XDP_INL_U 2
-#endif
-constexpr int kInlU = XDP_INL_U;
 __device__ __forceinline__ void rx_tail(const RxArgs &a, const FastWave &w,
 					uint64_t rb, uint32_t xc, uint32_t bc,
 					int wid, int nw, uint32_t *ctl, int lane,
@@ -2687,15 +2577,10 @@ constexpr int kCuBlock = kCuWaves * kWave;
 #ifndef XDP_WIN_AUX
 #define XDP_WIN_AUX 2
 #endif
-/* INLB: bulk frames finished inline (kernel comment below, "Inline bulk
- * batches"). */
-template <bool FRAGS, int DIAG = 0, bool V6 = false, bool INLB = false>
+template <bool FRAGS, int DIAG = 0, bool V6 = false>
 __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 {
 	__shared__ uint4 lds_all[kCuWaves * kDbWave];
-	/* INLB: per wave 64 words, the queue's staging area and the inline
-	 * batches' frame sums (never a DMA target) */
-	__shared__ uint32_t inl_all[INLB ? kCuWaves * kWave : 1];
 	/* the block's tile claims, list lengths (exception, bulk) and the
 	 * tail's batch claims (its two passes) */
 	__shared__ uint32_t ctl[8];
@@ -2793,54 +2678,6 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 	/* the previous step's outputs, stored after this step's wait (the
 	 * first step stores an empty TileOut: every lane out of range) */
 	TileOut pend = {};
-
-	/* Inline bulk batches (INLB): a bulk frame (its checksum range runs
-	 * past the window) joins the wave's queue, two registers of frame
-	 * indices (bq0: entries 0-63, bq1: 64-127), once its tile's outputs
-	 * (the provisional record and verdict) are stored; at 64 entries the
-	 * wave waits for its stores (vmcnt(0)) and finishes the 64 frames
-	 * there and then, bulk_batch with its sums in registers: the frames'
-	 * payload is read a few tiles after their windows, while the lines
-	 * the window DMA brought in are still in the L2 or the Infinity
-	 * Cache, not in the tail after the whole loop (IMIX: the window line
-	 * read twice from HBM, 1.29x the algorithmic bytes in round 3).  The
-	 * counted wait stays exact: the batch's memory ops are younger than
-	 * every DMA the next steps wait for, and only add to the count. */
-	uint32_t bq0 = 0, bq1 = 0, bq2 = 0, bqn = 0;
-	uint32_t *inl = inl_all + (INLB ? wid * kWave : 0);
-	/* one batch of the queue's first nbat frames (one call site in each
-	 * loop: a copy inlined in each step spilled 576 bytes a lane) */
-	auto inl_run = [&](uint32_t nbat) {
-		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-		bulk_batch<kInlU, true, false, kTailG, true>(a, nullptr, nullptr, lane, nullptr,
-							       nbat, w.cnt, w.my_bytes, bq0, inl);
-		bq0 = bq1;
-		bq1 = bq2;
-		bq2 = 0;
-		bqn -= nbat;
-	};
-	/* the bulk frames of a stored TileOut into the queue (lane order,
-	 * entries 0..191 in bq0..bq2: two tiles' frames past a batch) */
-	auto inl_push = [&](uint64_t t0, bool want) {
-		const uint64_t dm = __ballot(want);
-		if (!dm)
-			return;
-		const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
-			(uint32_t)(dm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0));
-		const uint32_t cnt = (uint32_t)__popcll(dm);
-		if (want)
-			inl[rank] = (uint32_t)(t0 + lane);
-		__builtin_amdgcn_wave_barrier();
-		const uint32_t l = (uint32_t)lane;
-		const uint32_t r0 = l - bqn, r1 = l + kWave - bqn, r2 = l + 2 * kWave - bqn;
-		const uint32_t v0 = inl[r0 < cnt ? r0 : 0], v1 = inl[r1 < cnt ? r1 : 0],
-			       v2 = inl[r2 < cnt ? r2 : 0];
-		bq0 = (l >= bqn && r0 < cnt) ? v0 : bq0;
-		bq1 = (l + kWave >= bqn && r1 < cnt) ? v1 : bq1;
-		bq2 = r2 < cnt ? v2 : bq2;
-		__builtin_amdgcn_wave_barrier();
-		bqn += cnt;
-	};
 	/* step on tile t, whose descriptor dv travels in registers: the
 	 * window DMA of tile tw (2 steps ahead, its descriptor from the slot:
 	 * returned), the descriptor DMA of tile td (4 ahead), the claim of
@@ -2860,9 +2697,6 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 		uint32_t F[18];
 		uint4 dn;
 		read_tile_db<kWaitN>(win, dsl, lane, F, dn);
-		/* the previous tile's bulk frames: queued once stored below */
-		const uint64_t pt0 = pend.t0;
-		const bool pbulk = INLB && (pend.fl & 16u);
 		if constexpr (DIAG != 1 && DIAG != 2)
 			store_tile(a, pend);
 		issue_win(dn, tw < ntiles, win);
@@ -2888,11 +2722,8 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 			__builtin_amdgcn_raw_buffer_store_b128((v4u_t){x, 0, x, 0}, rt,
 							       active ? 16 * li : off, 0, 2);
 		} else {
-			fast_tile<false, DIAG != 2, V6, INLB>(a, F, dv, i, active, dma, lane, w,
-							      &pend);
+			fast_tile<false, DIAG != 2, V6>(a, F, dv, i, active, dma, lane, w, &pend);
 		}
-		if constexpr (INLB)
-			inl_push(pt0, pbulk);
 		return dn;
 	};
 
@@ -2928,19 +2759,9 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 				break;
 			dc0 = n0;
 			dc1 = n1;
-			if constexpr (INLB) {
-				/* at most 191 queued after two steps */
-				while (bqn >= (uint32_t)kWave)
-					inl_run(kWave);
-			}
 		}
 		if constexpr (DIAG != 1 && DIAG != 2)
 			store_tile(a, pend);   /* the last tile's outputs */
-		if constexpr (INLB) {
-			inl_push(pend.t0, (pend.fl & 16u) != 0);
-			while (bqn >= (uint32_t)kWave)
-				inl_run(kWave);
-		}
 	}
 	/* Shared tiles: with its own tiles done, the wave claims the tiles of
 	 * its block's head (block b: head b mod heads) two at a time from the
@@ -3013,23 +2834,14 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 					lds_dma_landed();
 					read_tile_db<10>(win0, dsl0, lane, F, dn);
 					const uint64_t i0 = c0 * kWave + lane;
-					fast_tile<false, true, V6, INLB>(a, F, d0, i0, i0 < nfr, dma, lane, w,
-									 &pend);
+					fast_tile<false, true, V6>(a, F, d0, i0, i0 < nfr, dma, lane, w, &pend);
 					store_tile(a, pend);
-					if constexpr (INLB)
-						inl_push(pend.t0, (pend.fl & 16u) != 0);   /* < 128 */
 					if (c1 >= ntiles)
 						break;
 					read_tile_db<10>(win1, dsl1, lane, F, dn);
 					const uint64_t i1 = c1 * kWave + lane;
-					fast_tile<false, true, V6, INLB>(a, F, d1, i1, i1 < nfr, dma, lane, w,
-									 &pend);
+					fast_tile<false, true, V6>(a, F, d1, i1, i1 < nfr, dma, lane, w, &pend);
 					store_tile(a, pend);
-					if constexpr (INLB) {
-						inl_push(pend.t0, (pend.fl & 16u) != 0);   /* < 192 */
-						while (bqn >= (uint32_t)kWave)
-							inl_run(kWave);
-					}
 					c0 = first_of(vn);
 					if (c0 >= ntiles)
 						break;
@@ -3037,11 +2849,6 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 			}
 			lds_dma_landed();   /* a claim left outstanding at a break */
 		}
-	}
-	/* the queue's rest (fewer than 64 frames) */
-	if constexpr (INLB) {
-		while (bqn)
-			inl_run(bqn < (uint32_t)kWave ? bqn : (uint32_t)kWave);
 	}
 	STAMP(wgid, lane, 1);
 
@@ -3207,10 +3014,6 @@ static hipError_t launch_db(RxArgs a, uint32_t max_blocks, hipStream_t stream,
 	const dim3 grid((uint32_t)blocks), blk(kCuBlock);
 	if (a.frags)
 		hipLaunchKernelGGL((xdp_rx_db_kernel<true>), grid, blk, 0, stream, a);
-	else if (a.inlb && a.v6)
-		hipLaunchKernelGGL((xdp_rx_db_kernel<false, 0, true, true>), grid, blk, 0, stream, a);
-	else if (a.inlb)
-		hipLaunchKernelGGL((xdp_rx_db_kernel<false, 0, false, true>), grid, blk, 0, stream, a);
 	else if (diag == 1)
 		hipLaunchKernelGGL((xdp_rx_db_kernel<false, 1>), grid, blk, 0, stream, a);
 	else if (diag == 2)
@@ -3264,13 +3067,6 @@ hipError_t launch_rx(const RxArgs &a, uint32_t max_blocks, hipStream_t stream, u
 	 * partner head (the default goes on with the head in the other half
 	 * of the chip) */
 	b.partner = (tune >> 28) & 1 ? 1 : 2;
-	/* bulk frames finished inline (xdp_rx_db_kernel INLB) for batches
-	 * whose UMEM averages 128 bytes or more per frame (IMIX, 1500 B, the
-	 * echo leg's 128-byte frames; config 2's 64-byte frames have no bulk
-	 * frames); bit 22 forces it on, bit 23 off */
-	const bool big = a.n && a.usize / a.n >= 128;
-	b.inlb = a.res && !a.frags && !b.diag && !((tune >> 23) & 1) &&
-		 (big || ((tune >> 22) & 1));
 	return launch_db(b, max_blocks, stream, ev);
 }
 

@@ -149,9 +149,6 @@ struct RxArgs {
 				    * (diagnostic kernel variants)          */
 	uint32_t v6;               /* set by the launcher: the fast shape
 				    * includes untagged IPv6/UDP           */
-	uint32_t inlb;             /* set by the launcher: bulk frames
-				    * finished inline in the tile loop
-				    * (xdp_rx_db_kernel INLB)              */
 	uint32_t partner;          /* set by the launcher: 2 a wave claims
 				    * shared tiles of its own head, then of
 				    * the partner head h ^ 4 (default); 1

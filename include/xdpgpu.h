@@ -215,7 +215,9 @@ void *xdpgpu_host_alloc(uint64_t size);
 void xdpgpu_host_free(void *p);
 
 /* Device-resident form: every pointer is device memory (d_umem is written
- * only for ICMPv6 echo rewrites).  stream is a hipStream_t (NULL: the
+ * only for ICMPv6 echo rewrites; a d_umem in host memory, pinned or not, is
+ * refused with -EINVAL: no kernel of the library dereferences host
+ * memory).  stream is a hipStream_t (NULL: the
  * context's stream).  Returns after the launch is enqueued, also with
  * XDPGPU_CFG_FRAGS (no host round trip).  d_umem must be readable up to
  * round_up(umem_size, 16) (the kernel loads 16-byte aligned chunks and
