@@ -1302,6 +1302,13 @@ constexpr bool kBulkVerdictTile = XDP_BULK_VERDICT_TILE != 0;
 #define XDP_QUICK 1
 #endif
 constexpr bool kQuick = XDP_QUICK != 0;
+/* a tile of fast and bulk frames only (two in three of config 2's) skips
+ * the quick classification after one ballot (build knob): config 2 0.3086 /
+ * 0.3097 vs 0.3191 / 0.3145 ms a step, IMIX, 1500 B and echo unchanged,
+ * alternating processes (profiles/r04_ab_quick_skip.txt) */
+#ifndef XDP_QUICK_SKIP
+#define XDP_QUICK_SKIP 1
+#endif
 /* tiles with no tagged frame skip the tag shift of the window words
  * (fast_tile; build knob): config 2 0.3185 / 0.3315 vs 0.3344 / 0.3406 ms
  * per step without, alternating processes (profiles/r04_ab_untagged.txt) */
@@ -1346,7 +1353,7 @@ constexpr bool kTailAdapt = XDP_TAIL_ADAPT != 0;
 /* Batches of ranges within 64 bytes streamed in one step (stream_short;
  * build knob, off: DESIGN.md §5.2) */
 #ifndef XDP_TAIL_SHORT
-#define XDP_TAIL_SHORT 0
+#define XDP_TAIL_SHORT 1
 #endif
 constexpr bool kTailShort = XDP_TAIL_SHORT != 0;
 /* The bulk pass's payload streaming, G lanes per frame (dynamic frame
@@ -2091,7 +2098,7 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 	 * Every other frame the fast shape does not take stays an exception. */
 	bool quick = false;
 	uint32_t qv = XDPGPU_ABORTED;
-	if constexpr (!LQ && kQuick) {
+	if (!LQ && kQuick && (!XDP_QUICK_SKIP || __ballot(active & !fast & !bulk))) {
 		const uint32_t et = r[3] & 0xffff;
 		const bool big = (!a.force_generic) & staged & (len >= 64);
 		const bool arp = big & (et == 0x0608u);
@@ -2391,9 +2398,9 @@ __device__ __forceinline__ void rx_tail(const RxArgs &a, const FastWave &w,
 		}
 		if (q < nxb + nbb) {
 			const uint32_t b = (q - nxb) * kWave;
-			bulk_batch<kTailU, true, false, kTailG>(a, meta, part4, lane, w.bl + b,
-								bc - b < (uint32_t)kWave ? bc - b : kWave,
-								cnt, my_bytes);
+			bulk_batch<kTailU, true, false, kTailG>(
+				a, meta, part4, lane, w.bl + b,
+				bc - b < (uint32_t)kWave ? bc - b : kWave, cnt, my_bytes);
 			STAMP_ADD(rb * nw + wid, lane, 5);
 			continue;
 		}
@@ -2415,9 +2422,9 @@ __device__ __forceinline__ void rx_tail(const RxArgs &a, const FastWave &w,
 		if (yq >= nyb)
 			break;
 		const uint32_t b = yq * kWave;
-		bulk_batch<kTailU, true, true, kTailG>(a, meta, part4, lane, yl + b,
-						      ycn - b < (uint32_t)kWave ? ycn - b : kWave,
-						      cnt, my_bytes);
+		bulk_batch<kTailU, true, true, kTailG>(
+			a, meta, part4, lane, yl + b, ycn - b < (uint32_t)kWave ? ycn - b : kWave,
+			cnt, my_bytes);
 		STAMP_ADD(rb * nw + wid, lane, 6);
 	}
 }
