@@ -254,8 +254,8 @@ def pmc_traffic(n: int, size: int):
 def kt_round(kt: dict) -> dict:
     """The launch's HIP-event times.  One RX launch is one kernel
     (xdp_rx_db_kernel): the library records its start/end pair, then two
-    empty pairs where the three-kernel variant (cfg.tune bit 15) times its
-    exception and bulk kernels.  `launch_ms` (first to last event) is what
+    empty pairs (the record's exception and bulk fields, kept for the
+    struct's layout).  `launch_ms` (first to last event) is what
     `roofline.achieved` divides by; it agrees with rocprofv3's average
     duration of the kernel, `kernel_event_ms` (the first pair alone) reads
     ~3 % lower."""

@@ -598,7 +598,7 @@ int xdpgpu_kernel_times(xdpgpu_ctx *ctx, xdpgpu_ktimes *out)
 		for (int j = 0; j < 3; j++)
 			HIP_TRY(ctx, hipEventElapsedTime(&t[j], e[j], e[j + 1]));
 		HIP_TRY(ctx, hipEventElapsedTime(&all, e[0], e[3]));
-		out->fast_ms += t[0];       /* launch order: fast, exception, bulk */
+		out->fast_ms += t[0];       /* the kernel; then two empty pairs */
 		out->exception_ms += t[1];
 		out->bulk_ms += t[2];
 		out->total_ms += all;

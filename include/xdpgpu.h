@@ -297,10 +297,13 @@ int xdpgpu_ceiling_dev(struct xdpgpu_ctx *ctx, const void *d_umem,
 		       void *d_tuples, void *stream);
 
 /* Diagnostic (XDPGPU_CFG_TIMING): RX launches recorded since the last call
- * and the summed durations of their three kernels (fast, exception, bulk)
- * from HIP events on the launch stream.  Waits for the recorded work;
- * resets the record.  At most XDPGPU_TIMING_MAX launches are kept between
- * calls (later ones are not recorded). */
+ * and their summed durations from HIP events on the launch stream.  An RX
+ * launch is one kernel (xdp_rx_db_kernel): fast_ms is its event pair;
+ * exception_ms and bulk_ms stay in the struct for its layout and read ~0
+ * (two empty event pairs after the kernel); total_ms spans all four
+ * events.  Waits for the recorded work; resets the record.  At most
+ * XDPGPU_TIMING_MAX launches are kept between calls (later ones are not
+ * recorded). */
 #define XDPGPU_TIMING_MAX 1024
 struct xdpgpu_ktimes {
 	uint64_t launches;
