@@ -1356,6 +1356,15 @@ constexpr bool kTailAdapt = XDP_TAIL_ADAPT != 0;
 #define XDP_TAIL_SHORT 1
 #endif
 constexpr bool kTailShort = XDP_TAIL_SHORT != 0;
+/* Ranges longer than this many bytes streamed from their 128-byte line
+ * (bulk_batch; build knob, 0 off): 2 M x 1500 B 0.632 / 0.634 vs 0.658 /
+ * 0.661 ms and 3.69 vs 3.89 GB of HBM traffic a launch (the line a step
+ * boundary split was fetched twice); IMIX 1.927 / 1.930 vs 1.937 / 1.934;
+ * 256 (IMIX's 570-byte frames too) slowed IMIX to 1.96 ms
+ * (profiles/r04_ab_line_align.txt) */
+#ifndef XDP_TAIL_LINE_AL
+#define XDP_TAIL_LINE_AL 640
+#endif
 /* The bulk pass's payload streaming, G lanes per frame (dynamic frame
  * assignment): every listed frame's partial sums into part (16 per frame,
  * zero-filled for G < 16).  meta: the batch's ranges. */
@@ -1520,7 +1529,11 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 		x64 = *reinterpret_cast<const uint4 *>(a.umem + eff + 64);
 	/* absolute range [lo, lim), streamed from its 16-byte aligned start */
 	const uint64_t lo = eff + (GEN ? (ye.z & 0xffff) : 64u);
-	const uint64_t lo_al = lo & ~15ull;
+	/* ranges longer than XDP_TAIL_LINE_AL bytes streamed from their 128-byte
+	 * line (the group's chunks then cover whole lines and no line is split
+	 * between two steps); shorter ones from their 16-byte chunk (0: always) */
+	const uint64_t lo_al = lo & (XDP_TAIL_LINE_AL && lim > lo && lim - lo > XDP_TAIL_LINE_AL
+					     ? ~127ull : ~15ull);
 	uint32_t t = 0;
 	meta[lane] = make_uint4((uint32_t)lo_al, (uint32_t)(lo_al >> 32),
 				(uint32_t)(lim > lo ? lim - lo_al : 0),

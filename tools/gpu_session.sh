@@ -102,7 +102,15 @@ for s in "$@"; do
 		step "prof_$arg" 400 rocprofv3 --kernel-trace --stats --output-format csv \
 			-d "$OUT/prof_$arg" -o run -- $(workload "$arg") ;;
 	pmc)
-		step "pmc_$arg" 900 env DEST="$OUT/pmc_$arg.json" OUT="$OUT/pmc_$arg" \
+		# the pool's frame count and size for the summary (0: mixed sizes)
+		case $arg in
+		1500) geo="FRAMES=2097152 SIZE=1500" ;;
+		imix*) geo="FRAMES=16777216 SIZE=0" ;;
+		nat64*) geo="FRAMES=16777216 SIZE=128" ;;
+		*) geo="FRAMES=16777216 SIZE=64" ;;
+		esac
+		# shellcheck disable=SC2086
+		step "pmc_$arg" 900 env $geo DEST="$OUT/pmc_$arg.json" OUT="$OUT/pmc_$arg" \
 			PMC_CMD="$(workload "$arg")" LABEL="$arg" bash tools/pmc_profile.sh ;;
 	ab)
 		for r in 1 2; do
