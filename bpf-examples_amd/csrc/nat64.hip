@@ -742,7 +742,9 @@ __device__ uint32_t handle_v4(const Row &R, uint32_t len, int l3, uint64_t eff,
 	v6[5] = (uint8_t)pl;
 	v6[6] = (uint8_t)proto;
 	v6[7] = (uint8_t)R.b(l3 + 8);
-	if (eff < 20)
+	/* the bytes in front the frame may grow into (cfg.headroom) */
+	const uint64_t room = a.cfg.headroom && a.cfg.headroom < eff ? a.cfg.headroom : eff;
+	if (room < 20)
 		return XDPGPU_TC_ACT_SHOT;        /* no headroom to grow */
 	const int l4 = l3 + 20;
 	P.co = -1;
@@ -758,7 +760,7 @@ __device__ uint32_t handle_v4(const Row &R, uint32_t len, int l3, uint64_t eff,
 			if (!inner_v4_to_v6(R, len, l4 + 8, R.be16(l3 + 2), a, T, h6i, ihl_i))
 				return XDPGPU_TC_ACT_SHOT;
 			grow = 40 - ihl_i;
-			if (eff < 20 + grow)
+			if (room < 20 + grow)
 				return XDPGPU_TC_ACT_SHOT;
 			/* the pseudo header's length is the new payload_len */
 			const uint32_t pl2 = (pl + grow) & 0xffff;
@@ -1178,7 +1180,8 @@ __device__ __forceinline__ void egress_tile(const Nat64Args &a, const Tables &T,
 		slow = true;
 	} else if (!is4) {
 		act = XDPGPU_TC_ACT_OK;
-	} else if (vihl != 0x45 || len < 64 || eff < 32) {
+	} else if (vihl != 0x45 || len < 64 || eff < 32 ||
+		   (a.cfg.headroom && a.cfg.headroom < 20)) {
 		slow = true;   /* options / other versions; short; no room */
 	} else if (!inpref) {
 		act = XDPGPU_TC_ACT_OK;

@@ -2519,7 +2519,10 @@ __device__ __forceinline__ void read_tile_db(const uint4 *win, const uint4 *dslo
  * (256 each) and two descriptor slots (64 each), 10 KiB; kCuWaves waves per
  * block, one block per CU. */
 constexpr int kDbWave = 2 * 256 + 2 * 64;
-constexpr int kCuWaves = 15;
+#ifndef XDP_CU_WAVES
+#define XDP_CU_WAVES 15
+#endif
+constexpr int kCuWaves = XDP_CU_WAVES;
 constexpr int kCuBlock = kCuWaves * kWave;
 
 /*

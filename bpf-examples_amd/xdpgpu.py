@@ -131,7 +131,7 @@ class Nat64Cfg(C.Structure):
                 ("v4_prefix", C.c_uint32), ("v4_mask", C.c_uint32),
                 ("allow_plen", C.c_uint32), ("allow_prefix", C.c_uint8 * 16),
                 ("direction", C.c_uint32), ("flags", C.c_uint32),
-                ("rsvd", C.c_uint32 * 2)]
+                ("headroom", C.c_uint32), ("rsvd", C.c_uint32)]
 
 
 class Nat64Dyn(C.Structure):

@@ -348,7 +348,11 @@ struct xdpgpu_nat64_cfg {
 	uint8_t  allow_prefix[16];
 	uint32_t direction;        /* XDPGPU_NAT64_*                         */
 	uint32_t flags;            /* XDPGPU_NAT64_F_*, 0: the reference     */
-	uint32_t rsvd[2];
+	uint32_t headroom;         /* bytes in front of each frame that are
+				    * its own (its chunk's headroom), which
+				    * egress may grow into; 0: up to the
+				    * UMEM's start (below)                   */
+	uint32_t rsvd;
 };
 
 /* Opt-in extension (not in the reference, whose rewrite_icmp /
@@ -364,8 +368,14 @@ struct xdpgpu_nat64_cfg {
  *     payload_len.
  *   egress: the embedded IPv4 header (any IHL, not a fragment; its source
  *     in v4_reversemap) becomes a 40-byte IPv6 header; the frame starts
- *     60 - IHL bytes earlier (40 for IHL 20: that much UMEM headroom) and
+ *     60 - IHL bytes earlier (40 for IHL 20: that much headroom) and
  *     the outer payload_len grows by 40 - IHL.
+ * Egress writes in front of the frame (20 bytes; 60 - IHL with this flag).
+ * With headroom 0 the only bound is the UMEM's start, as in the reference,
+ * where the kernel guarantees the skb's headroom; in a packed UMEM that
+ * overwrites the previous frame, so a caller with packed frames sets
+ * headroom to what each frame owns, and a frame that would grow further
+ * is TC_ACT_SHOT.
  * The ICMP checksum is updated incrementally for the swapped header (a
  * frame that arrived with a valid checksum leaves with one); the embedded
  * transport header and its checksum are left as they are (RFC 7915 allows
@@ -391,7 +401,8 @@ int xdpgpu_nat64_setup(struct xdpgpu_ctx *ctx,
  * the per-packet TC programs nat64_ingress / nat64_egress
  * (nat64_kern.c:875-902).  d_action[i] gets the action; d_out[i] the
  * translated frame: an IPv6->IPv4 frame starts 20 bytes later, an
- * IPv4->IPv6 frame 20 bytes earlier (it needs 20 bytes of UMEM headroom),
+ * IPv4->IPv6 frame 20 bytes earlier (it needs 20 bytes of headroom: cfg
+ * headroom, or of UMEM when that is 0),
  * both as a plain UMEM offset.  Other frames keep their descriptor.  The
  * L2 header moves with the frame; only headers and the L4 checksum (ICMP:
  * type, code and rest-of-header) are written. */

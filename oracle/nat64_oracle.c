@@ -812,7 +812,9 @@ static int handle_v4(uint8_t *umem, uint64_t eff, uint32_t len, uint32_t l3,
 	put_be16(h6 + 4, (uint16_t)(be16(p + l3 + 2) - 20));
 	h6[6] = proto;
 	h6[7] = p[l3 + 8];
-	if (eff < 20)
+	/* the bytes in front the frame may grow into (cfg->headroom) */
+	const uint64_t room = cfg->headroom && cfg->headroom < eff ? cfg->headroom : eff;
+	if (room < 20)
 		return XDPGPU_TC_ACT_SHOT;             /* no headroom to grow */
 	const uint32_t l4 = l3 + 20;
 	int inner = 0;
@@ -828,7 +830,7 @@ static int handle_v4(uint8_t *umem, uint64_t eff, uint32_t len, uint32_t l3,
 			if (inner_v4_to_v6(p, len, l4 + 8, be16(p + l3 + 2), cfg, T, h6i, &ihl_i))
 				return XDPGPU_TC_ACT_SHOT;
 			grow = 40 - ihl_i;
-			if (eff < 20 + grow)
+			if (room < 20 + grow)
 				return XDPGPU_TC_ACT_SHOT;     /* headroom */
 			/* the pseudo header's length is the new payload_len */
 			put_be16(h6 + 4, (uint16_t)(be16(h6 + 4) + grow));

@@ -295,6 +295,38 @@ def test_oracle_inner_headroom():
             assert act[0] == w, headroom
 
 
+def packed(frames, headroom):
+    """frames back to back, each behind `headroom` bytes of its own (a
+    packed UMEM: a frame's headroom follows the previous frame's end)"""
+    stride = max(len(f) for f in frames) + headroom
+    stride = (stride + 63) & ~63
+    return place(frames, headroom=headroom + 64, stride=stride)
+
+
+def test_oracle_inner_packed_headroom():
+    """cfg.headroom bounds egress growth by each frame's own headroom, not
+    the UMEM's start: in a packed pool a frame that would grow into the
+    previous frame is TC_ACT_SHOT and the previous frame is untouched"""
+    frames = [err4(3, 3, bytes(4), inner4()), err4(3, 3, bytes(4), inner4(options=bytes(4))),
+              v4(udp_seg(ROUTER4, HOST4, False), 17, dst=HOST4)] * 3
+    for hr, want in ((40, [REDIR] * 3), (36, [SHOT, REDIR, REDIR]), (24, [SHOT, SHOT, REDIR]),
+                     (16, [SHOT, SHOT, SHOT])):
+        umem, descs = packed(frames, hr)
+        cfg, smap = inner_cfg(EG)
+        cfg.headroom = hr
+        act, out, u = run_oracle(umem, descs, EG, cfg=cfg, smap=smap)
+        assert list(act) == want * 3, hr
+        # nothing written below each frame's own headroom
+        for k in range(len(descs)):
+            lo = int(descs[k]["addr"]) - hr
+            prev_end = int(descs[k - 1]["addr"]) + int(descs[k - 1]["len"]) if k else 0
+            assert np.array_equal(u[prev_end:lo], umem[prev_end:lo]), (hr, k)
+        # without the bound the same pool grows into the gap in front
+        cfg.headroom = 0
+        act0, _, _ = run_oracle(umem, descs, EG, cfg=cfg, smap=smap)
+        assert list(act0) == [REDIR] * 9
+
+
 def dyn_state(direction, smap=()):
     from test_nat64_dyn import T_OUT, ostate, pool_cfg
     cfg = pool_cfg(direction)
@@ -334,6 +366,21 @@ def test_gpu_inner_cases(direction, headroom, skew):
     assert (want[0] == REDIR).sum() >= 8
     got = gpu_nat64(umem, descs, direction, cfg, smap)
     assert_nat64_same(got, want, f"inner/{direction}/{headroom}/{skew}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hr", [40, 36, 24, 16])
+def test_gpu_inner_packed_headroom(hr):
+    """cfg.headroom on the GPU (fast and general kernels) against the
+    oracle: the frames packed, each behind hr bytes of its own"""
+    frames = [c[1] for c in egress_cases()] + [v4(udp_seg(ROUTER4, HOST4, False), 17,
+                                                  dst=HOST4)] * 8
+    umem, descs = packed(frames, hr)
+    cfg, smap = inner_cfg(EG)
+    cfg.headroom = hr
+    want = run_oracle(umem, descs, EG, cfg=cfg, smap=smap)
+    got = gpu_nat64(umem, descs, EG, cfg, smap)
+    assert_nat64_same(got, want, f"inner-packed/{hr}")
 
 
 @pytest.mark.gpu
