@@ -194,13 +194,17 @@ def bulk_frames(seed: int, n: int, long_every: int = 3, aligned: bool = True):
 
 
 @pytest.mark.parametrize("tune", TUNES)
-def test_bulk_lengths_vs_oracle(dev, tune):
-    """The bulk path (checksum ranges past the window) and its boundaries."""
-    umem, descs = bulk_frames(21, 3000)
+@pytest.mark.parametrize("aligned", [True, False])
+def test_bulk_lengths_vs_oracle(dev, tune, aligned):
+    """The bulk path (checksum ranges past the window) and its boundaries;
+    long ranges start at every 16-byte (aligned: fast-shape frames) or byte
+    (exception frames) offset in their first 128-byte line, which the bulk
+    pass streams from (XDP_TAIL_LINE_AL)."""
+    umem, descs = bulk_frames(21 if aligned else 22, 3000, aligned=aligned)
     for flags, iv, fmt in ((0x5, 0, 1), (0x4, 0x12345, 2)):
         ov, ores, otup, ost = oracle.process(umem.copy(), descs, flags, iv, fmt)
         v, res, tup, um, st = run_dev(umem, descs, flags, iv, fmt, 64, tune)
-        assert_same((v, res, tup, None), (ov, ores, otup, None), f"bulk/{flags:#x}")
+        assert_same((v, res, tup, None), (ov, ores, otup, None), f"bulk/{aligned}/{flags:#x}")
         oracle_stats_match(st, ost)
         if flags == 0x5:
             assert (ov == xdpgpu.REDIRECT).sum() > 2000 and (ov == xdpgpu.DROP).sum() > 100

@@ -10,6 +10,7 @@
  *   rx_mix    : 80 B read + 33 B written per 64-B frame, as the RX kernel
  *               (16 B descriptor + 64 B frame; 16 B + 16 B + 1 B stores)
  *   rx_mix_nt : the same with non-temporal loads and stores
+ *   syn       : the SYN proxy leg's in-place shape (argument "syn")
  *
  * Build: hipcc --offload-arch=gfx950 -O3 -o tools/hbm_probe tools/hbm_probe.hip
  */
@@ -497,6 +498,66 @@ __global__ __launch_bounds__(256) void k_egress(uint8_t *p, size_t nframes, uint
 	}
 }
 
+/* the SYN proxy leg's shape (8 M frames at a 128-byte stride): per frame
+ * its first 96 bytes read and 80 written back in place (a 74-byte SYN-ACK
+ * as whole 16-byte chunks), and with DESC the 16-byte descriptor read, the
+ * 16-byte output descriptor and the verdict byte written */
+template <bool DESC>
+__global__ __launch_bounds__(256) void k_syn(uint4 *p, const uint4 *desc, uint4 *odesc,
+					     uint8_t *verdict, size_t nframes)
+{
+	const size_t n = nframes * 6;
+	for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+		const size_t f = i / 6;
+		const uint32_t c = i % 6;
+		uint4 *q = p + f * 8 + c;
+		uint4 v = *q;
+		if (c < 5) {
+			v.x += 1;
+			*q = v;
+		}
+		if (DESC && c == 0) {
+			uint4 d = desc[f];
+			d.z = 74;
+			odesc[f] = d;
+			verdict[f] = (uint8_t)(v.y | 3);
+		}
+	}
+}
+
+static int syn_main()
+{
+	const size_t frames = 8ull << 20;
+	uint4 *p, *d, *od;
+	uint8_t *vd;
+	CK(hipMalloc(&p, frames * 128));
+	CK(hipMalloc(&d, frames * 16));
+	CK(hipMalloc(&od, frames * 16));
+	CK(hipMalloc(&vd, frames));
+	CK(hipMemset(p, 1, frames * 128));
+	CK(hipMemset(d, 2, frames * 16));
+	hipEvent_t e0, e1;
+	CK(hipEventCreate(&e0));
+	CK(hipEventCreate(&e1));
+	for (int rep = 0; rep < 2; rep++)
+		for (int desc = 0; desc < 2; desc++)
+			for (int grid : {2048, 8192}) {
+				auto k = desc ? k_syn<true> : k_syn<false>;
+				for (int w = 0; w < 2; w++)
+					hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, 0, p, d, od, vd, frames);
+				CK(hipEventRecord(e0, 0));
+				for (int r = 0; r < 10; r++)
+					hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, 0, p, d, od, vd, frames);
+				CK(hipEventRecord(e1, 0));
+				CK(hipEventSynchronize(e1));
+				float ms;
+				CK(hipEventElapsedTime(&ms, e0, e1));
+				printf("syn %s grid %5d  %.4f ms / 8 M frames\n",
+				       desc ? "frame+desc+out" : "frame rw96/80", grid, ms / 10);
+			}
+	return 0;
+}
+
 static int stride_main()
 {
 	const size_t frames = 16ull << 20;
@@ -567,6 +628,8 @@ int main(int argc, char **argv)
 		return bulk_main();
 	if (argc > 1 && !strcmp(argv[1], "stride"))
 		return stride_main();
+	if (argc > 1 && !strcmp(argv[1], "syn"))
+		return syn_main();
 	const bool pair_only = argc > 1 && !strcmp(argv[1], "pair");
 	const size_t frames = 16ull << 20;
 	C.frames = frames;
