@@ -354,20 +354,83 @@ int oracle_nat64_state_read(const struct oracle_nat64_state *st,
 	return 0;
 }
 
-/* the tables one call sees: the static map, or the dynamic state */
+/* the tables one call sees: the static map, or the dynamic state; for a
+ * static map, open-addressed indices by v6 and by v4 (entry + 1, 0 empty)
+ * built per call, each holding a key's first entry as find_v6 / find_v4
+ * return it (a lookup tool of the test infrastructure: the map's semantics
+ * are the linear search's) */
 struct tabs {
 	const struct xdpgpu_nat64_map *map;
 	uint32_t nmap;
 	struct oracle_nat64_state *st;
 	uint64_t now;
+	uint32_t *ix6, *ix4, mask;
 };
+
+static uint32_t hash_bytes(const uint8_t *p, uint32_t n)
+{
+	uint32_t h = 2166136261u;                 /* FNV-1a */
+	for (uint32_t i = 0; i < n; i++)
+		h = (h ^ p[i]) * 16777619u;
+	return h;
+}
+
+static void tabs_index(struct tabs *T)
+{
+	uint32_t cap = 64;
+	while (cap < 2 * T->nmap)
+		cap <<= 1;
+	T->ix6 = calloc(cap, sizeof(uint32_t));
+	T->ix4 = calloc(cap, sizeof(uint32_t));
+	if (!T->ix6 || !T->ix4) {
+		free(T->ix6);
+		free(T->ix4);
+		T->ix6 = T->ix4 = NULL;
+		return;
+	}
+	T->mask = cap - 1;
+	for (uint32_t k = 0; k < T->nmap; k++) {
+		const struct xdpgpu_nat64_map *m = &T->map[k];
+		uint32_t h = hash_bytes(m->v6, 16) & T->mask;
+		while (T->ix6[h] && memcmp(T->map[T->ix6[h] - 1].v6, m->v6, 16))
+			h = (h + 1) & T->mask;
+		if (!T->ix6[h])
+			T->ix6[h] = k + 1;
+		h = hash_bytes((const uint8_t *)&m->v4, 4) & T->mask;
+		while (T->ix4[h] && T->map[T->ix4[h] - 1].v4 != m->v4)
+			h = (h + 1) & T->mask;
+		if (!T->ix4[h])
+			T->ix4[h] = k + 1;
+	}
+}
+
+static const struct xdpgpu_nat64_map *tabs_find_v6(const struct tabs *T, const uint8_t *v6)
+{
+	if (!T->ix6)
+		return find_v6(T->map, T->nmap, v6);
+	for (uint32_t h = hash_bytes(v6, 16) & T->mask; T->ix6[h]; h = (h + 1) & T->mask)
+		if (!memcmp(T->map[T->ix6[h] - 1].v6, v6, 16))
+			return &T->map[T->ix6[h] - 1];
+	return NULL;
+}
+
+static const struct xdpgpu_nat64_map *tabs_find_v4(const struct tabs *T, uint32_t v4)
+{
+	if (!T->ix4)
+		return find_v4(T->map, T->nmap, v4);
+	for (uint32_t h = hash_bytes((const uint8_t *)&v4, 4) & T->mask; T->ix4[h];
+	     h = (h + 1) & T->mask)
+		if (T->map[T->ix4[h] - 1].v4 == v4)
+			return &T->map[T->ix4[h] - 1];
+	return NULL;
+}
 
 /* v6_state_map for nat64_handle_v6 (:809-828): 1 and the address, 0 no
  * entry (static tables: NO_STATE), -1 allocation failed */
 static int tab_v6(const struct tabs *T, const uint8_t *v6, uint32_t *v4)
 {
 	if (!T->st) {
-		const struct xdpgpu_nat64_map *m = find_v6(T->map, T->nmap, v6);
+		const struct xdpgpu_nat64_map *m = tabs_find_v6(T, v6);
 		if (!m)
 			return 0;
 		*v4 = m->v4;
@@ -389,7 +452,7 @@ static int tab_v6(const struct tabs *T, const uint8_t *v6, uint32_t *v4)
 static int tab_v4(const struct tabs *T, uint32_t v4, uint8_t v6[16])
 {
 	if (!T->st) {
-		const struct xdpgpu_nat64_map *m = find_v4(T->map, T->nmap, v4);
+		const struct xdpgpu_nat64_map *m = tabs_find_v4(T, v4);
 		if (!m)
 			return 0;
 		memcpy(v6, m->v6, 16);
@@ -911,8 +974,13 @@ int oracle_nat64(uint8_t *umem, uint64_t umem_size, const struct xdpgpu_desc *de
 		 const struct xdpgpu_nat64_map *map, uint32_t nmap,
 		 uint8_t *action, struct xdpgpu_desc *out)
 {
-	const struct tabs T = {map, nmap, NULL, 0};
-	return run_batch(umem, umem_size, descs, n, cfg, &T, action, out);
+	struct tabs T = {map, nmap, NULL, 0, NULL, NULL, 0};
+	if (nmap > 64)
+		tabs_index(&T);
+	const int rc = run_batch(umem, umem_size, descs, n, cfg, &T, action, out);
+	free(T.ix6);
+	free(T.ix4);
+	return rc;
 }
 
 int oracle_nat64_dyn(uint8_t *umem, uint64_t umem_size, const struct xdpgpu_desc *descs,
@@ -920,6 +988,6 @@ int oracle_nat64_dyn(uint8_t *umem, uint64_t umem_size, const struct xdpgpu_desc
 		     struct oracle_nat64_state *st, uint64_t now, uint8_t *action,
 		     struct xdpgpu_desc *out)
 {
-	const struct tabs T = {NULL, 0, st, now};
+	const struct tabs T = {NULL, 0, st, now, NULL, NULL, 0};
 	return run_batch(umem, umem_size, descs, n, cfg, &T, action, out);
 }

@@ -250,6 +250,45 @@ def test_full_size_config2(dev):
     oracle_stats_match(st, ost)
 
 
+def test_full_size_config3(dev):
+    """Config 3 at full size: 16 M IMIX frames (5.98 GB, 30 % IPv6, VLAN
+    tags, the 44-byte network_tuple), as the bench leg runs it.  Bit-exact
+    against the oracle for every frame, and the generator's verdicts."""
+    n = 16 << 20
+    umem, descs, expect = xdpgpu.pool_generate(n, xdpgpu.POOL_IMIX, 64, 0x5EED0003)
+    v, res, tup, _, st = run_dev(umem, descs, 0x5, 0, 2)
+    np.testing.assert_array_equal(v, expect)
+    ov, ores, otup, ost = oracle.process(umem, descs, 0x5, 0, 2)
+    assert_same((v, res, tup, None), (ov, ores, otup, None), "config3-16M")
+    oracle_stats_match(st, ost)
+
+
+def test_repeat_launches_identical(dev):
+    """The HIP path against itself: one context, the same device batch
+    launched back to back (the shared-tile counters alternate between their
+    two sets, the tiles go to whichever CU claims them first) and on a
+    second stream, outputs identical byte for byte every time."""
+    umem, descs, _ = xdpgpu.pool_generate(1 << 20, xdpgpu.POOL_IMIX, 64, 0x5EED0013)
+    ctx = xdpgpu.XdpGpu(0, 0x5, 0x1234, 2, 64)
+    d_umem, d_desc = to_dev(umem), to_dev(np.ascontiguousarray(descs, xdpgpu.DESC_DTYPE), 16)
+    n = len(descs)
+    outs = []
+    s2 = torch.cuda.Stream()
+    for k in range(6):
+        d_v = torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda:0")
+        d_res = torch.full((n * 16,), 0xEE, dtype=torch.uint8, device="cuda:0")
+        d_tup = torch.full((n * 44,), 0xEE, dtype=torch.uint8, device="cuda:0")
+        torch.cuda.synchronize()
+        stream = s2.cuda_stream if k >= 4 else None
+        ctx.process_dev(d_umem, umem.nbytes, d_desc, n, d_v, d_res, d_tup, stream)
+        ctx.sync(stream)
+        outs.append((d_v.cpu().numpy(), d_res.cpu().numpy(), d_tup.cpu().numpy()))
+    ctx.close()
+    for k, o in enumerate(outs[1:], 1):
+        for x, y, what in zip(outs[0], o, ("verdict", "record", "tuple")):
+            assert np.array_equal(x, y), f"launch {k}: {what} differs"
+
+
 def test_empty_batch(dev):
     umem, descs, _ = xdpgpu.pool_generate(4, xdpgpu.POOL_UDP4, 64, 1)
     v, res, tup, um, st = run_dev(umem, descs[:0], 0x5, 0, 1)

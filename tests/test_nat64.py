@@ -404,6 +404,8 @@ def test_gpu_prefix_lengths(plen):
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind,direction,n,kw", [
     (xdpgpu.POOL_NAT64, IN, 1 << 20, {}),
+    # config 4 at full size (the bench leg's pool): every frame
+    pytest.param(xdpgpu.POOL_NAT64, IN, 16 << 20, {}, id="config4-16M"),
     (xdpgpu.POOL_NAT64, IN, 100000, dict(headroom=4, stride=256)),
     (xdpgpu.POOL_NAT64_V4, EG, 1 << 20, {}),
     (xdpgpu.POOL_NAT64_V4, EG, 100000, dict(headroom=21, stride=192)),
