@@ -139,9 +139,7 @@ struct xdpgpu_cfg {
 	uint32_t tune;          /* kernel variant (diagnostic, 0 = default):
 				 * bit 8 the exception pass keeps its payload
 				 * sums, bit 9 every frame through the
-				 * exception pass, bit 14 host path without
-				 * the mapped UMEM (span copies, compact echo
-				 * records), bits 16-17 no-compute / no-store
+				 * exception pass, bits 16-17 no-compute / no-store
 				 * timing variants, bit 18 no IPv6 in the
 				 * fast shape, bit 21 no shared tiles, bit 28
 				 * no partner head; nat64: bits 12-13 no map
