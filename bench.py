@@ -505,7 +505,7 @@ def frags_run(dev, stream, n, steps, local, size=9000, chunk=4096):
     return out
 
 
-def echo_run(dev, stream, n, steps, local, size=128, ppm=200000, tune=0):
+def echo_run(dev, stream, n, steps, local, size=128, ppm=200000, tune=0, window=0):
     """The ICMPv6 echo responder (af_xdp_user.c:968-1040) as a throughput
     mode: n frames of which ppm / 1e6 are echo requests, rewritten in place
     into replies (TX).  The rewrite changes the UMEM, so every step
@@ -526,7 +526,7 @@ def echo_run(dev, stream, n, steps, local, size=128, ppm=200000, tune=0):
     d_tup = torch.empty(n * 16, dtype=torch.uint8, device=dev)
     ms = []
     with xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT | xdpgpu.CFG_ICMP6_ECHO, 0,
-                       xdpgpu.TUPLE_V4, 64, tune=tune) as g:
+                       xdpgpu.TUPLE_V4, window, tune=tune) as g:
         for k in range(steps + 2):
             with torch.cuda.stream(stream):
                 work.copy_(pristine, non_blocking=True)
@@ -560,7 +560,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--frames", type=int, default=16 << 20, help="frames per GPU")
     ap.add_argument("--size", type=int, default=64)
-    ap.add_argument("--window", type=int, default=64)
+    ap.add_argument("--window", type=int, default=0,
+                    help="header window of every RX context: 64, 128, or 0 (the library "
+                         "picks per batch: 128 when the UMEM holds >= 128 B a frame)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--legs", default="1500,imix,nat64,frags,echo,synproxy",
@@ -635,9 +637,9 @@ def main():
                 replicate=8)
         if "imix" in legs:
             # config 3: IMIX with the 44 B network_tuple (429.3 B/frame)
-            ctx3 = xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT, 0, xdpgpu.TUPLE_NET, 64)
+            ctx3 = xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT, 0, xdpgpu.TUPLE_NET, args.window)
             tctx3 = xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT | xdpgpu.CFG_TIMING, 0,
-                                  xdpgpu.TUPLE_NET, 64)
+                                  xdpgpu.TUPLE_NET, args.window)
             secondary["config3_imix"] = side_run(
                 ctx3, tctx3, dev, stream, args.imix_frames, xdpgpu.POOL_IMIX, 64, 0x5EED0003,
                 xdpgpu.TUPLE_NET, steps2,
@@ -653,7 +655,7 @@ def main():
             secondary["multibuffer_9000B"] = frags_run(dev, stream, 1 << 16, steps2, local)
         if "echo" in legs:
             secondary["icmp6_echo"] = echo_run(dev, stream, 8 << 20, steps2, local,
-                                               tune=args.tune)
+                                               tune=args.tune, window=args.window)
         if "synproxy" in legs:
             secondary["synproxy"] = synproxy_run(dev, stream, 8 << 20, steps2, local)
 
@@ -661,7 +663,7 @@ def main():
     if not args.no_e2e and rank == 0 and world == 1:
         # host path: pinned UMEM, H2D span + descs, kernel, D2H outputs
         n3 = min(n, 4 << 20)
-        h = xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT, 0, xdpgpu.TUPLE_V4, 64,
+        h = xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT, 0, xdpgpu.TUPLE_V4, args.window,
                           max_batch=1 << 20)
         h.register_umem(umem)
         B = 1 << 20
@@ -712,7 +714,8 @@ def main():
                                    "packed 64B-stride UMEM, 1% bad L3 / 1% bad L4 / "
                                    "0.5% malformed / 0.1% ARP / 0.1% NDP",
                        "frames_per_gpu": n, "frame_size": args.size,
-                       "header_window": args.window, "parallelism": f"shard{world}",
+                       "header_window": args.window or (128 if args.size >= 128 else 64),
+                       "parallelism": f"shard{world}",
                        **({"rehearsal": "ranks sharing GPUs, gloo"} if rehearse else {})},
             "gbps": round(gbps, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1),

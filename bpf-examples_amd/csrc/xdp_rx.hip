@@ -157,6 +157,18 @@ __device__ __forceinline__ uint4 chunk_keep(uint64_t p, uint64_t lo, uint64_t hi
 	return make_uint4(m[0], m[1], m[2], m[3]);
 }
 
+/* A 128-byte window's second half (RxArgs.win 128): staged for a frame
+ * longer than 64 bytes whose first byte starts a 128-byte line (its bytes
+ * [64, 128) are then the rest of that line, which the bulk pass would
+ * otherwise fetch again) and which the UMEM's 16-byte rounded size holds.
+ * The tile loop's DMA (issue_win) and the bulk pass (bulk_batch) decide it
+ * the same way. */
+__device__ __forceinline__ bool win_hi(const RxArgs &a, uint64_t eff, uint32_t len)
+{
+	return a.win == 128 && len > 64 && !(eff & 127) &&
+	       eff + 128 <= ((a.usize + 15) & ~15ull);
+}
+
 /* af_xdp_user.c:590-606 csum16_add / csum16_sub / csum_replace2 */
 __device__ __forceinline__ uint32_t c16_add(uint32_t csum, uint32_t addend)
 {
@@ -1467,7 +1479,7 @@ __device__ __forceinline__ void stream_short(const RxArgs &a, const uint4 *meta,
 	}
 }
 
-template <int U, bool NT, bool GEN, int G>
+template <int U, bool NT, bool GEN, int G, int WIN = 64>
 __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 					   uint4 *part4, int lane,
 					   const void *list, uint32_t nb,
@@ -1528,7 +1540,8 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 	if (act && late)
 		x64 = *reinterpret_cast<const uint4 *>(a.umem + eff + 64);
 	/* absolute range [lo, lim), streamed from its 16-byte aligned start */
-	const uint64_t lo = eff + (GEN ? (ye.z & 0xffff) : 64u);
+	const uint64_t lo = eff + (GEN ? (ye.z & 0xffff)
+				       : (WIN == 128 && !r6 && win_hi(a, eff, dv.z)) ? 128u : 64u);
 	/* ranges longer than XDP_TAIL_LINE_AL bytes streamed from their 128-byte
 	 * line (the group's chunks then cover whole lines and no line is split
 	 * between two steps); shorter ones from their 16-byte chunk (0: always) */
@@ -1991,18 +2004,25 @@ __device__ __forceinline__ void defer_direct(bool want, uint64_t i, uint32_t *gl
 		st_asm_sb32(uniform_ptr(gl), (base + rank) * 4u, (uint32_t)i);
 }
 
-template <bool LQ, bool ST = true, bool V6 = false>
-__device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[18],
+/* NW: window words a lane holds, 16 (64-byte windows) or 32 (128-byte
+ * windows, RxArgs.win: a frame's bytes [64, 128) are staged too when it
+ * is longer than 64 bytes and starts a 128-byte line, win_hi below) */
+template <bool LQ, bool ST = true, bool V6 = false, int NW = 16>
+__device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[NW + 2],
 					  uint4 dv, uint64_t i, bool active,
 					  bool dma, int lane, FastWave &w,
 					  TileOut *to = nullptr)
 {
+	static_assert(NW == 16 || NW == 32, "64- or 128-byte windows");
 	const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
 	const uint32_t len = dv.z;
 	const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
 	const bool staged = dma & active & (len >= 14) & ((uint64_t)len <= a.usize) &
 			    (eff <= a.usize - len) & !(eff & 15) &
 			    (eff + 64 <= ((a.usize + 15) & ~15ull));
+	/* the window's end: 128 where the second half was staged */
+	const bool hi = NW == 32 && win_hi(a, eff, len);
+	const uint32_t wend = hi ? 128u : 64u;
 
 	/* 2. fast-shape classification, branch free (bitwise &/| on
 	 * flags, selects).  r[j] = frame dword j + nv */
@@ -2025,6 +2045,13 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 #pragma unroll
 		for (int j = 3; j < 16; j++)
 			r[j] = (F[j] & m0) | (F[j + 1] & m1) | (F[j + 2] & m2);
+	}
+	if constexpr (NW == 32) {
+		/* a second half not staged: zero past byte 64, as the 64-byte
+		 * window's words past its end (the words from 16 on are summed
+		 * below, straight from F) */
+		r[14] = (hi || nv < 2) ? r[14] : 0u;
+		r[15] = (hi || nv < 1) ? r[15] : 0u;
 	}
 	const uint32_t l3 = 14 + 4 * nv, l4 = l3 + 20;
 	const uint32_t tot = bswap16(r[4] & 0xffff);
@@ -2049,7 +2076,7 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 	 * past the window: the bulk kernel adds the payload sum */
 	const bool shape = fast;
 	const uint32_t over = icmp ? 0u : (cl & 1);
-	fast = shape & (l4 + cl + over <= 64u);
+	fast = shape & (l4 + cl + over <= wend);
 	bool bulk = shape & !fast & (a.res != nullptr);
 
 	/* V6: IPv6 with no extension header behind 0..2 VLAN tags, in the
@@ -2161,10 +2188,21 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 	/* L4 sum over [34, end) of the shifted frame with the pseudo
 	 * header, check word excluded; udp_csum's odd-length over-read
 	 * byte included (lib_checksum.h:142-179).  For a bulk frame the
-	 * window part: frame bytes [l4, 64) (F[16], F[17] are zero). */
+	 * window part: frame bytes [l4, wend) (r is zero past it). */
 	const int32_t e = (int32_t)(34 + cl + over);
 	uint64_t s4 = (uint64_t)(r[8] & 0xffff0000u) +
 		      (icmp ? 0ull : (uint64_t)sa + da + ((uint64_t)(proto + cl) << 8));
+	if constexpr (NW == 32) {
+		/* the second half's words (shifted as r), where staged */
+		const uint32_t m2 = 0u - (uint32_t)v2;
+		const uint32_t m1 = (0u - (uint32_t)v1) & ~m2;
+		const uint32_t m0 = ~(m1 | m2);
+		const uint32_t mh = hi ? ~0u : 0u;
+#pragma unroll
+		for (int j = 16; j < NW; j++)
+			s4 += ((F[j] & m0) | (F[j + 1] & m1) | (F[j + 2] & m2)) & mh &
+			      first_bytes(e - 4 * j);
+	}
 #pragma unroll
 	for (int j = 9; j < 16; j++) {
 		uint32_t m = first_bytes(e - 4 * j);
@@ -2199,9 +2237,13 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 		 * the check word left out where it lies inside: ICMPv6 at
 		 * 56-57, UDP at 60-61 (TCP's, at 70-71, never does) */
 		const bool u6 = v6 & !i6 & !t6;
+		/* an IPv6 frame's bulk range starts at byte 64 whatever the
+		 * window: its words past 64 - 4 nv stay out (128-byte windows) */
+		const uint32_t r14 = (NW == 16 || nv < 2) ? r[14] : 0u;
+		const uint32_t r15 = (NW == 16 || nv < 1) ? r[15] : 0u;
 		const uint64_t s46 = p6 + (r[13] & 0xffff0000u) +
-				     (r[14] & first_bytes(e6 - 56) & (i6 ? 0xffff0000u : ~0u)) +
-				     (r[15] & first_bytes(e6 - 60) & (u6 ? 0xffff0000u : ~0u));
+				     (r14 & first_bytes(e6 - 56) & (i6 ? 0xffff0000u : ~0u)) +
+				     (r15 & first_bytes(e6 - 60) & (u6 ? 0xffff0000u : ~0u));
 		key[4] = v6 ? (i6 ? 0u : r[13] >> 16) : key[4];
 		key[9] = v6 ? (i6 ? 0u : r[14] & 0xffffu) : key[9];
 		key[10] = v6 ? (nh6 | (10u << 16)) : key[10];
@@ -2375,6 +2417,7 @@ __device__ __forceinline__ void wave_stats_to_lds(const RxArgs &a,
 #define XDP_TAIL_U 4
 #endif
 constexpr int kTailG = XDP_TAIL_G, kTailU = XDP_TAIL_U;
+template <int WIN>
 __device__ __forceinline__ void rx_tail(const RxArgs &a, const FastWave &w,
 					uint64_t rb, uint32_t xc, uint32_t bc,
 					int wid, int nw, uint32_t *ctl, int lane,
@@ -2411,7 +2454,7 @@ __device__ __forceinline__ void rx_tail(const RxArgs &a, const FastWave &w,
 		}
 		if (q < nxb + nbb) {
 			const uint32_t b = (q - nxb) * kWave;
-			bulk_batch<kTailU, true, false, kTailG>(
+			bulk_batch<kTailU, true, false, kTailG, WIN>(
 				a, meta, part4, lane, w.bl + b,
 				bc - b < (uint32_t)kWave ? bc - b : kWave, cnt, my_bytes);
 			STAMP_ADD(rb * nw + wid, lane, 5);
@@ -2515,6 +2558,61 @@ __device__ __forceinline__ void read_tile_db(const uint4 *win, const uint4 *dslo
 	dn = make_uint4(vd.x, vd.y, vd.z, vd.w);
 }
 
+/* The 128-byte window form (xdp_rx_db_kernel WIN 128): a lane's two
+ * halves out of the two buffers (the first 64 bytes in win0, bytes
+ * [64, 128) in win1, each in the tile layout above) and the descriptor of
+ * the tile two steps ahead, after the counted wait vmcnt(N). */
+template <int N>
+__device__ __forceinline__ void read_tile_w2(const uint4 *win0, const uint4 *win1,
+					     const uint4 *dslot, int lane, uint32_t (&F)[34],
+					     uint4 &dn)
+{
+	const int sw = (lane >> 2) & 3;
+	const lds_uint4_t *l0 = (const lds_uint4_t *)win0;
+	const lds_uint4_t *l1 = (const lds_uint4_t *)win1;
+	const lds_uint4_t *ld = (const lds_uint4_t *)dslot;
+	uint32_t ad[9];
+#pragma unroll
+	for (int c = 0; c < 4; c++) {
+		ad[c] = (uint32_t)(uintptr_t)(l0 + 4 * lane + (c ^ sw));
+		ad[4 + c] = (uint32_t)(uintptr_t)(l1 + 4 * lane + (c ^ sw));
+	}
+	ad[8] = (uint32_t)(uintptr_t)(ld + lane);
+	v4u_t v0, v1, v2, v3, v4, v5, v6, v7, vd;
+#define XDP_READ_W2(N)                                                          \
+	asm volatile("s_waitcnt vmcnt(" #N ")\n\t"                             \
+		     "ds_read_b128 %0, %9\n\t"                                 \
+		     "ds_read_b128 %1, %10\n\t"                                \
+		     "ds_read_b128 %2, %11\n\t"                                \
+		     "ds_read_b128 %3, %12\n\t"                                \
+		     "ds_read_b128 %4, %13\n\t"                                \
+		     "ds_read_b128 %5, %14\n\t"                                \
+		     "ds_read_b128 %6, %15\n\t"                                \
+		     "ds_read_b128 %7, %16\n\t"                                \
+		     "ds_read_b128 %8, %17\n\t"                                \
+		     "s_waitcnt lgkmcnt(0)"                                     \
+		     : "=&v"(v0), "=&v"(v1), "=&v"(v2), "=&v"(v3), "=&v"(v4),   \
+		       "=&v"(v5), "=&v"(v6), "=&v"(v7), "=&v"(vd)               \
+		     : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3]), "v"(ad[4]), \
+		       "v"(ad[5]), "v"(ad[6]), "v"(ad[7]), "v"(ad[8])           \
+		     : "memory")
+	if constexpr (N == 1)
+		XDP_READ_W2(1);
+	else
+		XDP_READ_W2(0);
+#undef XDP_READ_W2
+	const v4u_t vv[8] = {v0, v1, v2, v3, v4, v5, v6, v7};
+#pragma unroll
+	for (int k = 0; k < 8; k++) {
+		F[4 * k] = vv[k].x;
+		F[4 * k + 1] = vv[k].y;
+		F[4 * k + 2] = vv[k].z;
+		F[4 * k + 3] = vv[k].w;
+	}
+	F[32] = F[33] = 0;
+	dn = make_uint4(vd.x, vd.y, vd.z, vd.w);
+}
+
 /* Per-wave LDS of the double-buffered kernel, in uint4: two window buffers
  * (256 each) and two descriptor slots (64 each), 10 KiB; kCuWaves waves per
  * block, one block per CU. */
@@ -2600,9 +2698,14 @@ constexpr int kCuBlock = kCuWaves * kWave;
 #ifndef XDP_WIN_AUX
 #define XDP_WIN_AUX 2
 #endif
-template <bool FRAGS, int DIAG = 0, bool V6 = false>
+/* WIN 128 (RxArgs.win): 128-byte windows, the two buffers holding one
+ * tile's two halves (single-buffered: tile k+1's DMA is issued as tile k
+ * is read), so the LDS and the waves per CU stay as they are; not with
+ * FRAGS or DIAG. */
+template <bool FRAGS, int DIAG = 0, bool V6 = false, int WIN = 64>
 __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 {
+	static_assert(WIN == 64 || (WIN == 128 && !FRAGS && !DIAG), "128-byte windows: the RX default only");
 	__shared__ uint4 lds_all[kCuWaves * kDbWave];
 	/* the block's tile claims, list lengths (exception, bulk) and the
 	 * tail's batch claims (its two passes) */
@@ -2690,6 +2793,40 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 				(lds_void_t *)(buf + kWave * k), 16, 0, XDP_WIN_AUX);
 		}
 	};
+	/* WIN 128: a tile's first halves into win0 and, for the frames
+	 * win_hi takes, bytes [64, 128) into win1 (others: the UMEM's first
+	 * 64 bytes, unused) */
+	auto issue_win2 = [&](uint4 dv, bool live) {
+		const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
+		const uint32_t len = dv.z;
+		const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
+		const bool ok = live & dma & (len >= 14) & ((uint64_t)len <= a.usize) &
+				(eff <= a.usize - len) & !(eff & 15) &
+				(eff + 64 <= ((a.usize + 15) & ~15ull));
+		const uint64_t e = ok ? eff : 0ull;
+		const uint64_t e2 = ok && win_hi(a, eff, len) ? eff + 64 : 0ull;
+#pragma unroll
+		for (int k = 0; k < 4; k++) {
+			const int f = 16 * k + (lane >> 2);
+			const int c = (lane & 3) ^ ((f >> 2) & 3);
+			uint64_t ef =
+				((uint64_t)(uint32_t)__shfl((int)(uint32_t)(e >> 32), f, kWave) << 32) |
+				(uint32_t)__shfl((int)(uint32_t)e, f, kWave);
+			uint64_t eg =
+				((uint64_t)(uint32_t)__shfl((int)(uint32_t)(e2 >> 32), f, kWave) << 32) |
+				(uint32_t)__shfl((int)(uint32_t)e2, f, kWave);
+			if (DBG_BAD(ef + 16 * c + 16 > ((a.usize + 15) & ~15ull), 4, ef))
+				ef = 0;
+			if (DBG_BAD(eg + 16 * c + 16 > ((a.usize + 15) & ~15ull), 4, eg))
+				eg = 0;
+			__builtin_amdgcn_global_load_lds(
+				(const void *)(a.umem + ef + 16 * c),
+				(lds_void_t *)(win0 + kWave * k), 16, 0, XDP_WIN_AUX);
+			__builtin_amdgcn_global_load_lds(
+				(const void *)(a.umem + eg + 16 * c),
+				(lds_void_t *)(win1 + kWave * k), 16, 0, XDP_WIN_AUX);
+		}
+	};
 	/* DMA of a tile's 64 descriptors into a slot (lane l: descriptor l) */
 	auto issue_desc = [&](uint64_t tt, uint4 *slot) {
 		uint64_t di = desc_at(tt);
@@ -2750,11 +2887,55 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 		return dn;
 	};
 
+	/* WIN 128: step on tile t (descriptor dv), single-buffered: the
+	 * counted wait is for the windows the previous step issued (only its
+	 * descriptor DMA, and any deferral stores, are younger), then the
+	 * previous tile's stores, tile tw's windows (its descriptor dnext,
+	 * read a step earlier), the descriptor DMA of tile td (4 ahead into
+	 * this step's slot, read 2 steps ahead as now) and the claim */
+	auto step2 = [&](uint64_t t, uint4 *dsl, uint4 dv, uint4 dnext, uint64_t tw,
+			 uint64_t td, uint64_t &tn) -> uint4 {
+		const uint64_t i = t * kWave + lane;
+		const bool active = i < nfr;
+		uint32_t F[34];
+		uint4 dn;
+		read_tile_w2<1>(win0, win1, dsl, lane, F, dn);
+		store_tile(a, pend);
+		issue_win2(dnext, tw < ntiles);
+		issue_desc(td, dsl);
+		tn = tile_of(claim(1));
+		fast_tile<false, true, V6, 32>(a, F, dv, i, active, dma, lane, w, &pend);
+		return dn;
+	};
+
 	/* the wave's tiles T0 < T1 < ...: the first five claimed at once */
 	const uint64_t first = claim(5);
 	uint64_t q0 = tile_of(first), q1 = tile_of(first + 1), q2 = tile_of(first + 2),
 		 q3 = tile_of(first + 3), q4 = tile_of(first + 4), q5;
-	if (q0 < ntiles) {
+	if (WIN == 128 && q0 < ntiles) {
+		/* prologue: descriptors of T0 and T1 in registers; descriptor
+		 * DMA T2, windows T0, descriptor DMA T3 (one op younger than
+		 * T0's windows, as every later step has) */
+		const uint4 d0 = *reinterpret_cast<const uint4 *>(a.desc + desc_at(q0));
+		const uint4 d1 = *reinterpret_cast<const uint4 *>(a.desc + desc_at(q1));
+		issue_desc(q2, dsl0);
+		issue_win2(d0, true);
+		issue_desc(q3, dsl1);
+		uint4 c0 = d0, c1 = d1;
+		for (;;) {
+			const uint4 n0 = step2(q0, dsl0, c0, c1, q1, q4, q5);
+			q0 = q1; q1 = q2; q2 = q3; q3 = q4; q4 = q5;
+			if (q0 >= ntiles)
+				break;
+			const uint4 n1 = step2(q0, dsl1, c1, n0, q1, q4, q5);
+			q0 = q1; q1 = q2; q2 = q3; q3 = q4; q4 = q5;
+			if (q0 >= ntiles)
+				break;
+			c0 = n0;
+			c1 = n1;
+		}
+		store_tile(a, pend);   /* the last tile's outputs */
+	} else if (WIN == 64 && q0 < ntiles) {
 		/* prologue: descriptors of the first two tiles in registers;
 		 * then, in this order, descriptor DMA T2, window DMA T0,
 		 * descriptor DMA T3, window DMA T1: at least 5 ops younger than
@@ -2845,7 +3026,36 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 				 * flight, one wait, then the two tiles.  (Pipelined over
 				 * pairs, each buffer refilled as soon as read: 0.3361 vs
 				 * 0.3250 ms on config 2, one process.) */
-				for (;;) {
+				for (; WIN == 128;) {
+					/* one tile's two halves at a time: the second
+					 * tile's DMA issued as the first is read */
+					const uint64_t c1 = second_of(c0);
+					const uint4 d0 = *reinterpret_cast<const uint4 *>(a.desc + desc_at(c0));
+					const uint4 d1 = *reinterpret_cast<const uint4 *>(a.desc + desc_at(c1));
+					issue_win2(d0, true);
+					const uint32_t vn = claim2();
+					uint32_t F[34];
+					uint4 dn;
+					lds_dma_landed();
+					read_tile_w2<0>(win0, win1, dsl0, lane, F, dn);
+					issue_win2(d1, c1 < ntiles);
+					const uint64_t i0 = c0 * kWave + lane;
+					fast_tile<false, true, V6, 32>(a, F, d0, i0, i0 < nfr, dma, lane, w,
+								       &pend);
+					store_tile(a, pend);
+					if (c1 >= ntiles)
+						break;
+					lds_dma_landed();
+					read_tile_w2<0>(win0, win1, dsl0, lane, F, dn);
+					const uint64_t i1 = c1 * kWave + lane;
+					fast_tile<false, true, V6, 32>(a, F, d1, i1, i1 < nfr, dma, lane, w,
+								       &pend);
+					store_tile(a, pend);
+					c0 = first_of(vn);
+					if (c0 >= ntiles)
+						break;
+				}
+				for (; WIN == 64;) {
 					const uint64_t c1 = second_of(c0);
 					const uint4 d0 = *reinterpret_cast<const uint4 *>(a.desc + desc_at(c0));
 					const uint4 d1 = *reinterpret_cast<const uint4 *>(a.desc + desc_at(c1));
@@ -2880,7 +3090,7 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 	lds_dma_landed();
 	__syncthreads();
 	const uint32_t xc = ctl[1], bc = ctl[2];
-	rx_tail(a, w, rb, xc, bc, wid, kCuWaves, ctl, lane, reinterpret_cast<uint32_t *>(wl),
+	rx_tail<WIN>(a, w, rb, xc, bc, wid, kCuWaves, ctl, lane, reinterpret_cast<uint32_t *>(wl),
 		reinterpret_cast<uint64_t *>(wl + 272), wl, wl + kWave, w.cnt, w.my_bytes);
 
 	/* counters: this wave's own slot (kMaxRxBlocks..: per-wave slots) */
@@ -3032,11 +3242,18 @@ static hipError_t launch_db(RxArgs a, uint32_t max_blocks, hipStream_t stream,
 			a.xregion = (uint32_t)xr;
 		}
 	}
+	/* 128-byte windows: the default kernel only */
+	if (a.win != 128 || a.frags || diag)
+		a.win = 64;
 	if (ev)
 		(void)hipEventRecord(ev[0], stream);
 	const dim3 grid((uint32_t)blocks), blk(kCuBlock);
 	if (a.frags)
 		hipLaunchKernelGGL((xdp_rx_db_kernel<true>), grid, blk, 0, stream, a);
+	else if (a.win == 128 && a.v6)
+		hipLaunchKernelGGL((xdp_rx_db_kernel<false, 0, true, 128>), grid, blk, 0, stream, a);
+	else if (a.win == 128)
+		hipLaunchKernelGGL((xdp_rx_db_kernel<false, 0, false, 128>), grid, blk, 0, stream, a);
 	else if (diag == 1)
 		hipLaunchKernelGGL((xdp_rx_db_kernel<false, 1>), grid, blk, 0, stream, a);
 	else if (diag == 2)

@@ -274,7 +274,7 @@ int xdpgpu_init(const xdpgpu_cfg *cfg, xdpgpu_ctx **out)
 {
 	if (!cfg || !out)
 		return -EINVAL;
-	if (cfg->window != 0 && cfg->window != 64)
+	if (cfg->window != 0 && cfg->window != 64 && cfg->window != 128)
 		return -EINVAL;
 	if (cfg->tuple_fmt > XDPGPU_TUPLE_NET)
 		return -EINVAL;
@@ -288,8 +288,6 @@ int xdpgpu_init(const xdpgpu_cfg *cfg, xdpgpu_ctx **out)
 	if (!ctx)
 		return -ENOMEM;
 	ctx->cfg = *cfg;
-	if (!ctx->cfg.window)
-		ctx->cfg.window = 64;
 	if (!ctx->cfg.max_batch)
 		ctx->cfg.max_batch = kDefaultMaxBatch;
 	ctx->err[0] = 0;
@@ -551,6 +549,11 @@ static int enqueue_rx(xdpgpu_ctx *ctx, Slot &s, uint8_t *d_umem, uint64_t usize,
 	 * Config 2, one box, one process: none 0.3435 ms, 8 0.3284, 12
 	 * 0.3226, 14 0.3227, 16 0.331 (tools/gpu_ab_steal.sh) */
 	a.steal_16ths = (ctx->cfg.tune >> 21) & 1 ? 0u : 12u;
+	/* the header window: as configured, or (0) 128 bytes for a batch whose
+	 * UMEM holds at least 128 bytes a frame (frames longer than 64 bytes
+	 * then read their first line once), else 64 */
+	a.win = ctx->cfg.window ? ctx->cfg.window
+				: (usize >= 128ull * n ? 128u : 64u);
 
 	rc = scratch_enter(ctx, s, stream);
 	if (rc)

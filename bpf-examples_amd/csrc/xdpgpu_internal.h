@@ -163,6 +163,8 @@ struct RxArgs {
 	uint32_t steal_16ths;      /* shared tiles = tiles x steal_16ths / 16
 				    * (0: none)                            */
 	uint32_t steal_tiles;      /* set by the launcher                  */
+	uint32_t win;              /* header window: 64, or 128 (a second
+				    * half for long frames starting a line) */
 	uint64_t xcap;             /* entries of each deferral list        */
 };
 

@@ -134,8 +134,14 @@ struct xdpgpu_cfg {
 	uint32_t max_batch;     /* max descriptors per host-path call (0: 2^20) */
 	uint32_t jhash_initval; /* initval of jhash (CLI option, default 0)    */
 	uint32_t tuple_fmt;     /* XDPGPU_TUPLE_*                              */
-	uint32_t window;        /* header bytes staged per frame: 64 (0: 64;
-				 * any other value is -EINVAL) */
+	uint32_t window;        /* header bytes staged per frame: 64, or 128
+				 * (a frame longer than 64 bytes that starts
+				 * a 128-byte line has its whole first line
+				 * staged, so the payload pass does not read
+				 * it again); 0: per batch, 128 when the UMEM
+				 * holds at least 128 bytes a frame, else 64;
+				 * any other value is -EINVAL.  Outputs are
+				 * the same whatever the window. */
 	uint32_t tune;          /* kernel variant (diagnostic, 0 = default):
 				 * bit 8 the exception pass keeps its payload
 				 * sums, bit 9 every frame through the

@@ -32,6 +32,12 @@ def to_dev(a: np.ndarray, pad: int = 64):
 # exception pass keeping its payload sums (bit 8); no shared tiles (bit 21);
 # shared tiles without the partner head (bit 28)
 TUNES = [0, 512, 512 | 256, 1 << 21, 1 << 28]
+# (cfg.tune, cfg.window): every tune with 64-byte windows; the 128-byte
+# window kernel (a long frame starting a 128-byte line has its bytes
+# [64, 128) staged too) with the default, all-exception, no-shared-tile and
+# no-partner tunes
+VARIANTS = [(t, 64) for t in TUNES] + [(0, 128), (512, 128), (1 << 21, 128), (1 << 28, 128)]
+SHORT_VARIANTS = [(0, 64), (512, 64), (1 << 21, 64), (0, 128), (512, 128)]
 
 
 def run_dev(umem, descs, flags=0x5, initval=0, fmt=1, window=64, tune=0):
@@ -82,13 +88,13 @@ def oracle_stats_match(st, ost):
 
 
 # ---------------------------------------------------------------- golden
-@pytest.mark.parametrize("tune", TUNES)
+@pytest.mark.parametrize("tune,window", VARIANTS)
 @pytest.mark.parametrize("cfg", ["verify", "echo_net", "noverify"])
-def test_golden_fixtures_device(dev, golden, cfg, tune):
+def test_golden_fixtures_device(dev, golden, cfg, tune, window):
     fx, meta = golden
     flags, iv, fmt = meta["cfgs"][cfg]
     descs = fx["descs"].view(xdpgpu.DESC_DTYPE)
-    v, res, tup, um, st = run_dev(fx["umem"], descs, flags, iv, fmt, 64, tune)
+    v, res, tup, um, st = run_dev(fx["umem"], descs, flags, iv, fmt, window, tune)
     want = (fx[f"{cfg}_verdict"], fx[f"{cfg}_res"].view(xdpgpu.RESULT_DTYPE),
             fx[f"{cfg}_tup"], fx[f"{cfg}_umem_after"])
     assert_same((v, res, tup, um), want, f"golden/{cfg}")
@@ -124,14 +130,14 @@ POOLS = [
 ]
 
 
-@pytest.mark.parametrize("tune", TUNES)
+@pytest.mark.parametrize("tune,window", VARIANTS)
 @pytest.mark.parametrize("name,kind,size,seed,n,kw", POOLS, ids=[p[0] for p in POOLS])
-def test_pool_vs_oracle(dev, name, kind, size, seed, n, kw, tune):
+def test_pool_vs_oracle(dev, name, kind, size, seed, n, kw, tune, window):
     umem, descs, expect = xdpgpu.pool_generate(n, kind, size, seed, **kw)
     for flags, iv, fmt in ((0x5, 0, 1), (0x7, 0x9E3779B9, 2)):
         ou = umem.copy()
         ov, ores, otup, ost = oracle.process(ou, descs, flags, iv, fmt)
-        v, res, tup, um, st = run_dev(umem, descs, flags, iv, fmt, 64, tune)
+        v, res, tup, um, st = run_dev(umem, descs, flags, iv, fmt, window, tune)
         assert_same((v, res, tup, um), (ov, ores, otup, ou), f"{name}/{flags:#x}")
         oracle_stats_match(st, ost)
         if flags == 0x5:
@@ -193,9 +199,9 @@ def bulk_frames(seed: int, n: int, long_every: int = 3, aligned: bool = True):
     return umem, descs
 
 
-@pytest.mark.parametrize("tune", TUNES)
+@pytest.mark.parametrize("tune,window", VARIANTS)
 @pytest.mark.parametrize("aligned", [True, False])
-def test_bulk_lengths_vs_oracle(dev, tune, aligned):
+def test_bulk_lengths_vs_oracle(dev, tune, window, aligned):
     """The bulk path (checksum ranges past the window) and its boundaries;
     long ranges start at every 16-byte (aligned: fast-shape frames) or byte
     (exception frames) offset in their first 128-byte line, which the bulk
@@ -203,16 +209,16 @@ def test_bulk_lengths_vs_oracle(dev, tune, aligned):
     umem, descs = bulk_frames(21 if aligned else 22, 3000, aligned=aligned)
     for flags, iv, fmt in ((0x5, 0, 1), (0x4, 0x12345, 2)):
         ov, ores, otup, ost = oracle.process(umem.copy(), descs, flags, iv, fmt)
-        v, res, tup, um, st = run_dev(umem, descs, flags, iv, fmt, 64, tune)
+        v, res, tup, um, st = run_dev(umem, descs, flags, iv, fmt, window, tune)
         assert_same((v, res, tup, None), (ov, ores, otup, None), f"bulk/{aligned}/{flags:#x}")
         oracle_stats_match(st, ost)
         if flags == 0x5:
             assert (ov == xdpgpu.REDIRECT).sum() > 2000 and (ov == xdpgpu.DROP).sum() > 100
 
 
-@pytest.mark.parametrize("tune", [0, 512, 1 << 21])
+@pytest.mark.parametrize("tune,window", SHORT_VARIANTS)
 @pytest.mark.parametrize("aligned", [True, False])
-def test_short_bulk_vs_oracle(dev, tune, aligned):
+def test_short_bulk_vs_oracle(dev, tune, window, aligned):
     """Bulk batches whose ranges all end within 64 bytes of the window
     (stream_short) and batches just past that, fast-shape (aligned) and
     exception (unaligned) frames."""
@@ -220,7 +226,7 @@ def test_short_bulk_vs_oracle(dev, tune, aligned):
     for flags, iv, fmt in ((0x5, 0, 1), (0x4, 0x12345, 2), (0x7, 9, 0)):
         ou = umem.copy()
         ov, ores, otup, ost = oracle.process(ou, descs, flags, iv, fmt)
-        v, res, tup, um, st = run_dev(umem, descs, flags, iv, fmt, 64, tune)
+        v, res, tup, um, st = run_dev(umem, descs, flags, iv, fmt, window, tune)
         assert_same((v, res, tup, um), (ov, ores, otup, ou), f"short/{aligned}/{flags:#x}")
         oracle_stats_match(st, ost)
         if flags == 0x5:
@@ -256,7 +262,7 @@ def test_full_size_config3(dev):
     against the oracle for every frame, and the generator's verdicts."""
     n = 16 << 20
     umem, descs, expect = xdpgpu.pool_generate(n, xdpgpu.POOL_IMIX, 64, 0x5EED0003)
-    v, res, tup, _, st = run_dev(umem, descs, 0x5, 0, 2)
+    v, res, tup, _, st = run_dev(umem, descs, 0x5, 0, 2, 0)     # window: automatic (128)
     np.testing.assert_array_equal(v, expect)
     ov, ores, otup, ost = oracle.process(umem, descs, 0x5, 0, 2)
     assert_same((v, res, tup, None), (ov, ores, otup, None), "config3-16M")
@@ -499,8 +505,8 @@ def test_v6_late_frames_cover_aborted_tcp():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tune", [0, 512, 1 << 21])
-def test_v6_late_frames_vs_oracle(dev, tune):
+@pytest.mark.parametrize("tune,window", SHORT_VARIANTS)
+def test_v6_late_frames_vs_oracle(dev, tune, window):
     """Tagged IPv6 and IPv6/TCP through the network_tuple / no-tuple builds
     (late check words and data offsets in the bulk pass) against the
     oracle, with and without the echo responder."""
@@ -509,13 +515,14 @@ def test_v6_late_frames_vs_oracle(dev, tune):
                            (0x7, 0, 1), (0x3, 5, 0)):
         ou = umem.copy()
         ov, ores, otup, ost = oracle.process(ou, descs, flags, iv, fmt)
-        v, res, tup, um2, st = run_dev(umem, descs, flags | xdpgpu.CFG_STATS, iv, fmt, 64, tune)
+        v, res, tup, um2, st = run_dev(umem, descs, flags | xdpgpu.CFG_STATS, iv, fmt, window,
+                                       tune)
         assert_same((v, res, tup, um2), (ov, ores, otup, ou), f"late/{flags:#x}/fmt{fmt}")
         oracle_stats_match(st, ost)
 
 
-@pytest.mark.parametrize("tune", [0, 512, 1 << 21])
-def test_v6_build_icmp_vs_oracle(dev, golden, tune):
+@pytest.mark.parametrize("tune,window", SHORT_VARIANTS)
+def test_v6_build_icmp_vs_oracle(dev, golden, tune, window):
     """The IPv6 builds (network_tuple, no tuple, and any tuple with the echo
     responder): IPv4 ICMP and ICMPv6 other than NDP go through the fast
     shape and the bulk pass, which answers untagged echo requests; the
@@ -535,7 +542,7 @@ def test_v6_build_icmp_vs_oracle(dev, golden, tune):
                                (0x6, 3, 0)):
             ou = umem.copy()
             ov, ores, otup, ost = oracle.process(ou, descs, flags, iv, fmt)
-            v, res, tup, um2, st = run_dev(umem, descs, flags, iv, fmt, 64, tune)
+            v, res, tup, um2, st = run_dev(umem, descs, flags, iv, fmt, window, tune)
             assert_same((v, res, tup, um2), (ov, ores, otup, ou),
                         f"{name}/{flags:#x}/fmt{fmt}")
             oracle_stats_match(st, ost)

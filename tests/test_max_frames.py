@@ -77,13 +77,14 @@ def test_oracle_max_frames():
 @pytest.mark.gpu
 def test_gpu_max_frames_vs_oracle():
     pytest.importorskip("torch")
-    from test_gpu_parity import TUNES, assert_same, oracle_stats_match, run_dev
+    from test_gpu_parity import VARIANTS, assert_same, oracle_stats_match, run_dev
     umem, descs, _ = max_pool()
-    for tune in TUNES:
+    for tune, window in VARIANTS:
         for flags, iv, fmt in ((0x5, 0, 1), (0x7, 0x9E3779B9, 2), (0x4, 7, 1)):
             ou = umem.copy()
             ov, ores, otup, ost = oracle.process(ou, descs, flags, iv, fmt)
-            print(f"max frames: tune {tune:#x} flags {flags:#x}", flush=True)
-            v, res, tup, um, st = run_dev(umem, descs, flags, iv, fmt, 64, tune)
-            assert_same((v, res, tup, um), (ov, ores, otup, ou), f"max/{tune:#x}/{flags:#x}")
+            print(f"max frames: tune {tune:#x} window {window} flags {flags:#x}", flush=True)
+            v, res, tup, um, st = run_dev(umem, descs, flags, iv, fmt, window, tune)
+            assert_same((v, res, tup, um), (ov, ores, otup, ou),
+                        f"max/{tune:#x}/{window}/{flags:#x}")
             oracle_stats_match(st, ost)
