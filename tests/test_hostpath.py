@@ -45,13 +45,13 @@ def ring_batches(nframes: int, nbatch: int, B: int, seed: int):
     return out
 
 
-def run_ring(umem, descs, batches, flags, tune, fmt=xdpgpu.TUPLE_NET, pinned=True):
+def run_ring(umem, descs, batches, flags, tune, fmt=xdpgpu.TUPLE_NET, pinned=True, window=64):
     """Submit the batches alternately on the two slots, waiting for a slot
     only when it is needed again; returns outputs per batch and stats."""
     n_max = max(len(b) for b in batches)
     tb = xdpgpu.TUPLE_BYTES[fmt]
     outs = []
-    with xdpgpu.XdpGpu(0, flags, 0x9E3779B9, fmt, max_batch=n_max, tune=tune) as ctx:
+    with xdpgpu.XdpGpu(0, flags, 0x9E3779B9, fmt, window, max_batch=n_max, tune=tune) as ctx:
         ctx.register_umem(umem)
         bufs = []
         for slot in range(2):
@@ -113,13 +113,14 @@ def oracle_ring(umem, descs, batches, flags, fmt=xdpgpu.TUPLE_NET):
 
 @pytest.mark.parametrize("tune", [0], ids=["span_copy"])
 @pytest.mark.parametrize("pinned", [True, False], ids=["pinned", "pageable"])
-def test_ring_echo_two_slots(tune, pinned):
+@pytest.mark.parametrize("window", [64, 0], ids=["w64", "wauto"])
+def test_ring_echo_two_slots(tune, pinned, window):
     nframes = 16384
     umem, descs, _ = xdpgpu.pool_generate(nframes, xdpgpu.POOL_UDP4, 128, 31,
                                           ppm_echo6=300000)
     batches = ring_batches(nframes, 24, 2048, 5)
     host = umem.copy()
-    got, st = run_ring(host, descs, batches, ECHO, tune, pinned=pinned)
+    got, st = run_ring(host, descs, batches, ECHO, tune, pinned=pinned, window=window)
     ou = umem.copy()
     want, ost = oracle_ring(ou, descs, batches, ECHO)
     ntx = 0
@@ -305,7 +306,8 @@ def test_device_entry_points_reject_host_memory():
     np.testing.assert_array_equal(dv.cpu().numpy(), expect)
 
 
-def test_scattered_batch_runs():
+@pytest.mark.parametrize("window", [64, 0], ids=["w64", "wauto"])
+def test_scattered_batch_runs(window):
     """A batch scattered over a large UMEM (a recycled fill ring's order)
     is copied as at most 64 merged runs, never by reading the host UMEM
     from a kernel: every frame's outputs equal the oracle's, and frames
@@ -317,7 +319,7 @@ def test_scattered_batch_runs():
     batch = np.sort(rng.choice(nframes, 3000, replace=False))[::-1].copy()
     host = umem.copy()
     d = np.ascontiguousarray(descs[batch])
-    with xdpgpu.XdpGpu(0, ECHO, 0, xdpgpu.TUPLE_V4, max_batch=len(batch)) as ctx:
+    with xdpgpu.XdpGpu(0, ECHO, 0, xdpgpu.TUPLE_V4, window, max_batch=len(batch)) as ctx:
         ctx.register_umem(host)
         v, res, tup = ctx.process(d)
     ou = umem.copy()
