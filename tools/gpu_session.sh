@@ -62,6 +62,8 @@ workload() {
 	config2) echo "python3 tools/tune_rx.py --variants 64:0 --rounds 3" ;;
 	1500) echo "python3 tools/tune_rx.py --variants 64:0 --rounds 3 --frames 2097152 --size 1500" ;;
 	imix) echo "python3 tools/tune_rx.py --variants 64:0 --rounds 3 --frames 16777216 --kind 1 --seed 0x5EED0003 --fmt 2" ;;
+	imix128) echo "python3 tools/tune_rx.py --variants 128:0 --rounds 3 --frames 16777216 --kind 1 --seed 0x5EED0003 --fmt 2" ;;
+	1500_128) echo "python3 tools/tune_rx.py --variants 128:0 --rounds 3 --frames 2097152 --size 1500" ;;
 	imix_r2) echo "python3 tools/tune_rx.py --variants 64:0 --rounds 3 --frames 16777216 --kind 1 --seed 0x5EED0003 --fmt 2 --ppm-v6 125000" ;;
 	nat64) echo "python3 tools/nat64_probe.py --reps 5" ;;
 	nat64_egress) echo "python3 tools/nat64_probe.py --reps 5 --direction 1" ;;
