@@ -513,9 +513,13 @@ static int scratch_sync(xdpgpu_ctx *ctx, Slot &s)
 	return 0;
 }
 
+/* bytes a frame for the automatic window (cfg.window 0): the caller's
+ * UMEM over the batch (device path), or the batch's own mean frame length
+ * (host path, whose descriptors the library reads) */
 static int enqueue_rx(xdpgpu_ctx *ctx, Slot &s, uint8_t *d_umem, uint64_t usize,
 		      const xdpgpu_desc *d_desc, uint32_t n, uint8_t *d_verdict,
-		      xdpgpu_result *d_res, uint8_t *d_tup, hipStream_t stream)
+		      xdpgpu_result *d_res, uint8_t *d_tup, hipStream_t stream,
+		      uint64_t per_frame = 0)
 {
 	int rc = ensure_xlist(ctx, s, n);
 	if (rc)
@@ -549,11 +553,12 @@ static int enqueue_rx(xdpgpu_ctx *ctx, Slot &s, uint8_t *d_umem, uint64_t usize,
 	 * Config 2, one box, one process: none 0.3435 ms, 8 0.3284, 12
 	 * 0.3226, 14 0.3227, 16 0.331 (tools/gpu_ab_steal.sh) */
 	a.steal_16ths = (ctx->cfg.tune >> 21) & 1 ? 0u : 12u;
-	/* the header window: as configured, or (0) 128 bytes for a batch whose
-	 * UMEM holds at least 128 bytes a frame (frames longer than 64 bytes
-	 * then read their first line once), else 64 */
-	a.win = ctx->cfg.window ? ctx->cfg.window
-				: (usize >= 128ull * n ? 128u : 64u);
+	/* the header window: as configured, or (0) 128 bytes for a batch of
+	 * at least 128 bytes a frame (frames longer than 64 bytes then read
+	 * their first line once), else 64 */
+	if (!per_frame)
+		per_frame = n ? usize / n : 0;
+	a.win = ctx->cfg.window ? ctx->cfg.window : (per_frame >= 128 ? 128u : 64u);
 
 	rc = scratch_enter(ctx, s, stream);
 	if (rc)
@@ -1143,7 +1148,7 @@ int xdpgpu_submit(xdpgpu_ctx *ctx, uint32_t slot, const xdpgpu_desc *descs,
 				    hipMemcpyHostToDevice, s.stream));
 	uint8_t *d_tup = (tuples && ctx->cfg.tuple_fmt) ? s.d_tup : nullptr;
 	rc = enqueue_rx(ctx, s, s.d_mirror, ctx->umem_size, s.d_desc, n, s.d_verdict,
-			res ? s.d_res : nullptr, d_tup, s.stream);
+			res ? s.d_res : nullptr, d_tup, s.stream, used / n + 1);
 	if (rc)
 		return rc;
 	/* echo replies were written in the mirror: only the TX frames' first

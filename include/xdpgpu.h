@@ -138,8 +138,10 @@ struct xdpgpu_cfg {
 				 * (a frame longer than 64 bytes that starts
 				 * a 128-byte line has its whole first line
 				 * staged, so the payload pass does not read
-				 * it again); 0: per batch, 128 when the UMEM
-				 * holds at least 128 bytes a frame, else 64;
+				 * it again); 0: per batch, 128 when its frames
+				 * average at least 128 bytes (the host path:
+				 * their mean length; the device path: the
+				 * UMEM size over the frame count), else 64;
 				 * any other value is -EINVAL.  Outputs are
 				 * the same whatever the window. */
 	uint32_t tune;          /* kernel variant (diagnostic, 0 = default):
