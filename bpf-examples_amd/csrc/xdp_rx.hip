@@ -1500,6 +1500,13 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 		i = 0;
 	const uint4 dv = *reinterpret_cast<const uint4 *>(a.desc + i);
 	uint4 rv = *reinterpret_cast<const uint4 *>(a.res + i);
+	/* an IPv6 frame whose 128-byte window summed to byte 128 (fast_tile's
+	 * mark in the nvlan byte, cleared here) */
+	bool w6 = false;
+	if constexpr (!GEN && WIN == 128) {
+		w6 = (rv.z >> 31) != 0;
+		rv.z &= 0x7fffffffu;
+	}
 	const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
 	const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
 	const uint32_t cl = rv.w >> 16;
@@ -1535,13 +1542,16 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 	 * before l4 + 20 <= len) */
 	const uint32_t p6 = (rv.z >> 8) & 0xff;
 	const uint32_t chk6 = p6 == 6 ? 16u : p6 == 17 ? 6u : 2u;
-	const bool late = r6 && l4 + chk6 >= 64;
+	const bool late = r6 && !w6 && l4 + chk6 >= 64;
 	uint4 x64 = make_uint4(0, 0, 0, 0);
 	if (act && late)
 		x64 = *reinterpret_cast<const uint4 *>(a.umem + eff + 64);
 	/* absolute range [lo, lim), streamed from its 16-byte aligned start */
+	/* from byte 128 where the tile's 128-byte window summed to there: an
+	 * IPv4 frame with a staged second half (win_hi), an IPv6 frame
+	 * fast_tile marked */
 	const uint64_t lo = eff + (GEN ? (ye.z & 0xffff)
-				       : (WIN == 128 && !r6 && win_hi(a, eff, dv.z)) ? 128u : 64u);
+				       : (WIN == 128 && (r6 ? w6 : win_hi(a, eff, dv.z))) ? 128u : 64u);
 	/* ranges longer than XDP_TAIL_LINE_AL bytes streamed from their 128-byte
 	 * line (the group's chunks then cover whole lines and no line is split
 	 * between two steps); shorter ones from their 16-byte chunk (0: always) */
@@ -2007,11 +2017,21 @@ __device__ __forceinline__ void defer_direct(bool want, uint64_t i, uint32_t *gl
 /* NW: window words a lane holds, 16 (64-byte windows) or 32 (128-byte
  * windows, RxArgs.win: a frame's bytes [64, 128) are staged too when it
  * is longer than 64 bytes and starts a 128-byte line, win_hi below) */
+/* A 128-byte window's second half as read_tile_w2 reduces it (so that
+ * its 16 words need no registers past the read): the sum of the frame's
+ * words 16 + nv .. 31 (nv VLAN tags), and its words 16 + nv and 17 + nv
+ * (the tag-shifted words 16 and 17: IPv6/TCP's data offset and check
+ * word).  Its words 16 and 17 themselves are F[16], F[17]. */
+struct WinHi {
+	uint64_t s2;
+	uint32_t w16, w17;
+};
+
 template <bool LQ, bool ST = true, bool V6 = false, int NW = 16>
-__device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[NW + 2],
+__device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[18],
 					  uint4 dv, uint64_t i, bool active,
 					  bool dma, int lane, FastWave &w,
-					  TileOut *to = nullptr)
+					  TileOut *to = nullptr, const WinHi *wh = nullptr)
 {
 	static_assert(NW == 16 || NW == 32, "64- or 128-byte windows");
 	const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
@@ -2020,9 +2040,8 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[N
 	const bool staged = dma & active & (len >= 14) & ((uint64_t)len <= a.usize) &
 			    (eff <= a.usize - len) & !(eff & 15) &
 			    (eff + 64 <= ((a.usize + 15) & ~15ull));
-	/* the window's end: 128 where the second half was staged */
+	/* the second half was staged (128-byte windows) */
 	const bool hi = NW == 32 && win_hi(a, eff, len);
-	const uint32_t wend = hi ? 128u : 64u;
 
 	/* 2. fast-shape classification, branch free (bitwise &/| on
 	 * flags, selects).  r[j] = frame dword j + nv */
@@ -2045,13 +2064,6 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[N
 #pragma unroll
 		for (int j = 3; j < 16; j++)
 			r[j] = (F[j] & m0) | (F[j + 1] & m1) | (F[j + 2] & m2);
-	}
-	if constexpr (NW == 32) {
-		/* a second half not staged: zero past byte 64, as the 64-byte
-		 * window's words past its end (the words from 16 on are summed
-		 * below, straight from F) */
-		r[14] = (hi || nv < 2) ? r[14] : 0u;
-		r[15] = (hi || nv < 1) ? r[15] : 0u;
 	}
 	const uint32_t l3 = 14 + 4 * nv, l4 = l3 + 20;
 	const uint32_t tot = bswap16(r[4] & 0xffff);
@@ -2076,7 +2088,9 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[N
 	 * past the window: the bulk kernel adds the payload sum */
 	const bool shape = fast;
 	const uint32_t over = icmp ? 0u : (cl & 1);
-	fast = shape & (l4 + cl + over <= wend);
+	/* the window ends at 64, or at 128 where the second half was staged
+	 * (its words, masked by the range, come summed in wh) */
+	fast = shape & (l4 + cl + over <= (hi ? 128u : 64u));
 	bool bulk = shape & !fast & (a.res != nullptr);
 
 	/* V6: IPv6 with no extension header behind 0..2 VLAN tags, in the
@@ -2097,7 +2111,7 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[N
 	 * A check word at or past byte 64 (TCP; UDP behind a tag; ICMPv6
 	 * behind two) is "late": the bulk pass reads it, and the data offset,
 	 * from frame bytes [64, 80). */
-	bool v6 = false, i6 = false, t6 = false;
+	bool v6 = false, i6 = false, t6 = false, full6 = false, fast6 = false;
 	uint32_t ulen6 = 0, nh6 = 0;
 	if constexpr (V6) {
 		const uint32_t plen = bswap16(r[4] >> 16);
@@ -2114,11 +2128,27 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[N
 		     (a.res != nullptr);
 		i6 = i6 & v6;
 		t6 = t6 & v6;
-		/* always through the bulk pass, which also writes the
-		 * network_tuple (its addresses are not among the words a tile
-		 * keeps for its stores); a payload inside the window is an
-		 * empty range there */
-		bulk = bulk | v6;
+		if constexpr (NW == 32) {
+			/* 128-byte windows: a staged IPv6 frame (full6) is
+			 * summed to its range end or byte 128 here, its check
+			 * word and TCP's data offset taken from the window (a
+			 * data offset that fails parse_tcphdr is left to the bulk
+			 * pass's late path, which ABORTs it); a range that ends
+			 * inside the window is finished here, but for an untagged
+			 * ICMPv6 frame under the echo responder, which the bulk
+			 * pass answers */
+			const uint32_t thl6 = ((wh->w16 >> 20) & 0xf) * 4;
+			const uint32_t re6 = 54 + 4 * nv + ulen6;
+			full6 = hi & v6 &
+				(!t6 | ((thl6 >= 20) & (54 + 4 * nv + thl6 <= len) & (thl6 <= ulen6)));
+			const bool echo_el = i6 & (nv == 0) & ((a.flags & XDPGPU_CFG_ICMP6_ECHO) != 0);
+			fast6 = full6 & (re6 <= 128u) & !echo_el;
+		}
+		/* through the bulk pass (which also reads a late check word)
+		 * unless finished in a 128-byte window; a payload inside the
+		 * window is an empty range there */
+		bulk = bulk | (v6 & !fast6);
+		fast = fast | fast6;
 	}
 
 	/* Quick frames (kQuick, the per-CU kernel): verdicts parse_lane
@@ -2188,21 +2218,15 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[N
 	/* L4 sum over [34, end) of the shifted frame with the pseudo
 	 * header, check word excluded; udp_csum's odd-length over-read
 	 * byte included (lib_checksum.h:142-179).  For a bulk frame the
-	 * window part: frame bytes [l4, wend) (r is zero past it). */
-	const int32_t e = (int32_t)(34 + cl + over);
+	 * window part: frame bytes [l4, 64), or [l4, 128) with a staged
+	 * second half (hi: its words past r's come summed in wh->s2).  r holds
+	 * frame words up to 15 + nv; those past 15 count only for hi. */
+	const int32_t e0 = (int32_t)(34 + cl + over);
+	const int32_t e = (NW == 16 || hi) ? e0 : min(e0, (int32_t)(64 - 4 * nv));
 	uint64_t s4 = (uint64_t)(r[8] & 0xffff0000u) +
 		      (icmp ? 0ull : (uint64_t)sa + da + ((uint64_t)(proto + cl) << 8));
-	if constexpr (NW == 32) {
-		/* the second half's words (shifted as r), where staged */
-		const uint32_t m2 = 0u - (uint32_t)v2;
-		const uint32_t m1 = (0u - (uint32_t)v1) & ~m2;
-		const uint32_t m0 = ~(m1 | m2);
-		const uint32_t mh = hi ? ~0u : 0u;
-#pragma unroll
-		for (int j = 16; j < NW; j++)
-			s4 += ((F[j] & m0) | (F[j + 1] & m1) | (F[j + 2] & m2)) & mh &
-			      first_bytes(e - 4 * j);
-	}
+	if constexpr (NW == 32)
+		s4 += hi ? wh->s2 : 0ull;
 #pragma unroll
 	for (int j = 9; j < 16; j++) {
 		uint32_t m = first_bytes(e - 4 * j);
@@ -2237,13 +2261,17 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[N
 		 * the check word left out where it lies inside: ICMPv6 at
 		 * 56-57, UDP at 60-61 (TCP's, at 70-71, never does) */
 		const bool u6 = v6 & !i6 & !t6;
-		/* an IPv6 frame's bulk range starts at byte 64 whatever the
-		 * window: its words past 64 - 4 nv stay out (128-byte windows) */
-		const uint32_t r14 = (NW == 16 || nv < 2) ? r[14] : 0u;
-		const uint32_t r15 = (NW == 16 || nv < 1) ? r[15] : 0u;
-		const uint64_t s46 = p6 + (r[13] & 0xffff0000u) +
-				     (r14 & first_bytes(e6 - 56) & (i6 ? 0xffff0000u : ~0u)) +
-				     (r15 & first_bytes(e6 - 60) & (u6 ? 0xffff0000u : ~0u));
+		/* r's words past frame byte 64 count only for full6 (with
+		 * 64-byte windows they are zero) */
+		const uint32_t r14 = (NW == 16 || nv < 2 || full6) ? r[14] : 0u;
+		const uint32_t r15 = (NW == 16 || nv < 1 || full6) ? r[15] : 0u;
+		uint64_t s46 = p6 + (r[13] & 0xffff0000u) +
+			       (r14 & first_bytes(e6 - 56) & (i6 ? 0xffff0000u : ~0u)) +
+			       (r15 & first_bytes(e6 - 60) & (u6 ? 0xffff0000u : ~0u));
+		if constexpr (NW == 32)
+			/* the second half (TCP's check word left out by the
+			 * read) */
+			s46 += full6 ? wh->s2 : 0ull;
 		key[4] = v6 ? (i6 ? 0u : r[13] >> 16) : key[4];
 		key[9] = v6 ? (i6 ? 0u : r[14] & 0xffffu) : key[9];
 		key[10] = v6 ? (nh6 | (10u << 16)) : key[10];
@@ -2252,8 +2280,12 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[N
 		c3v = v6 ? 0u : c3v;
 		/* the check word where the window holds it (0: late, the bulk
 		 * pass loads it) */
-		c4v = v6 ? (i6 ? (nv <= 1 ? r[14] & 0xffffu : 0u)
-			       : u6 && nv == 0 ? r[15] & 0xffffu : 0u)
+		uint32_t c6 = 0;
+		if constexpr (NW == 32)
+			c6 = full6 ? (i6 ? r[14] & 0xffffu : u6 ? r[15] & 0xffffu : wh->w17 >> 16) : 0u;
+		c4v = v6 ? (full6 ? c6
+			    : i6 ? (nv <= 1 ? r[14] & 0xffffu : 0u)
+			    : u6 && nv == 0 ? r[15] & 0xffffu : 0u)
 			 : c4v;
 		clv = v6 ? ulen6 : clv;
 		l4v = v6 ? 54u + 4 * nv : l4v;
@@ -2279,6 +2311,10 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[N
 		(fast && absent ? XDPGPU_F_L4_ABSENT : 0u) |
 		(protov << 8) | (l3 << 16) | (nv << 24);
 	rec.w = (fast ? l4v : c4v) | (clv << 16);
+	/* an IPv6 bulk frame summed to byte 128 in its window (full6): the
+	 * nvlan byte's top bit tells the bulk pass, which clears it */
+	if constexpr (NW == 32)
+		rec.z |= (full6 & !fast6) ? 0x80000000u : 0u;
 	/* the verdict stored with the tile: a fast frame's, and a bulk frame's
 	 * provisional one (DROP for a bad IPv4 header under verification,
 	 * else REDIRECT), which the bulk pass overwrites only when the frame's
@@ -2562,10 +2598,10 @@ __device__ __forceinline__ void read_tile_db(const uint4 *win, const uint4 *dslo
  * halves out of the two buffers (the first 64 bytes in win0, bytes
  * [64, 128) in win1, each in the tile layout above) and the descriptor of
  * the tile two steps ahead, after the counted wait vmcnt(N). */
-template <int N>
+template <int N, bool V6>
 __device__ __forceinline__ void read_tile_w2(const uint4 *win0, const uint4 *win1,
-					     const uint4 *dslot, int lane, uint32_t (&F)[34],
-					     uint4 &dn)
+					     const uint4 *dslot, int lane, uint32_t (&F)[18],
+					     WinHi &wh, uint4 &dn)
 {
 	const int sw = (lane >> 2) & 3;
 	const lds_uint4_t *l0 = (const lds_uint4_t *)win0;
@@ -2601,15 +2637,50 @@ __device__ __forceinline__ void read_tile_w2(const uint4 *win0, const uint4 *win
 	else
 		XDP_READ_W2(0);
 #undef XDP_READ_W2
-	const v4u_t vv[8] = {v0, v1, v2, v3, v4, v5, v6, v7};
+	const v4u_t vv[4] = {v0, v1, v2, v3};
 #pragma unroll
-	for (int k = 0; k < 8; k++) {
+	for (int k = 0; k < 4; k++) {
 		F[4 * k] = vv[k].x;
 		F[4 * k + 1] = vv[k].y;
 		F[4 * k + 2] = vv[k].z;
 		F[4 * k + 3] = vv[k].w;
 	}
-	F[32] = F[33] = 0;
+	/* the second half, reduced now (WinHi): the words past the frame's
+	 * tags, each masked by the range end fast_tile derives (the same
+	 * fields: an IPv4 frame's L4 range, with udp_csum's over-read byte
+	 * and, in V6 builds, ICMP's none; an IPv6 frame's UDP length or
+	 * payload length), an IPv6/TCP check word (bytes 70-71 shifted) out;
+	 * fast_tile uses the sum only for the shapes it takes */
+	const uint32_t A[34] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w,
+				v2.x, v2.y, v2.z, v2.w, v3.x, v3.y, v3.z, v3.w,
+				v4.x, v4.y, v4.z, v4.w, v5.x, v5.y, v5.z, v5.w,
+				v6.x, v6.y, v6.z, v6.w, v7.x, v7.y, v7.z, v7.w, 0u, 0u};
+#pragma unroll
+	for (int k = 0; k < 18; k++)
+		F[k] = A[k];
+	const bool t1 = le_is_vlan(A[3] & 0xffff);
+	const bool t2 = t1 & le_is_vlan(A[4] & 0xffff);
+	const uint32_t M2 = t2 ? ~0u : 0u, M1 = (t1 ? ~0u : 0u) & ~M2, M0 = ~(M1 | M2);
+	auto shw = [&](int j) -> uint32_t {
+		return (A[j] & M0) | (A[j + 1] & M1) | (A[j + 2] & M2);
+	};
+	const uint32_t w3 = shw(3), w4 = shw(4), w5 = shw(5);
+	const bool is6 = (w3 & 0xffff) == 0xdd86u;
+	const uint32_t proto = w5 >> 24, nh6 = w5 & 0xff;
+	const uint32_t tot = bswap16(w4 & 0xffff), plen = bswap16(w4 >> 16);
+	const uint32_t cl = proto == 17 ? bswap16(shw(9) >> 16) : tot - 20;
+	const uint32_t e4 = 34 + cl + ((V6 && proto == 1) ? 0u : (cl & 1));
+	const uint32_t e6 = 54 + (nh6 == 17 ? bswap16(shw(14) >> 16) : plen);
+	const int32_t e = (int32_t)(is6 ? e6 : e4);
+	const uint32_t w16 = shw(16), w17 = shw(17);
+	uint64_t s2 = (uint64_t)(w16 & first_bytes(e - 64)) +
+		      (w17 & first_bytes(e - 68) & ((is6 && nh6 == 6) ? 0x0000ffffu : ~0u));
+#pragma unroll
+	for (int j = 18; j < 32; j++)
+		s2 += shw(j) & first_bytes(e - 4 * j);
+	wh.s2 = s2;
+	wh.w16 = w16;
+	wh.w17 = w17;
 	dn = make_uint4(vd.x, vd.y, vd.z, vd.w);
 }
 
@@ -2897,14 +2968,15 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 			 uint64_t td, uint64_t &tn) -> uint4 {
 		const uint64_t i = t * kWave + lane;
 		const bool active = i < nfr;
-		uint32_t F[34];
+		uint32_t F[18];
+		WinHi wh;
 		uint4 dn;
-		read_tile_w2<1>(win0, win1, dsl, lane, F, dn);
+		read_tile_w2<1, V6>(win0, win1, dsl, lane, F, wh, dn);
 		store_tile(a, pend);
 		issue_win2(dnext, tw < ntiles);
 		issue_desc(td, dsl);
 		tn = tile_of(claim(1));
-		fast_tile<false, true, V6, 32>(a, F, dv, i, active, dma, lane, w, &pend);
+		fast_tile<false, true, V6, 32>(a, F, dv, i, active, dma, lane, w, &pend, &wh);
 		return dn;
 	};
 
@@ -3034,22 +3106,23 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 					const uint4 d1 = *reinterpret_cast<const uint4 *>(a.desc + desc_at(c1));
 					issue_win2(d0, true);
 					const uint32_t vn = claim2();
-					uint32_t F[34];
+					uint32_t F[18];
+					WinHi wh;
 					uint4 dn;
 					lds_dma_landed();
-					read_tile_w2<0>(win0, win1, dsl0, lane, F, dn);
+					read_tile_w2<0, V6>(win0, win1, dsl0, lane, F, wh, dn);
 					issue_win2(d1, c1 < ntiles);
 					const uint64_t i0 = c0 * kWave + lane;
 					fast_tile<false, true, V6, 32>(a, F, d0, i0, i0 < nfr, dma, lane, w,
-								       &pend);
+								       &pend, &wh);
 					store_tile(a, pend);
 					if (c1 >= ntiles)
 						break;
 					lds_dma_landed();
-					read_tile_w2<0>(win0, win1, dsl0, lane, F, dn);
+					read_tile_w2<0, V6>(win0, win1, dsl0, lane, F, wh, dn);
 					const uint64_t i1 = c1 * kWave + lane;
 					fast_tile<false, true, V6, 32>(a, F, d1, i1, i1 < nfr, dma, lane, w,
-								       &pend);
+								       &pend, &wh);
 					store_tile(a, pend);
 					c0 = first_of(vn);
 					if (c0 >= ntiles)
