@@ -37,7 +37,8 @@ d_desc = torch.from_numpy(descs.view(np.uint8)).to(dev)
 d_v = torch.empty(n, dtype=torch.uint8, device=dev)
 d_res = torch.empty(n * 16, dtype=torch.uint8, device=dev)
 d_tup = torch.empty(n * 44, dtype=torch.uint8, device=dev)
-ctx = xdpgpu.XdpGpu(0, flags, 0, fmt, 64, tune=tune)
+# STAMPS_WINDOW: the header window (64, 128, 0 = the library's choice)
+ctx = xdpgpu.XdpGpu(0, flags, 0, fmt, int(os.environ.get("STAMPS_WINDOW", "64")), tune=tune)
 st = np.zeros(8 * 8192, np.uint64)
 reps = int(os.environ.get("STAMPS_REPS", "6"))
 per_rep = []   # per launch: each XCC's median and last loop end (us)
