@@ -2446,8 +2446,13 @@ __device__ __forceinline__ void wave_stats_to_lds(const RxArgs &a,
  * groups of 8 loads, every load of a 570-byte IMIX payload useful, ran
  * 8 % slower on IMIX and 13 % on 1500 B: the loads of an instruction
  * then touch 16 frames) */
+/* (8-lane groups since round 4's 128-byte windows, with the bulk ranges
+ * starting at byte 128: IMIX 1.864 / 1.859 vs 1.884 / 1.885 ms, 2 M x
+ * 1500 B 0.589 / 0.590 vs 0.604 / 0.602, the echo leg and config 2
+ * unchanged, alternating processes, profiles/r04_ab_tail_g8.txt; six
+ * loads a lane spilled: IMIX 2.10 ms) */
 #ifndef XDP_TAIL_G
-#define XDP_TAIL_G 16
+#define XDP_TAIL_G 8
 #endif
 #ifndef XDP_TAIL_U
 #define XDP_TAIL_U 4
