@@ -233,14 +233,15 @@ def test_short_bulk_vs_oracle(dev, tune, window, aligned):
             assert (ov == xdpgpu.REDIRECT).sum() > 4000 and (ov == xdpgpu.DROP).sum() > 200
 
 
-def test_unaligned_encoded_descriptors(dev):
+@pytest.mark.parametrize("window", [64, 128])
+def test_unaligned_encoded_descriptors(dev, window):
     """Unaligned-chunk addresses (offset << 48 | base, if_xdp.h:104-106)."""
     umem, descs, _ = xdpgpu.pool_generate(50000, xdpgpu.POOL_IMIX, 64, 11)
     enc = descs.copy()
     base = enc["addr"] & ~np.uint64(0xFFF)
     enc["addr"] = ((enc["addr"] - base) << np.uint64(48)) | base
     ov, ores, otup, _ = oracle.process(umem.copy(), descs, 0x5, 0, 1)
-    v, res, tup, um, _ = run_dev(umem, enc, 0x5, 0, 1)
+    v, res, tup, um, _ = run_dev(umem, enc, 0x5, 0, 1, window)
     assert_same((v, res, tup, None), (ov, ores, otup, None), "encoded")
 
 

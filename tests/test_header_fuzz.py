@@ -93,7 +93,7 @@ def _mutate(fr: bytes, rng) -> bytes:
     return bytes(b)
 
 
-def fuzz_pool(seed: int, n: int):
+def fuzz_pool(seed: int, n: int, align: int = 16):
     rng = np.random.default_rng(seed)
     blobs = []
     for _ in range(n):
@@ -105,8 +105,9 @@ def fuzz_pool(seed: int, n: int):
         blobs.append(fr)
     offs, o = [], 0
     for fr in blobs:
-        # mostly 16-byte aligned (the fast and quick shapes), some not
-        o = (o + 15) & ~15 if rng.random() < 0.9 else o + int(rng.integers(1, 16))
+        # mostly aligned (16 bytes: the fast and quick shapes; 128: a
+        # 128-byte window's second half staged), some not
+        o = (o + align - 1) & ~(align - 1) if rng.random() < 0.9 else o + int(rng.integers(1, 16))
         offs.append(o)
         o += max(len(fr), 1)
     umem = np.zeros(o + 64, np.uint8)
@@ -129,15 +130,20 @@ def test_fuzz_pool_covers_every_class():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed", [1, 2, 3])
-def test_fuzz_vs_oracle(seed):
+@pytest.mark.parametrize("seed,window,align", [(1, 64, 16), (2, 64, 16), (3, 64, 16),
+                                               (4, 128, 128), (5, 128, 128), (6, 128, 16)])
+def test_fuzz_vs_oracle(seed, window, align):
+    """Mutated headers against the oracle; with 128-byte windows the
+    frames mostly start a 128-byte line, so that the second half is staged
+    and the read-time range parse (read_tile_w2) sees the mutations too."""
     torch = pytest.importorskip("torch")
     from test_gpu_parity import assert_same, oracle_stats_match, run_dev
-    umem, descs = fuzz_pool(seed, 20000)
+    umem, descs = fuzz_pool(seed, 20000, align)
     for flags, iv, fmt in ((0x5, 0, 1), (0x7, 0x9E3779B9, 2), (0x4, 3, 0)):
         ou = umem.copy()
         ov, ores, otup, ost = oracle.process(ou, descs, flags, iv, fmt)
-        v, res, tup, um, st = run_dev(umem, descs, flags, iv, fmt, 64, 0)
-        assert_same((v, res, tup, um), (ov, ores, otup, ou), f"fuzz{seed}/{flags:#x}/{fmt}")
+        v, res, tup, um, st = run_dev(umem, descs, flags, iv, fmt, window, 0)
+        assert_same((v, res, tup, um), (ov, ores, otup, ou),
+                    f"fuzz{seed}/w{window}/{flags:#x}/{fmt}")
         oracle_stats_match(st, ost)
     del torch
