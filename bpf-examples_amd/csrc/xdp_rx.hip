@@ -183,6 +183,33 @@ __device__ __forceinline__ uint32_t csum_replace2(uint32_t sum, uint32_t old,
 	return ~c16_add(t, nw) & 0xffff;
 }
 
+/* process_packet's echo reply (af_xdp_user.c:968-1040) of an untagged
+ * ICMPv6 echo request whose first 64 bytes are d: MACs and addresses
+ * swapped, type 129, csum_replace2 of the type word, written over the
+ * frame's first 64 bytes at fp as whole 16-byte chunks */
+__device__ __forceinline__ void echo_reply_store(uint8_t *fp, const uint32_t (&d)[16])
+{
+	uint32_t o[16];
+	auto byte = [&](int b) -> uint32_t { return (d[b >> 2] >> (8 * (b & 3))) & 0xff; };
+	auto src = [&](int b) -> int {
+		return b < 6 ? b + 6 : b < 12 ? b - 6 : (b >= 22 && b < 38) ? b + 16
+		       : (b >= 38 && b < 54) ? b - 16 : b;
+	};
+#pragma unroll
+	for (int w = 0; w < 16; w++)
+		o[w] = byte(src(4 * w)) | (byte(src(4 * w + 1)) << 8) |
+		       (byte(src(4 * w + 2)) << 16) | (byte(src(4 * w + 3)) << 24);
+	/* byte 54: type 129; bytes 56-57: the check word */
+	const uint32_t ck = csum_replace2(d[14] & 0xffff, 0x0080, 0x0081);
+	o[13] = (o[13] & 0xff00ffffu) | (129u << 16);
+	o[14] = (o[14] & 0xffff0000u) | ck;
+	uint4 *fw = reinterpret_cast<uint4 *>(fp);
+	fw[0] = make_uint4(o[0], o[1], o[2], o[3]);
+	fw[1] = make_uint4(o[4], o[5], o[6], o[7]);
+	fw[2] = make_uint4(o[8], o[9], o[10], o[11]);
+	fw[3] = make_uint4(o[12], o[13], o[14], o[15]);
+}
+
 /* ------------------------------------------------------------------ */
 /* jhash (include/jhash.h:25-52), word form; jhash(key, 44) equals
  * jhash2(words, 11) on little-endian (jhash.h:68-142).                 */
@@ -1640,27 +1667,9 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 	 * whole 16-byte chunks; the record and tuple are the request's */
 	const bool echo_tx = echo6 && ((h3.y >> 16) & 0xff) == 128 && !drop;
 	if (echo_tx && !(XDP_TAIL_DIAG & 1)) {
-		uint32_t d[16] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w,
-				  h2.x, h2.y, h2.z, h2.w, h3.x, h3.y, h3.z, h3.w};
-		uint32_t o[16];
-		auto byte = [&](int b) -> uint32_t { return (d[b >> 2] >> (8 * (b & 3))) & 0xff; };
-		auto src = [&](int b) -> int {
-			return b < 6 ? b + 6 : b < 12 ? b - 6 : (b >= 22 && b < 38) ? b + 16
-			       : (b >= 38 && b < 54) ? b - 16 : b;
-		};
-#pragma unroll
-		for (int w = 0; w < 16; w++)
-			o[w] = byte(src(4 * w)) | (byte(src(4 * w + 1)) << 8) |
-			       (byte(src(4 * w + 2)) << 16) | (byte(src(4 * w + 3)) << 24);
-		/* byte 54: type 129; bytes 56-57: the check word */
-		const uint32_t ck = csum_replace2(d[14] & 0xffff, 0x0080, 0x0081);
-		o[13] = (o[13] & 0xff00ffffu) | (129u << 16);
-		o[14] = (o[14] & 0xffff0000u) | ck;
-		uint4 *fw = reinterpret_cast<uint4 *>(a.umem + eff);
-		fw[0] = make_uint4(o[0], o[1], o[2], o[3]);
-		fw[1] = make_uint4(o[4], o[5], o[6], o[7]);
-		fw[2] = make_uint4(o[8], o[9], o[10], o[11]);
-		fw[3] = make_uint4(o[12], o[13], o[14], o[15]);
+		const uint32_t d[16] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w,
+					h2.x, h2.y, h2.z, h2.w, h3.x, h3.y, h3.z, h3.w};
+		echo_reply_store(a.umem + eff, d);
 	}
 	if (XDP_TAIL_DIAG & 1) {
 		/* diagnostic: no output stores */
@@ -2027,7 +2036,9 @@ struct WinHi {
 	uint32_t w16, w17;
 };
 
-template <bool LQ, bool ST = true, bool V6 = false, int NW = 16>
+/* ECHO (128-byte windows with the echo responder on): an untagged ICMPv6
+ * echo request whose range ends inside the window is answered here too */
+template <bool LQ, bool ST = true, bool V6 = false, int NW = 16, bool ECHO = false>
 __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[18],
 					  uint4 dv, uint64_t i, bool active,
 					  bool dma, int lane, FastWave &w,
@@ -2111,7 +2122,7 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 	 * A check word at or past byte 64 (TCP; UDP behind a tag; ICMPv6
 	 * behind two) is "late": the bulk pass reads it, and the data offset,
 	 * from frame bytes [64, 80). */
-	bool v6 = false, i6 = false, t6 = false, full6 = false, fast6 = false;
+	bool v6 = false, i6 = false, t6 = false, full6 = false, fast6 = false, echo_el = false;
 	uint32_t ulen6 = 0, nh6 = 0;
 	if constexpr (V6) {
 		const uint32_t plen = bswap16(r[4] >> 16);
@@ -2141,8 +2152,8 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 			const uint32_t re6 = 54 + 4 * nv + ulen6;
 			full6 = hi & v6 &
 				(!t6 | ((thl6 >= 20) & (54 + 4 * nv + thl6 <= len) & (thl6 <= ulen6)));
-			const bool echo_el = i6 & (nv == 0) & ((a.flags & XDPGPU_CFG_ICMP6_ECHO) != 0);
-			fast6 = full6 & (re6 <= 128u) & !echo_el;
+			echo_el = i6 & (nv == 0) & ((a.flags & XDPGPU_CFG_ICMP6_ECHO) != 0);
+			fast6 = full6 & (re6 <= 128u) & (ECHO | !echo_el);
 		}
 		/* through the bulk pass (which also reads a late check word)
 		 * unless finished in a 128-byte window; a payload inside the
@@ -2299,6 +2310,17 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 	const bool absent = udpv && c4v == 0;
 	const bool l4_ok = absent || (~fold16((uint64_t)sum4 + c4v) & 0xffff) == 0;
 	const bool drop = (a.flags & XDPGPU_CFG_VERIFY_CSUM) && (!l3_ok || !l4_ok);
+	/* the echo responder (ECHO): a finished untagged echo request that
+	 * was not dropped is answered in place (the bulk pass's reply) */
+	bool echo_tx = false;
+	if constexpr (V6 && NW == 32 && ECHO) {
+		echo_tx = fast6 & echo_el & (((r[13] >> 16) & 0xff) == 128) & !drop;
+		if (echo_tx) {
+			const uint32_t d[16] = {F[0], F[1], F[2], F[3], F[4], F[5], F[6], F[7],
+						F[8], F[9], F[10], F[11], F[12], F[13], F[14], F[15]};
+			echo_reply_store(a.umem + eff, d);
+		}
+	}
 	/* a bulk frame's record carries its window sum in the l4_csum field
 	 * and its check word in l4_off until the bulk pass completes it */
 	uint4 rec;
@@ -2358,7 +2380,7 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 		to->li = (uint32_t)(i - to->t0);
 		to->fl = (fast || quick ? 1u : 0u) | (out || quick ? 2u : 0u) | (v6 ? 4u : 0u) |
 			 (quick ? 8u : 0u);
-		to->verdict = quick ? qv : vdrop ? XDPGPU_DROP : XDPGPU_REDIRECT;
+		to->verdict = quick ? qv : echo_tx ? XDPGPU_TX : vdrop ? XDPGPU_DROP : XDPGPU_REDIRECT;
 		/* an IPv6 frame's 16-byte tuple: no addresses, its ports (none
 		 * for ICMPv6), ipv 10 (emit_tuple's layout); a quick frame's:
 		 * zero */
@@ -2385,7 +2407,9 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 				__popcll(__ballot(quick && qv == XDPGPU_ABORTED));
 		}
 		w.cnt[CNT_VERDICT0 + XDPGPU_DROP] += __popcll(__ballot(fast && drop));
-		w.cnt[CNT_VERDICT0 + XDPGPU_REDIRECT] += __popcll(__ballot(fast && !drop));
+		w.cnt[CNT_VERDICT0 + XDPGPU_REDIRECT] += __popcll(__ballot(fast && !drop && !echo_tx));
+		if constexpr (ECHO)
+			w.cnt[CNT_VERDICT0 + XDPGPU_TX] += __popcll(__ballot(echo_tx));
 		w.cnt[CNT_L3_BAD] += __popcll(__ballot(fast && !l3_ok));
 		w.cnt[CNT_L4_BAD] += __popcll(__ballot(fast && !l4_ok));
 		w.cnt[CNT_L4_ABSENT] += __popcll(__ballot(fast && absent));
@@ -2778,10 +2802,11 @@ constexpr int kCuBlock = kCuWaves * kWave;
  * tile's two halves (single-buffered: tile k+1's DMA is issued as tile k
  * is read), so the LDS and the waves per CU stay as they are; not with
  * FRAGS or DIAG. */
-template <bool FRAGS, int DIAG = 0, bool V6 = false, int WIN = 64>
+template <bool FRAGS, int DIAG = 0, bool V6 = false, int WIN = 64, bool ECHO = false>
 __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 {
 	static_assert(WIN == 64 || (WIN == 128 && !FRAGS && !DIAG), "128-byte windows: the RX default only");
+	static_assert(!ECHO || (V6 && WIN == 128), "the tile loop's echo responder: V6, 128-byte windows");
 	__shared__ uint4 lds_all[kCuWaves * kDbWave];
 	/* the block's tile claims, list lengths (exception, bulk) and the
 	 * tail's batch claims (its two passes) */
@@ -2981,7 +3006,7 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 		issue_win2(dnext, tw < ntiles);
 		issue_desc(td, dsl);
 		tn = tile_of(claim(1));
-		fast_tile<false, true, V6, 32>(a, F, dv, i, active, dma, lane, w, &pend, &wh);
+		fast_tile<false, true, V6, 32, ECHO>(a, F, dv, i, active, dma, lane, w, &pend, &wh);
 		return dn;
 	};
 
@@ -3118,7 +3143,7 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 					read_tile_w2<0, V6>(win0, win1, dsl0, lane, F, wh, dn);
 					issue_win2(d1, c1 < ntiles);
 					const uint64_t i0 = c0 * kWave + lane;
-					fast_tile<false, true, V6, 32>(a, F, d0, i0, i0 < nfr, dma, lane, w,
+					fast_tile<false, true, V6, 32, ECHO>(a, F, d0, i0, i0 < nfr, dma, lane, w,
 								       &pend, &wh);
 					store_tile(a, pend);
 					if (c1 >= ntiles)
@@ -3126,7 +3151,7 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 					lds_dma_landed();
 					read_tile_w2<0, V6>(win0, win1, dsl0, lane, F, wh, dn);
 					const uint64_t i1 = c1 * kWave + lane;
-					fast_tile<false, true, V6, 32>(a, F, d1, i1, i1 < nfr, dma, lane, w,
+					fast_tile<false, true, V6, 32, ECHO>(a, F, d1, i1, i1 < nfr, dma, lane, w,
 								       &pend, &wh);
 					store_tile(a, pend);
 					c0 = first_of(vn);
@@ -3328,6 +3353,8 @@ static hipError_t launch_db(RxArgs a, uint32_t max_blocks, hipStream_t stream,
 	const dim3 grid((uint32_t)blocks), blk(kCuBlock);
 	if (a.frags)
 		hipLaunchKernelGGL((xdp_rx_db_kernel<true>), grid, blk, 0, stream, a);
+	else if (a.win == 128 && a.v6 && (a.flags & XDPGPU_CFG_ICMP6_ECHO))
+		hipLaunchKernelGGL((xdp_rx_db_kernel<false, 0, true, 128, true>), grid, blk, 0, stream, a);
 	else if (a.win == 128 && a.v6)
 		hipLaunchKernelGGL((xdp_rx_db_kernel<false, 0, true, 128>), grid, blk, 0, stream, a);
 	else if (a.win == 128)
