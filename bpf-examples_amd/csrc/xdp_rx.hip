@@ -1506,7 +1506,7 @@ __device__ __forceinline__ void stream_short(const RxArgs &a, const uint4 *meta,
 	}
 }
 
-template <int U, bool NT, bool GEN, int G, int WIN = 64>
+template <int U, bool NT, bool GEN, int G, int WIN = 64, bool EC = true>
 __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 					   uint4 *part4, int lane,
 					   const void *list, uint32_t nb,
@@ -1554,7 +1554,8 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 	const bool tup6 = net6 && !kTup6Tile;
 	/* an untagged ICMPv6 frame under the echo responder: its first 64
 	 * bytes, for the type and the rewrite */
-	const bool echo6 = !GEN && act && r6 && (a.flags & XDPGPU_CFG_ICMP6_ECHO) &&
+	/* EC false: an instance the launcher never takes with the responder on */
+	const bool echo6 = EC && !GEN && act && r6 && (a.flags & XDPGPU_CFG_ICMP6_ECHO) &&
 			   ((rv.z >> 8) & 0xff) == 58 && (rv.z >> 24) == 0;
 	uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0, h2 = h0, h3 = h0;
 	if (tup6 || echo6) {
@@ -2145,15 +2146,16 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 			 * word and TCP's data offset taken from the window (a
 			 * data offset that fails parse_tcphdr is left to the bulk
 			 * pass's late path, which ABORTs it); a range that ends
-			 * inside the window is finished here, but for an untagged
-			 * ICMPv6 frame under the echo responder, which the bulk
-			 * pass answers */
+			 * inside the window is finished here (an untagged echo
+			 * request under the responder too: the ECHO instance
+			 * answers it below) */
 			const uint32_t thl6 = ((wh->w16 >> 20) & 0xf) * 4;
 			const uint32_t re6 = 54 + 4 * nv + ulen6;
 			full6 = hi & v6 &
 				(!t6 | ((thl6 >= 20) & (54 + 4 * nv + thl6 <= len) & (thl6 <= ulen6)));
-			echo_el = i6 & (nv == 0) & ((a.flags & XDPGPU_CFG_ICMP6_ECHO) != 0);
-			fast6 = full6 & (re6 <= 128u) & (ECHO | !echo_el);
+			/* (the launcher takes the ECHO instance whenever the responder is on) */
+			echo_el = ECHO & i6 & (nv == 0);
+			fast6 = full6 & (re6 <= 128u);
 		}
 		/* through the bulk pass (which also reads a late check word)
 		 * unless finished in a 128-byte window; a payload inside the
@@ -2482,7 +2484,7 @@ __device__ __forceinline__ void wave_stats_to_lds(const RxArgs &a,
 #define XDP_TAIL_U 4
 #endif
 constexpr int kTailG = XDP_TAIL_G, kTailU = XDP_TAIL_U;
-template <int WIN>
+template <int WIN, bool EC>
 __device__ __forceinline__ void rx_tail(const RxArgs &a, const FastWave &w,
 					uint64_t rb, uint32_t xc, uint32_t bc,
 					int wid, int nw, uint32_t *ctl, int lane,
@@ -2519,7 +2521,7 @@ __device__ __forceinline__ void rx_tail(const RxArgs &a, const FastWave &w,
 		}
 		if (q < nxb + nbb) {
 			const uint32_t b = (q - nxb) * kWave;
-			bulk_batch<kTailU, true, false, kTailG, WIN>(
+			bulk_batch<kTailU, true, false, kTailG, WIN, EC>(
 				a, meta, part4, lane, w.bl + b,
 				bc - b < (uint32_t)kWave ? bc - b : kWave, cnt, my_bytes);
 			STAMP_ADD(rb * nw + wid, lane, 5);
@@ -3193,7 +3195,9 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 	lds_dma_landed();
 	__syncthreads();
 	const uint32_t xc = ctl[1], bc = ctl[2];
-	rx_tail<WIN>(a, w, rb, xc, bc, wid, kCuWaves, ctl, lane, reinterpret_cast<uint32_t *>(wl),
+	/* the bulk pass answers echo requests in a 64-byte window build and
+	 * those the ECHO instance's tiles left to it */
+	rx_tail<WIN, V6 && (WIN == 64 || ECHO)>(a, w, rb, xc, bc, wid, kCuWaves, ctl, lane, reinterpret_cast<uint32_t *>(wl),
 		reinterpret_cast<uint64_t *>(wl + 272), wl, wl + kWave, w.cnt, w.my_bytes);
 
 	/* counters: this wave's own slot (kMaxRxBlocks..: per-wave slots) */
