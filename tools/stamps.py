@@ -110,6 +110,11 @@ for c in cus:
         rank_corr.append(np.corrcoef(order, rk)[0, 1])
 out["waves_per_cu"] = pct(np.array([int((cu == c).sum()) for c in cus]))
 out["within_cu_spread_us"] = pct(np.array(spread))
+# where the launch ends: each CU's last wave against its mean, and the CUs'
+# last waves against each other (the tail phase's imbalance)
+out["within_cu_end_spread_us"] = pct(np.array([np.ptp(us[cu == c, 2]) for c in cus]))
+out["cu_max_end_us"] = pct(np.array([us[cu == c, 2].max() for c in cus]))
+out["cu_mean_end_us"] = pct(np.array([us[cu == c, 2].mean() for c in cus]))
 out["cu_mean_loop_end_us"] = pct(np.array(means))
 out["rank_corr_launch_order_vs_end"] = round(float(np.mean(rank_corr)), 3)
 # per SIMD slot: the waves of one SIMD ranked by launch order
