@@ -38,7 +38,8 @@ constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = kWave * kWavesPerBlock;
 
 /* Diagnostic builds (-DXDPGPU_DBG, tools/dbg_build.sh): the accesses of the
- * double-buffered kernel and its tail are bounds-checked; a violation is
+ * double-buffered kernel and its tail are bounds-checked (codes 1-9; 10:
+ * the echo responder's 64-byte reply store); a violation is
  * counted (g_dbg[2 code]) with its value (g_dbg[2 code + 1]) and the access
  * is skipped.  Read by xdpgpu_debug_read. */
 #ifdef XDPGPU_DBG
@@ -1667,7 +1668,8 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 	 * csum_replace2 of the type word, written over the first 64 bytes as
 	 * whole 16-byte chunks; the record and tuple are the request's */
 	const bool echo_tx = echo6 && ((h3.y >> 16) & 0xff) == 128 && !drop;
-	if (echo_tx && !(XDP_TAIL_DIAG & 1)) {
+	if (echo_tx && !(XDP_TAIL_DIAG & 1) &&
+	    !DBG_BAD(eff + 64 > ((a.usize + 15) & ~15ull), 10, eff)) {
 		const uint32_t d[16] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w,
 					h2.x, h2.y, h2.z, h2.w, h3.x, h3.y, h3.z, h3.w};
 		echo_reply_store(a.umem + eff, d);
@@ -2317,7 +2319,7 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 	bool echo_tx = false;
 	if constexpr (V6 && NW == 32 && ECHO) {
 		echo_tx = fast6 & echo_el & (((r[13] >> 16) & 0xff) == 128) & !drop;
-		if (echo_tx) {
+		if (echo_tx && !DBG_BAD(eff + 64 > ((a.usize + 15) & ~15ull), 10, eff)) {
 			const uint32_t d[16] = {F[0], F[1], F[2], F[3], F[4], F[5], F[6], F[7],
 						F[8], F[9], F[10], F[11], F[12], F[13], F[14], F[15]};
 			echo_reply_store(a.umem + eff, d);
