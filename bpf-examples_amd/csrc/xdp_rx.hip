@@ -1530,10 +1530,12 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 	uint4 rv = *reinterpret_cast<const uint4 *>(a.res + i);
 	/* an IPv6 frame whose 128-byte window summed to byte 128 (fast_tile's
 	 * mark in the nvlan byte, cleared here) */
-	bool w6 = false;
+	bool w6 = false, tsh = false;
 	if constexpr (!GEN && WIN == 128) {
 		w6 = (rv.z >> 31) != 0;
-		rv.z &= 0x7fffffffu;
+		/* its last bytes summed by the tile (XDP_TAIL_SHARE) */
+		tsh = ((rv.z >> 30) & 1) != 0;
+		rv.z &= 0x3fffffffu;
 	}
 	const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
 	const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
@@ -1546,6 +1548,8 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 	const uint32_t l4 = GEN ? (rv.w & 0xffff) : ((rv.z >> 16) & 0xff) + (r6 ? 40u : 20u);
 	const uint32_t rhi = GEN ? (ye.w & 0xffff) : l4 + cl + (nov ? 0u : (cl & 1));
 	uint64_t lim = eff + rhi;
+	/* (the tile took [the line start, lim)) */
+	lim = tsh ? lim & ~127ull : lim;
 	lim = lim < a.usize ? lim : a.usize;
 	/* an IPv6/UDP frame's network_tuple words (the tile stored none):
 	 * frame bytes [16, 64), loaded here so that the round trip overlaps
@@ -2037,7 +2041,21 @@ __device__ __forceinline__ void defer_direct(bool want, uint64_t i, uint32_t *gl
 struct WinHi {
 	uint64_t s2;
 	uint32_t w16, w17;
+	/* XDP_TAIL_SHARE: bit 16 set when the next lane's window held this
+	 * frame's last bytes (its range ends in the first half of the line
+	 * the next frame starts halfway into), their sum folded in bits 0-15 */
+	uint32_t tail;
 };
+/* The line a 64-byte-offset frame starts in: its first half is the end of
+ * the frame before it, which the bulk pass would fetch again.  With
+ * XDP_TAIL_SHARE the window DMA stages that first half in the second
+ * half's slot (no bytes the line fetch does not bring anyway) and the
+ * previous lane's frame, a bulk frame whose range ends there, takes its
+ * sum: the bulk pass streams that frame only to the line start. */
+#ifndef XDP_TAIL_SHARE
+#define XDP_TAIL_SHARE 1
+#endif
+constexpr bool kTailShare = XDP_TAIL_SHARE != 0;
 
 /* ECHO (128-byte windows with the echo responder on): an untagged ICMPv6
  * echo request whose range ends inside the window is answered here too */
@@ -2307,6 +2325,14 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 		protov = v6 ? nh6 : protov;
 		udpv = udpv & !v6;               /* a stored 0 is not absent */
 	}
+	/* a bulk frame whose last bytes the next lane summed (XDP_TAIL_SHARE;
+	 * not an IPv6 frame the bulk pass streams from byte 64, whose check
+	 * word it takes out of its own sum) */
+	bool tshare = false;
+	if constexpr (NW == 32 && kTailShare) {
+		tshare = bulk & ((wh->tail >> 16) & 1) & (!v6 | full6);
+		s4v += tshare ? (wh->tail & 0xffffu) : 0u;
+	}
 	const uint32_t l3c = v6 ? 0u : ~fold16(s3v) & 0xffff;
 	const bool l3_ok = fold16(s3v + c3v) == 0xffff;
 	const uint32_t sum4 = fold16(s4v);
@@ -2340,7 +2366,7 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 	/* an IPv6 bulk frame summed to byte 128 in its window (full6): the
 	 * nvlan byte's top bit tells the bulk pass, which clears it */
 	if constexpr (NW == 32)
-		rec.z |= (full6 & !fast6) ? 0x80000000u : 0u;
+		rec.z |= ((full6 & !fast6) ? 0x80000000u : 0u) | (tshare ? 0x40000000u : 0u);
 	/* the verdict stored with the tile: a fast frame's, and a bulk frame's
 	 * provisional one (DROP for a bad IPv4 header under verification,
 	 * else REDIRECT), which the bulk pass overwrites only when the frame's
@@ -2632,9 +2658,10 @@ __device__ __forceinline__ void read_tile_db(const uint4 *win, const uint4 *dslo
  * [64, 128) in win1, each in the tile layout above) and the descriptor of
  * the tile two steps ahead, after the counted wait vmcnt(N). */
 template <int N, bool V6>
-__device__ __forceinline__ void read_tile_w2(const uint4 *win0, const uint4 *win1,
-					     const uint4 *dslot, int lane, uint32_t (&F)[18],
-					     WinHi &wh, uint4 &dn)
+__device__ __forceinline__ void read_tile_w2(const RxArgs &a, const uint4 *win0,
+					     const uint4 *win1, const uint4 *dslot, int lane,
+					     uint32_t (&F)[18], WinHi &wh, uint4 &dn, uint4 dv,
+					     bool st_ok)
 {
 	const int sw = (lane >> 2) & 3;
 	const lds_uint4_t *l0 = (const lds_uint4_t *)win0;
@@ -2714,6 +2741,39 @@ __device__ __forceinline__ void read_tile_w2(const uint4 *win0, const uint4 *win
 	wh.s2 = s2;
 	wh.w16 = w16;
 	wh.w17 = w17;
+	wh.tail = 0;
+	if constexpr (kTailShare) {
+		/* this lane's range end, absolute, to the next lane; the end of
+		 * the previous lane's, back */
+		const uint64_t addr = ((uint64_t)dv.y << 32) | dv.x;
+		const uint32_t len = dv.z;
+		const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
+		const bool staged = st_ok & (len >= 14) & ((uint64_t)len <= a.usize) &
+				    (eff <= a.usize - len) & !(eff & 15) &
+				    (eff + 64 <= ((a.usize + 15) & ~15ull));
+		/* (a frame starting 64-byte aligned only: its bulk range then
+		 * starts 64-byte aligned too, so it starts at or before the line
+		 * start wherever it ends inside that line's first half; a frame
+		 * starting 16 bytes before the line would have its window and the
+		 * next lane's half-line overlap) */
+		const uint32_t nvt = (uint32_t)t1 + (uint32_t)t2;
+		const uint64_t E = (eff & 63) ? 0ull : eff + (uint32_t)(e > 0 ? e : 0) + 4 * nvt;
+		const uint64_t Ep =
+			((uint64_t)(uint32_t)__shfl_up((int)(uint32_t)(E >> 32), 1, kWave) << 32) |
+			(uint32_t)__shfl_up((int)(uint32_t)E, 1, kWave);
+		/* win1 holds [eff - 64, eff) for a staged frame 64 bytes into its
+		 * line (issue_win2) */
+		const bool lo = staged & ((eff & 127) == 64) & (lane > 0) & (Ep > eff - 64) &
+				(Ep <= eff);
+		const int32_t m = lo ? (int32_t)(Ep - (eff - 64)) : 0;
+		uint64_t ts = 0;
+#pragma unroll
+		for (int j = 0; j < 16; j++)
+			ts += A[16 + j] & first_bytes(m - 4 * j);
+		const uint32_t snd = lo ? 0x10000u | fold16(ts) : 0u;
+		const uint32_t rcv = (uint32_t)__shfl_down((int)snd, 1, kWave);
+		wh.tail = lane < kWave - 1 ? rcv : 0u;
+	}
 	dn = make_uint4(vd.x, vd.y, vd.z, vd.w);
 }
 
@@ -2909,7 +2969,8 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 				(eff <= a.usize - len) & !(eff & 15) &
 				(eff + 64 <= ((a.usize + 15) & ~15ull));
 		const uint64_t e = ok ? eff : 0ull;
-		const uint64_t e2 = ok && win_hi(a, eff, len) ? eff + 64 : 0ull;
+		const uint64_t e2 = ok && win_hi(a, eff, len) ? eff + 64
+				  : kTailShare && ok && (eff & 127) == 64 ? eff - 64 : 0ull;
 #pragma unroll
 		for (int k = 0; k < 4; k++) {
 			const int f = 16 * k + (lane >> 2);
@@ -3005,7 +3066,7 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 		uint32_t F[18];
 		WinHi wh;
 		uint4 dn;
-		read_tile_w2<1, V6>(win0, win1, dsl, lane, F, wh, dn);
+		read_tile_w2<1, V6>(a, win0, win1, dsl, lane, F, wh, dn, dv, active && dma);
 		store_tile(a, pend);
 		issue_win2(dnext, tw < ntiles);
 		issue_desc(td, dsl);
@@ -3144,17 +3205,19 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 					WinHi wh;
 					uint4 dn;
 					lds_dma_landed();
-					read_tile_w2<0, V6>(win0, win1, dsl0, lane, F, wh, dn);
-					issue_win2(d1, c1 < ntiles);
 					const uint64_t i0 = c0 * kWave + lane;
+					read_tile_w2<0, V6>(a, win0, win1, dsl0, lane, F, wh, dn, d0,
+							    i0 < nfr && dma);
+					issue_win2(d1, c1 < ntiles);
 					fast_tile<false, true, V6, 32, ECHO>(a, F, d0, i0, i0 < nfr, dma, lane, w,
 								       &pend, &wh);
 					store_tile(a, pend);
 					if (c1 >= ntiles)
 						break;
 					lds_dma_landed();
-					read_tile_w2<0, V6>(win0, win1, dsl0, lane, F, wh, dn);
 					const uint64_t i1 = c1 * kWave + lane;
+					read_tile_w2<0, V6>(a, win0, win1, dsl0, lane, F, wh, dn, d1,
+							    i1 < nfr && dma);
 					fast_tile<false, true, V6, 32, ECHO>(a, F, d1, i1, i1 < nfr, dma, lane, w,
 								       &pend, &wh);
 					store_tile(a, pend);

@@ -216,6 +216,92 @@ def test_bulk_lengths_vs_oracle(dev, tune, window, aligned):
             assert (ov == xdpgpu.REDIRECT).sum() > 2000 and (ov == xdpgpu.DROP).sum() > 100
 
 
+def shared_line_frames(seed: int, n: int):
+    """Frames laid so that each range ends in the first half of the line
+    the next frame starts 64 bytes into (XDP_TAIL_SHARE: the next lane's
+    window holds those bytes): IPv4 UDP (odd and even lengths, the odd
+    ones' over-read byte the last byte before the next frame), TCP, ICMP,
+    0..2 tags, and IPv6 UDP/TCP/ICMPv6 behind 0..1 tag starting a line;
+    the range ending 1..64 bytes before the next frame, some with pad or
+    a gap, some starting 16 bytes off a 64-byte boundary (not taken), a
+    tenth with a corrupted payload byte."""
+    import frames as F
+    rng = np.random.default_rng(seed)
+    blobs, offs, o = [], [], 0
+    for k in range(n):
+        v6 = rng.random() < 0.3
+        tags = [(0x8100, 5)] * int(rng.integers(0, 2 if v6 else 3))
+        # frame start: a line start (IPv6: its window's second half staged)
+        # or 64 bytes into one; now and then 16 bytes off
+        o = (o + 127) & ~127 if v6 else (o + 63) & ~63
+        if not v6 and rng.random() < 0.1:
+            o += 16
+        start = o
+        # the range end: 1..64 bytes into the line after a line start 64
+        # bytes before the next frame
+        hdr = 14 + 4 * len(tags) + (40 if v6 else 20)
+        lines = int(rng.integers(1, 12))
+        nxt = ((start + hdr + 8 + 127) // 128 + lines) * 128 + 64
+        end = nxt - int(rng.integers(0, 64))           # range end, exclusive
+        kind = int(rng.integers(0, 3))
+        if v6:
+            plen = end - start - hdr - 8
+            pay = rng.integers(0, 256, max(plen, 0), dtype=np.uint8).tobytes()
+            seg = (F.udp(4000 + k, 53, pay) if kind == 0 else
+                   F.tcp(4000 + k, 80, pay[8:] if len(pay) >= 12 else pay) if kind == 1 else
+                   F.icmp(128, 0, b"\x12\x34\x00\x01" + pay))
+            fr = F.v6_frame({0: 17, 1: 6, 2: 58}[kind], seg, tags=tags)
+        else:
+            proto = {0: 17, 1: 6, 2: 1}[kind]
+            plen = end - start - hdr - 8 - (1 if proto == 17 and rng.random() < 0.5 else 0)
+            pay = rng.integers(0, 256, max(plen, 0), dtype=np.uint8).tobytes()
+            seg = (F.udp(4000 + k, 53, pay) if proto == 17 else
+                   F.tcp(4000 + k, 80, pay[12:] if len(pay) >= 12 else pay) if proto == 6 else
+                   F.icmp(8, 0, b"\x12\x34\x00\x01" + pay))
+            fr = F.v4_frame(proto, seg, tags=tags)
+        if rng.random() < 0.1:
+            b = bytearray(fr)
+            b[-1 - int(rng.integers(0, 8))] ^= 0x5A
+            fr = bytes(b)
+        if rng.random() < 0.2:
+            fr += rng.integers(0, 256, int(rng.integers(1, 9)), dtype=np.uint8).tobytes()
+        blobs.append(fr)
+        offs.append(start)
+        o = max(start + len(fr), nxt - (0 if rng.random() < 0.8 else 64))
+    size = offs[-1] + len(blobs[-1]) + 1
+    umem = np.zeros(size, np.uint8)
+    for off, fr in zip(offs, blobs):
+        umem[off:off + len(fr)] = np.frombuffer(fr, np.uint8)
+    # bytes between frames: not zero, so that a wrongly masked half-line
+    # changes the sum
+    gap = np.ones(size, bool)
+    for off, fr in zip(offs, blobs):
+        gap[off:off + len(fr)] = False
+    umem[gap] = rng.integers(1, 256, int(gap.sum()), dtype=np.uint8)
+    descs = np.zeros(n, xdpgpu.DESC_DTYPE)
+    descs["addr"] = offs
+    descs["len"] = [len(fr) for fr in blobs]
+    return umem, descs
+
+
+@pytest.mark.parametrize("tune,window", [(0, 64), (0, 128), (512, 128), (1 << 21, 128)])
+def test_shared_line_vs_oracle(dev, tune, window):
+    """A frame whose range ends in the first half of the line the next
+    frame starts 64 bytes into: the next lane sums those bytes for it and
+    the bulk pass stops at the line start (XDP_TAIL_SHARE, 128-byte
+    windows)."""
+    umem, descs = shared_line_frames(31, 4000)
+    for flags, iv, fmt in ((0x5, 0, 1), (0x4, 0x12345, 2), (0x5, 7, 0)):
+        ov, ores, otup, ost = oracle.process(umem.copy(), descs, flags, iv, fmt)
+        v, res, tup, um, st = run_dev(umem, descs, flags, iv, fmt, window, tune)
+        assert_same((v, res, tup, None), (ov, ores, otup, None), f"shared/{flags:#x}")
+        oracle_stats_match(st, ost)
+        if flags == 0x5 and fmt == 1:
+            # (odd lengths over-read the next, non-zero byte: DROP, with
+            # the record's sum still compared)
+            assert (ov == xdpgpu.REDIRECT).sum() > 2000 and (ov == xdpgpu.DROP).sum() > 100
+
+
 @pytest.mark.parametrize("tune,window", SHORT_VARIANTS)
 @pytest.mark.parametrize("aligned", [True, False])
 def test_short_bulk_vs_oracle(dev, tune, window, aligned):
