@@ -1380,7 +1380,8 @@ constexpr bool kTup6Tile = XDP_TUP6_TILE != 0;
 
 /* Diagnostic builds of the bulk pass (XDP_TAIL_DIAG, never the product):
  * bit 0: no output stores (record, verdict, tuple); bit 1: no payload
- * loads (the range summed as zeros) */
+ * loads (the range summed as zeros); bit 2: no record store; bit 3: no
+ * verdict store */
 #ifndef XDP_TAIL_DIAG
 #define XDP_TAIL_DIAG 0
 #endif
@@ -1701,7 +1702,9 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 		rv.z |= (l4_ok ? XDPGPU_F_L4_OK : 0u) |
 			(absent ? XDPGPU_F_L4_ABSENT : 0u);
 		rv.w = l4 | (cl << 16);
-		if constexpr (kTailRecNt)
+		if constexpr (XDP_TAIL_DIAG & 4) {
+			/* diagnostic: no record store */
+		} else if constexpr (kTailRecNt)
 			st_nt16(a.res + i, rv);
 		else
 			*reinterpret_cast<uint4 *>(a.res + i) = rv;
@@ -1737,7 +1740,7 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 		/* the tile stored the provisional verdict (kBulkVerdictTile) */
 		const uint8_t vprov = (a.flags & XDPGPU_CFG_VERIFY_CSUM) && l3_bad ? XDPGPU_DROP
 										 : XDPGPU_REDIRECT;
-		if (GEN || !kBulkVerdictTile || vd != vprov) {
+		if (!(XDP_TAIL_DIAG & 8) && (GEN || !kBulkVerdictTile || vd != vprov)) {
 			if constexpr (kTailVerdictNt)
 				__builtin_nontemporal_store(vd, a.verdict + i);
 			else
