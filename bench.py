@@ -6,6 +6,10 @@ UMEM pool, xdpsock geometry), one pool shard per GPU (config 5 at N > 1).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
+--gpus N > 1 with no rank environment: this process only launches N child
+ranks (one per GPU, rendezvous on 127.0.0.1) and returns the first failure's
+code; under torch.distributed.run (WORLD_SIZE set) it is one of the ranks.
+
 A step = one RX launch (xdp_rx_db_kernel: one block per CU, the tile loop
 and the deferred-frame tail in one kernel) over the whole 16 M-frame shard
 resident in HBM.  Timing: W untimed steps, barrier + synchronize, K timed
@@ -553,6 +557,202 @@ def echo_run(dev, stream, n, steps, local, size=128, ppm=200000, tune=0, window=
     return out
 
 
+def pcie_ceiling(dev, mib: int = 256, reps: int = 10) -> dict:
+    """What this box's PCIe link moves between page-locked host memory and
+    HBM with plain copies (the ceiling the host path is priced against):
+    H2D alone, D2H alone, and both at once on two streams, GB/s."""
+    nb = mib << 20
+    h_in = torch.empty(nb, dtype=torch.uint8, pin_memory=True)
+    h_out = torch.empty(nb, dtype=torch.uint8, pin_memory=True)
+    d_a = torch.empty(nb, dtype=torch.uint8, device=dev)
+    d_b = torch.empty(nb, dtype=torch.uint8, device=dev)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / reps
+
+    def h2d():
+        with torch.cuda.stream(s1):
+            d_a.copy_(h_in, non_blocking=True)
+
+    def d2h():
+        with torch.cuda.stream(s2):
+            h_out.copy_(d_b, non_blocking=True)
+
+    def both():
+        h2d()
+        d2h()
+
+    t_in, t_out, t_both = timed(h2d), timed(d2h), timed(both)
+    out = {"h2d_gbps": round(nb / t_in / 1e9, 1), "d2h_gbps": round(nb / t_out / 1e9, 1),
+           "duplex_gbps": round(2 * nb / t_both / 1e9, 1),
+           "probe": f"{mib} MiB page-locked copies, {reps} each, torch streams"}
+    del h_in, h_out, d_a, d_b
+    return out
+
+
+def e2e_run(local, umem, descs, expect, B: int, nbatches: int, chunk: int, window: int,
+            ceil: dict) -> dict:
+    """The host path as an RX loop drives it (xdpgpu_submit / xdpgpu_wait,
+    two batches in flight): each batch's frames copied from the pinned host
+    UMEM into the slot's device mirror (rows of chunks when chunk is given:
+    xdpgpu_register_umem), its descriptors in, the kernel, verdicts,
+    records and tuples back into page-locked per-slot buffers.  Batches of B
+    consecutive descriptors cycle over the pool.  One pass checks every
+    batch's verdicts, a second is timed; the PCIe bytes per frame come from
+    xdpgpu_host_stats over the timed pass."""
+    n = len(descs)
+    per = max(1, n // B)
+    h = xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT, 0, xdpgpu.TUPLE_V4, window, max_batch=B)
+    h.register_umem(umem, chunk)
+    # the descriptors as the RX ring holds them (page-locked), and
+    # page-locked per-slot outputs, as an RX loop keeps them
+    hd = xdpgpu.HostBuffer(per * B, xdpgpu.DESC_DTYPE)
+    hd.array[:] = descs[: per * B]
+    outs = [[xdpgpu.HostBuffer(B, dt) for dt in (np.uint8, xdpgpu.RESULT_DTYPE,
+                                                 xdpgpu.TUPLE4_DTYPE)] for _ in range(2)]
+
+    def one_pass(check: bool):
+        ok = True
+        pending = [None, None]
+        t0 = time.perf_counter()
+        for k in range(nbatches + 2):
+            slot = k & 1
+            if pending[slot] is not None:
+                h.wait(slot)
+                if check:
+                    lo = pending[slot]
+                    ok &= bool(np.array_equal(outs[slot][0].array, expect[lo:lo + B]))
+                pending[slot] = None
+            if k >= nbatches:
+                continue
+            lo = (k % per) * B
+            v, r, t = (b.array for b in outs[slot])
+            h.submit(slot, hd.array[lo:lo + B], v, r, t)
+            pending[slot] = lo
+        return time.perf_counter() - t0, ok
+
+    _, ok = one_pass(True)
+    s0 = h.host_stats()
+    te, _ = one_pass(False)
+    s1 = h.host_stats()
+    h.close()
+    hd.close()
+    for o in outs:
+        for b in o:
+            b.close()
+    fr = s1["frames"] - s0["frames"]
+    h2d = (s1["umem_h2d_bytes"] - s0["umem_h2d_bytes"]) + (s1["desc_h2d_bytes"] -
+                                                           s0["desc_h2d_bytes"])
+    d2h = s1["out_d2h_bytes"] - s0["out_d2h_bytes"]
+    h2d_gbps = h2d / te / 1e9
+    d2h_gbps = d2h / te / 1e9
+    return {"mpps": round(fr / te / 1e6, 1), "frames": fr, "batch": B, "batches": nbatches,
+            "chunk": chunk, "pinned_buffers": True,
+            "h2d_bytes_per_frame": round(h2d / fr, 1),
+            "umem_copies_per_batch": round((s1["umem_copies"] - s0["umem_copies"]) /
+                                           max(1, s1["batches"] - s0["batches"]), 1),
+            "d2h_bytes_per_frame": round(d2h / fr, 1),
+            "h2d_gbps": round(h2d_gbps, 1), "d2h_gbps": round(d2h_gbps, 1),
+            "pcie_ceiling": ceil,
+            "pcie_frac": round(max(h2d_gbps / ceil["h2d_gbps"], d2h_gbps / ceil["d2h_gbps"]), 3),
+            "verdicts_ok": ok}
+
+
+def free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def rank_envs(n: int, base: dict, port: int) -> list:
+    """The environment of each of n ranks on this node, as
+    torch.distributed.run sets it: one process per GPU (rank r drives
+    cuda:r), rendezvous on 127.0.0.1."""
+    envs = []
+    for r in range(n):
+        e = dict(base)
+        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n),
+                  "LOCAL_WORLD_SIZE": str(n), "GROUP_RANK": "0",
+                  "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+        e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        envs.append(e)
+    return envs
+
+
+def launch_ranks(cmd: list, n: int, base_env: dict | None = None, poll_s: float = 0.2) -> int:
+    """`bench.py --gpus N` without an outer launcher: start N fresh child
+    processes of `cmd`, one per GPU (the reference's unit of scale is one
+    XSK socket per RX queue, af_xdp_user.c:1542-1611; here one rank per
+    GPU), and wait for them.  The parent is a pure launcher: it has touched
+    neither the GPU nor libxdpgpu (nothing here initialises HIP), and it
+    never execs itself.  If a rank fails, the others are terminated (a rank
+    left waiting in a collective would never finish); the return code is
+    the first failure's, else 0."""
+    import signal
+    import subprocess
+    envs = rank_envs(n, dict(os.environ if base_env is None else base_env), free_port())
+    procs = [subprocess.Popen(cmd, env=e, start_new_session=True) for e in envs]
+    rc = 0
+    try:
+        live = set(range(n))
+        while live:
+            for r in sorted(live):
+                c = procs[r].poll()
+                if c is None:
+                    continue
+                live.discard(r)
+                if c != 0 and rc == 0:
+                    rc = c if c > 0 else 128 - c
+                    log(f"[launcher] rank {r} exited with {c}: stopping the others")
+                    for q in live:
+                        try:
+                            os.killpg(procs[q].pid, signal.SIGTERM)
+                        except ProcessLookupError:
+                            pass
+            if live:
+                time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+                p.wait()
+    return rc
+
+
+def world_plan(gpus: int, env: dict, device_count: int, rehearse: bool) -> str:
+    """What this process is for: "run" (a rank: the outer launcher's, ours,
+    or N = 1) or "launch" (N > 1 and no rank environment: start N ranks).
+    Raises when the world and --gpus disagree, or when fewer GPUs exist
+    than ranks asked for (unless rehearsing: ranks then share GPUs)."""
+    if gpus < 1:
+        raise SystemExit(f"--gpus {gpus}: need at least 1")
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if world != gpus:
+            raise SystemExit(f"WORLD_SIZE {world} but --gpus {gpus}: the launcher and the "
+                             "bench disagree on the number of ranks")
+        plan = "run"
+    else:
+        plan = "launch" if gpus > 1 else "run"
+    if not rehearse and device_count < gpus:
+        raise SystemExit(f"--gpus {gpus} but {device_count} GPU(s) visible: one rank per GPU "
+                         "(set XDPGPU_BENCH_REHEARSE=1 to rehearse ranks sharing GPUs)")
+    return plan
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -573,15 +773,26 @@ def main():
                     help="cfg.tune of the secondary legs' contexts (diagnostic A/B)")
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the end-to-end host path (pinned H2D + kernel + D2H)")
+    ap.add_argument("--e2e-batches", type=int, default=32,
+                    help="batches per timed pass of each host-path leg")
+    ap.add_argument("--e2e-chunked-frames", type=int, default=1 << 20,
+                    help="frames (4 KiB chunks) of the chunked host-path leg's UMEM; 0: skip")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     # XDPGPU_BENCH_REHEARSE=1: a rehearsal of the N-rank path on fewer GPUs
     # than ranks (ranks share devices, gloo for the control collectives);
     # its numbers are not a scaling measurement
     rehearse = os.environ.get("XDPGPU_BENCH_REHEARSE") == "1"
+    # device_count() does not initialise the GPU on this image: the
+    # launcher's children get a clean process each
+    plan = world_plan(args.gpus, os.environ, torch.cuda.device_count(), rehearse)
+    if plan == "launch":
+        sys.exit(launch_ranks([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                              args.gpus))
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
     if rehearse:
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)      # before RCCL binds the rank
@@ -660,36 +871,28 @@ def main():
             secondary["synproxy"] = synproxy_run(dev, stream, 8 << 20, steps2, local)
 
     e2e = None
+    e2e_chunked = None
     if not args.no_e2e and rank == 0 and world == 1:
-        # host path: pinned UMEM, H2D span + descs, kernel, D2H outputs
-        n3 = min(n, 4 << 20)
-        h = xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT, 0, xdpgpu.TUPLE_V4, args.window,
-                          max_batch=1 << 20)
-        h.register_umem(umem)
-        B = 1 << 20
-        # page-locked descriptor and output arrays (xdpgpu_host_alloc), as
-        # an RX loop keeps them
-        hb = [xdpgpu.HostBuffer(n3, dt) for dt in
-              (xdpgpu.DESC_DTYPE, np.uint8, xdpgpu.RESULT_DTYPE, xdpgpu.TUPLE4_DTYPE)]
-        d3, v3, r3, t3 = (b.array for b in hb)
-        d3[:] = descs[:n3]
-        for rep in range(2):
-            t0 = time.perf_counter()
-            for k, lo in enumerate(range(0, n3, B)):
-                slot = k & 1
-                if k >= 2:
-                    h.wait(slot)
-                hi = min(n3, lo + B)
-                h.submit(slot, d3[lo:hi], v3[lo:hi], r3[lo:hi], t3[lo:hi])
-            h.wait(0)
-            h.wait(1)
-            te = time.perf_counter() - t0
-        e2e = {"mpps": round(n3 / te / 1e6, 1), "frames": n3, "batch": B,
-               "pinned_buffers": True,
-               "verdicts_ok": bool(np.array_equal(v3, expect[:n3]))}
-        h.close()
-        for b in hb:
-            b.close()
+        ceil = pcie_ceiling(dev)
+        # host path, the packed pool: pinned UMEM, H2D span + descs, kernel,
+        # D2H outputs
+        e2e = e2e_run(local, umem, descs, expect, 1 << 20, args.e2e_batches, 0,
+                      args.window, ceil)
+        e2e["workload"] = (f"config-2 frames from a packed 64B-stride host UMEM "
+                           f"({umem.nbytes >> 20} MiB), batches cycling over it")
+        if args.e2e_chunked_frames:
+            # the reference's UMEM geometry: 4 KiB chunks (af_xdp_user.c:56-57,
+            # xdpsock.c:133), each 64 B frame at its chunk's XDP_PACKET_HEADROOM
+            nc = args.e2e_chunked_frames
+            cu, cd, ce = xdpgpu.pool_generate(nc, xdpgpu.POOL_UDP4, args.size, 0x5EED0032,
+                                              stride=4096, headroom=256)
+            e2e_chunked = e2e_run(local, cu, cd, ce, nc // 2, args.e2e_batches, 4096,
+                                  args.window, ceil)
+            e2e_chunked["workload"] = (f"{nc} x {args.size}B IPv4/UDP frames in 4 KiB chunks "
+                                       f"at headroom 256 ({cu.nbytes >> 20} MiB host UMEM, "
+                                       "registered with chunk_size 4096), batches of half "
+                                       "the UMEM cycling over it")
+            del cu, cd, ce
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -736,6 +939,8 @@ def main():
         line.update(secondary)
         if e2e:
             line["e2e_host_path"] = e2e
+        if e2e_chunked:
+            line["e2e_host_path_chunked"] = e2e_chunked
         print(json.dumps(line), flush=True)
     ctx.close()
     tctx.close()

@@ -598,15 +598,33 @@ struct injector {
 	volatile uint64_t lost;      /* frames the kernel dropped (no fill
 				      * buffer, RX ring full), or given up on */
 	volatile int stop;
-	volatile int done;           /* every frame sent, or the injector
-				      * failed (rc)                         */
+	volatile int done;           /* every frame sent and accounted for,
+				      * or the injector failed (rc)         */
 	int rc;
+	int64_t drops0;              /* XDP_STATISTICS drops at the start  */
+	uint64_t given_up;           /* frames of stalled windows          */
 };
+
+/* Frames lost so far: the kernel's drops since the start, or the frames
+ * given up on in stalled windows, whichever is more (a window given up on
+ * may be the kernel's drops, reported later: not counted twice). */
+static uint64_t inject_lost(struct injector *in)
+{
+	const int64_t dr = xsk_rx_drops(in->x);
+	const uint64_t kdrop = dr >= 0 && in->drops0 >= 0 && dr > in->drops0 ?
+				       (uint64_t)(dr - in->drops0) : 0;
+	const uint64_t lost = kdrop > in->given_up ? kdrop : in->given_up;
+	in->lost = lost;
+	return lost;
+}
 
 /* Frames given up on when the window has not moved for this long and the
  * kernel reports no drop: far longer than any batch, the first one's code
  * object load and buffer allocation included. */
 #define INJECT_STALL_NS 5000000000ull
+/* After the last send: how long the loss of the final window is waited
+ * for (the receive loop stops 200 ms after its last frame anyway). */
+#define INJECT_DRAIN_NS 1000000000ull
 
 /* Sends the source's frames into the peer, cycling it, keeping at most
  * ring_size / 2 frames ahead of the receiver (no RX-ring overflow: every
@@ -630,15 +648,12 @@ static void *inject_main(void *arg)
 		return NULL;
 	}
 
-	const int64_t drops0 = xsk_rx_drops(in->x);
-	uint64_t given_up = 0, last_rx = 0, t_stall = 0;
+	in->drops0 = xsk_rx_drops(in->x);
+	in->given_up = 0;
+	uint64_t last_rx = 0, t_stall = 0;
 	while (!in->stop && k < in->lv->inject_count) {
 		uint64_t m = in->lv->inject_count - k;
-		const int64_t dr = xsk_rx_drops(in->x);
-		const uint64_t kdrop = dr >= 0 && drops0 >= 0 && dr > drops0 ?
-					       (uint64_t)(dr - drops0) : 0;
-		const uint64_t lost = kdrop + given_up;
-		in->lost = lost;
+		const uint64_t lost = inject_lost(in);
 		const uint64_t got = in->received + lost;
 		const uint64_t ahead = k > got ? k - got : 0;
 		if (ahead >= window) {
@@ -647,7 +662,7 @@ static void *inject_main(void *arg)
 				last_rx = in->received;
 				t_stall = t;
 			} else if (t - t_stall > INJECT_STALL_NS) {
-				given_up += ahead;
+				in->given_up += ahead;
 				t_stall = 0;
 			}
 			usleep(20);
@@ -670,6 +685,15 @@ static void *inject_main(void *arg)
 		in->sent = k;
 	}
 	close(fd);
+	/* the last window (up to ring_size / 2 frames): the kernel counts its
+	 * drops after the last send, so the loss is read until every frame
+	 * sent is received or dropped, for at most INJECT_DRAIN_NS */
+	const uint64_t t_end = now_ns();
+	while (!in->stop && !in->rc) {
+		if (in->received + inject_lost(in) >= k || now_ns() - t_end > INJECT_DRAIN_NS)
+			break;
+		usleep(100);
+	}
 	in->done = 1;
 	return NULL;
 }
@@ -942,6 +966,8 @@ int rx_run_live(const struct rx_live *lv, const struct rx_opts *o, struct rx_tot
 		th_up = false;
 		if (!rc && in.rc)
 			rc = in.rc;
+		/* drops the kernel counted after the injector's last look */
+		(void)inject_lost(&in);
 	}
 	out->seconds = (double)(t1 - t0) / 1e9;
 	if (rc)

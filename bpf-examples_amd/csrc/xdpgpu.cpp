@@ -19,6 +19,8 @@
 #include <vector>
 
 #include <algorithm>
+#include <initializer_list>
+#include <utility>
 #include <map>
 #include <mutex>
 #include <new>
@@ -87,9 +89,12 @@ struct xdpgpu_ctx {
 	uint8_t *h_umem = nullptr;
 	uint64_t umem_size = 0;
 	bool pinned = false;
-	/* the last device UMEM a *_dev call was checked for (device memory
-	 * only: no kernel of the library dereferences host memory) */
-	const void *dev_ok = nullptr;
+	/* aligned-mode chunk size (a power of two) when register_umem gave
+	 * one, else 0: the host path then copies rows of chunks */
+	uint32_t chunk = 0;
+	uint32_t chunk_shift = 0;
+	/* host-path copy accounting (xdpgpu_host_stats) */
+	struct xdpgpu_host_stats hstats{};
 	/* XDPGPU_CFG_TIMING: 4 events per recorded launch */
 	hipEvent_t *tev = nullptr;
 	/* nat64 translator (xdpgpu_nat64_setup) */
@@ -390,6 +395,13 @@ int xdpgpu_register_umem(xdpgpu_ctx *ctx, void *base, uint64_t size,
 	release_umem(ctx);
 	ctx->h_umem = (uint8_t *)base;
 	ctx->umem_size = size;
+	ctx->chunk = 0;
+	ctx->chunk_shift = 0;
+	if (!(flags & XDPGPU_UMEM_UNALIGNED_CHUNK_FLAG) && chunk_size >= 64) {
+		ctx->chunk = chunk_size;
+		while ((1u << ctx->chunk_shift) < chunk_size)
+			ctx->chunk_shift++;
+	}
 	/* pin the caller's UMEM for the copy engines (pageable memory still
 	 * works, only slower).  No kernel reads or writes it: every batch's
 	 * frames are copied into the slot's device mirror and the echo
@@ -616,25 +628,36 @@ int xdpgpu_kernel_times(xdpgpu_ctx *ctx, xdpgpu_ktimes *out)
 	return 0;
 }
 
-/* The UMEM of a *_dev call must be device memory: no kernel of the
- * library dereferences host memory (pinned or mapped host memory read or
- * written through its GPU mapping is what the host-memory faults of
- * rounds 2-3 had in common).  One pointer query per new
- * UMEM (the last one checked is remembered). */
-static int check_dev_umem(xdpgpu_ctx *ctx, const void *p)
+/* Every buffer a *_dev call hands a kernel must be device memory: no
+ * kernel of the library dereferences host memory (pinned or mapped host
+ * memory read or written through its GPU mapping is what the host-memory
+ * faults of rounds 2-3 had in common).  Each pointer is
+ * queried on every call, nothing is remembered: a freed device range can
+ * come back as host memory at the same address (profiles/r04_va_probe*),
+ * and a query costs well under a microsecond next to a launch.  Null
+ * pointers (optional outputs) are skipped. */
+static int check_dev(xdpgpu_ctx *ctx, const char *what, const void *p)
 {
-	if (p == ctx->dev_ok)
+	if (!p)
 		return 0;
 	hipPointerAttribute_t at;
 	memset(&at, 0, sizeof(at));
 	if (hipPointerGetAttributes(&at, p) != hipSuccess) {
 		(void)hipGetLastError();
-		return set_err(ctx, -EINVAL, "UMEM %p is not device memory", p);
+		return set_err(ctx, -EINVAL, "%s %p is not device memory", what, p);
 	}
 	if (at.type != hipMemoryTypeDevice && !at.isManaged)
-		return set_err(ctx, -EINVAL, "UMEM %p is host memory (type %d): the kernels "
-			       "read device memory only", p, (int)at.type);
-	ctx->dev_ok = p;
+		return set_err(ctx, -EINVAL, "%s %p is host memory (type %d): the kernels "
+			       "read and write device memory only", what, p, (int)at.type);
+	return 0;
+}
+
+static int check_dev_all(xdpgpu_ctx *ctx, std::initializer_list<std::pair<const char *,
+			 const void *>> ptrs)
+{
+	for (const auto &w : ptrs)
+		if (int rc = check_dev(ctx, w.first, w.second))
+			return rc;
 	return 0;
 }
 
@@ -647,7 +670,9 @@ int xdpgpu_process_dev(xdpgpu_ctx *ctx, void *d_umem, uint64_t umem_size,
 		return -EINVAL;
 	if (n == 0)
 		return 0;
-	int rc = check_dev_umem(ctx, d_umem);
+	int rc = check_dev_all(ctx, {{"UMEM", d_umem}, {"descriptors", d_descs},
+				     {"verdicts", d_verdict}, {"results", d_res},
+				     {"tuples", d_tuples}});
 	if (rc)
 		return rc;
 	hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
@@ -889,7 +914,8 @@ int xdpgpu_nat64_dev(xdpgpu_ctx *ctx, void *d_umem, uint64_t umem_size,
 		return set_err(ctx, -EINVAL, "xdpgpu_nat64_setup not called");
 	if (n == 0)
 		return 0;
-	if (int rc0 = check_dev_umem(ctx, d_umem))
+	if (int rc0 = check_dev_all(ctx, {{"UMEM", d_umem}, {"descriptors", d_descs},
+					  {"actions", d_action}, {"output descriptors", d_out}}))
 		return rc0;
 	Nat64Args a;
 	memset(&a, 0, sizeof(a));
@@ -996,7 +1022,9 @@ int xdpgpu_synproxy_dev(xdpgpu_ctx *ctx, void *d_umem, uint64_t umem_size,
 	if (n == 0)
 		return 0;
 	HIP_TRY(ctx, hipSetDevice(ctx->cfg.device));
-	if (int rc0 = check_dev_umem(ctx, d_umem))
+	if (int rc0 = check_dev_all(ctx, {{"UMEM", d_umem}, {"descriptors", d_descs},
+					  {"verdicts", d_verdict}, {"output descriptors", d_out},
+					  {"SYN-ACK count", d_synacks}}))
 		return rc0;
 	hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
 	if (d_synacks && !ctx->d_spread) {
@@ -1113,6 +1141,159 @@ static void batch_runs(const xdpgpu_ctx *ctx, const xdpgpu_desc *descs,
 	}
 }
 
+/* Chunked UMEMs (aligned mode, register_umem's chunk_size; the reference's
+ * geometry is 4 KiB chunks, af_xdp_user.c:56-57, xdpsock.c:133, with each
+ * frame at its chunk's headroom): the bytes a batch names are one window
+ * [off_lo, off_hi) of each chunk it uses, the same offsets in every chunk
+ * (the kernel's XDP_PACKET_HEADROOM plus the UMEM headroom, plus the
+ * frame).  They go over as rows: runs of consecutive chunk indices c0..c1
+ * (gaps of up to kRowGap unused chunks copied along), one pitched copy per
+ * run, pitch = the chunk, width = the window.  A 64 B frame in a 4 KiB
+ * chunk then moves its own line, where the span copy of batch_runs moves
+ * the whole chunk.  False when the rows do not pay (the window is half the
+ * chunk or more: frames fill their chunks) or do not hold (a frame whose
+ * udp_csum over-read byte lies in the next chunk): the caller copies
+ * spans. */
+struct Rows {
+	uint64_t c0, c1;
+};
+constexpr uint64_t kRowGap = 8;
+
+static bool batch_rows(const xdpgpu_ctx *ctx, const xdpgpu_desc *descs, uint32_t n,
+		       std::vector<Rows> &rows, uint64_t &off_lo, uint64_t &off_hi,
+		       uint64_t &used)
+{
+	rows.clear();
+	used = 0;
+	if (!ctx->chunk)
+		return false;
+	const uint64_t mask = ctx->chunk - 1;
+	const uint32_t sh = ctx->chunk_shift;
+	off_lo = UINT64_MAX;
+	off_hi = 0;
+	bool scattered = false;
+	for (uint32_t i = 0; i < n; i++) {
+		const uint64_t eff = descs[i].addr;
+		/* an offset field in aligned mode: decoded as the kernel decodes
+		 * it (addr>>48 added), by the span path */
+		if (eff >> 48)
+			return false;
+		if (eff >= ctx->umem_size)
+			continue;
+		const uint64_t off = eff & mask;
+		const uint64_t end = off + descs[i].len + 1;
+		if (end > ctx->chunk)
+			return false;
+		off_lo = std::min(off_lo, off);
+		off_hi = std::max(off_hi, end);
+		used += descs[i].len;
+		if (scattered)
+			continue;
+		const uint64_t c = eff >> sh;
+		if (!rows.empty() && c >= rows.back().c0 && c <= rows.back().c1 + kRowGap) {
+			rows.back().c1 = std::max(rows.back().c1, c);
+			continue;
+		}
+		if (rows.size() == kMaxRuns) {
+			scattered = true;
+			continue;
+		}
+		rows.push_back({c, c});
+	}
+	if (off_hi <= off_lo || 2 * (off_hi - off_lo) > ctx->chunk) {
+		/* (an empty window: no frame in the UMEM; rows: none to copy) */
+		if (off_hi <= off_lo) {
+			rows.clear();
+			return true;
+		}
+		return false;
+	}
+	if (!scattered)
+		return true;
+	std::vector<uint64_t> cs;
+	cs.reserve(n);
+	for (uint32_t i = 0; i < n; i++)
+		if (descs[i].addr < ctx->umem_size)
+			cs.push_back(descs[i].addr >> sh);
+	std::sort(cs.begin(), cs.end());
+	cs.erase(std::unique(cs.begin(), cs.end()), cs.end());
+	for (uint64_t gap = kRowGap;; gap *= 4) {
+		rows.clear();
+		for (uint64_t c : cs) {
+			if (!rows.empty() && c <= rows.back().c1 + gap)
+				rows.back().c1 = c;
+			else
+				rows.push_back({c, c});
+		}
+		if (rows.size() <= kMaxRuns)
+			return true;
+	}
+}
+
+/* Copy a batch's frames into the slot's mirror: rows of chunks where they
+ * pay (batch_rows), else spans (batch_runs).  Sets used (the bytes the
+ * descriptors name) and adds the copy's bytes to the host stats. */
+static int copy_batch(xdpgpu_ctx *ctx, Slot &s, const xdpgpu_desc *descs, uint32_t n,
+		      uint64_t &used)
+{
+	std::vector<Rows> rows;
+	uint64_t off_lo = 0, off_hi = 0;
+	uint64_t bytes = 0, copies = 0;
+	if (batch_rows(ctx, descs, n, rows, off_lo, off_hi, used)) {
+		const uint64_t chunk = ctx->chunk, w = off_hi - off_lo;
+		const uint32_t sh = ctx->chunk_shift;
+		for (const Rows &r : rows) {
+			uint64_t c1 = r.c1;
+			/* a last chunk cut short by the UMEM's end: its row alone,
+			 * clamped (the host UMEM is never read past its size) */
+			if ((c1 << sh) + off_hi > ctx->umem_size) {
+				const uint64_t a = (c1 << sh) + off_lo;
+				if (a < ctx->umem_size) {
+					HIP_TRY(ctx, hipMemcpyAsync(s.d_mirror + a, ctx->h_umem + a,
+								    ctx->umem_size - a,
+								    hipMemcpyHostToDevice, s.stream));
+					bytes += ctx->umem_size - a;
+					copies++;
+				}
+				if (c1 == r.c0)
+					continue;
+				c1--;
+			}
+			const uint64_t a = (r.c0 << sh) + off_lo, h = c1 - r.c0 + 1;
+			if (h == 1)
+				HIP_TRY(ctx, hipMemcpyAsync(s.d_mirror + a, ctx->h_umem + a, w,
+							    hipMemcpyHostToDevice, s.stream));
+			else
+				HIP_TRY(ctx, hipMemcpy2DAsync(s.d_mirror + a, chunk, ctx->h_umem + a,
+							      chunk, w, h, hipMemcpyHostToDevice,
+							      s.stream));
+			bytes += w * h;
+			copies++;
+		}
+	} else {
+		std::vector<Run> runs;
+		uint64_t lo, hi;
+		batch_runs(ctx, descs, n, runs, lo, hi, used);
+		for (const Run &r : runs) {
+			HIP_TRY(ctx, hipMemcpyAsync(s.d_mirror + r.lo, ctx->h_umem + r.lo, r.hi - r.lo,
+						    hipMemcpyHostToDevice, s.stream));
+			bytes += r.hi - r.lo;
+			copies++;
+		}
+	}
+	ctx->hstats.umem_h2d_bytes += bytes;
+	ctx->hstats.umem_copies += copies;
+	return 0;
+}
+
+int xdpgpu_host_stats(xdpgpu_ctx *ctx, struct xdpgpu_host_stats *out)
+{
+	if (!ctx || !out)
+		return -EINVAL;
+	*out = ctx->hstats;
+	return 0;
+}
+
 int xdpgpu_submit(xdpgpu_ctx *ctx, uint32_t slot, const xdpgpu_desc *descs,
 		  uint32_t n, uint8_t *verdict, xdpgpu_result *res,
 		  void *tuples)
@@ -1137,18 +1318,24 @@ int xdpgpu_submit(xdpgpu_ctx *ctx, uint32_t slot, const xdpgpu_desc *descs,
 
 	/* the frames go to this slot's own mirror: a batch in flight on the
 	 * other slot never sees them, whatever the two batches' addresses */
-	std::vector<Run> runs;
-	uint64_t lo, hi, used;
-	batch_runs(ctx, descs, n, runs, lo, hi, used);
+	uint64_t used = 0;
+	rc = copy_batch(ctx, s, descs, n, used);
+	if (rc)
+		return rc;
 	const bool echo = ctx->cfg.flags & XDPGPU_CFG_ICMP6_ECHO;
-	for (const Run &r : runs)
-		HIP_TRY(ctx, hipMemcpyAsync(s.d_mirror + r.lo, ctx->h_umem + r.lo, r.hi - r.lo,
-					    hipMemcpyHostToDevice, s.stream));
 	HIP_TRY(ctx, hipMemcpyAsync(s.d_desc, descs, (size_t)n * sizeof(*descs),
 				    hipMemcpyHostToDevice, s.stream));
 	uint8_t *d_tup = (tuples && ctx->cfg.tuple_fmt) ? s.d_tup : nullptr;
+	/* the mean frame length picks the window (xdpgpu.h: 128 bytes when
+	 * the frames average at least 128) */
 	rc = enqueue_rx(ctx, s, s.d_mirror, ctx->umem_size, s.d_desc, n, s.d_verdict,
-			res ? s.d_res : nullptr, d_tup, s.stream, used / n + 1);
+			res ? s.d_res : nullptr, d_tup, s.stream,
+			std::max<uint64_t>(used / n, 1));
+	ctx->hstats.batches++;
+	ctx->hstats.frames += n;
+	ctx->hstats.desc_h2d_bytes += (uint64_t)n * sizeof(*descs);
+	ctx->hstats.out_d2h_bytes += (uint64_t)n * (1 + (res ? sizeof(*res) : 0) +
+						     (d_tup ? tuple_bytes(ctx->cfg.tuple_fmt) : 0));
 	if (rc)
 		return rc;
 	/* echo replies were written in the mirror: only the TX frames' first
@@ -1362,7 +1549,8 @@ int xdpgpu_hints_dev(xdpgpu_ctx *ctx, const void *d_umem, uint64_t umem_size,
 		return -EINVAL;
 	if (n == 0)
 		return 0;
-	if (int rc0 = check_dev_umem(ctx, d_umem))
+	if (int rc0 = check_dev_all(ctx, {{"UMEM", d_umem}, {"descriptors", d_descs},
+					  {"hints", d_out}}))
 		return rc0;
 	hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
 	HIP_TRY(ctx, launch_hints((const uint8_t *)d_umem, umem_size, d_descs, n,

@@ -104,6 +104,13 @@ class Stats(C.Structure):
                 "l4_absent": self.l4_absent, "frag": self.frag}
 
 
+class HostStats(C.Structure):
+    """struct xdpgpu_host_stats"""
+    _fields_ = [("batches", C.c_uint64), ("frames", C.c_uint64),
+                ("umem_h2d_bytes", C.c_uint64), ("umem_copies", C.c_uint64),
+                ("desc_h2d_bytes", C.c_uint64), ("out_d2h_bytes", C.c_uint64)]
+
+
 class KTimes(C.Structure):
     _fields_ = [("launches", C.c_uint64), ("fast_ms", C.c_double),
                 ("bulk_ms", C.c_double), ("exception_ms", C.c_double),
@@ -165,6 +172,7 @@ EXPORTS = (
     "xdpgpu_host_free", "xdpgpu_jhash2_dev", "xdpgpu_jhash_nwords_dev",
     "xdpgpu_queue_stats", "xdpgpu_nat64_dynamic", "xdpgpu_nat64_clock",
     "xdpgpu_nat64_state", "xdpgpu_nat64_direction", "xdpgpu_synproxy_dev",
+    "xdpgpu_host_stats",
 )
 
 # struct xdpgpu_hints (XDP hints in front of a frame)
@@ -223,6 +231,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.xdpgpu_host_alloc.restype = vp
     lib.xdpgpu_host_free.argtypes = [vp]
     lib.xdpgpu_host_free.restype = None
+    lib.xdpgpu_host_stats.argtypes = [vp, C.POINTER(HostStats)]
     _lib = lib
     return lib
 
@@ -474,6 +483,12 @@ class XdpGpu:
         s = Stats()
         self._check(self.lib.xdpgpu_stats(self.h, C.byref(s)), "xdpgpu_stats")
         return s.as_dict()
+
+    def host_stats(self) -> dict:
+        """What the host path moved over PCIe (xdpgpu_host_stats)."""
+        s = HostStats()
+        self._check(self.lib.xdpgpu_host_stats(self.h, C.byref(s)), "xdpgpu_host_stats")
+        return {k: int(getattr(s, k)) for k, _ in HostStats._fields_}
 
     def stats_reset(self) -> None:
         self._check(self.lib.xdpgpu_stats_reset(self.h), "xdpgpu_stats_reset")

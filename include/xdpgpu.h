@@ -183,8 +183,10 @@ void xdpgpu_fini(struct xdpgpu_ctx *ctx);
 
 /* Register the host UMEM (replaces xsk_umem__create's buffer argument,
  * af_xdp_user.c:433 / xdpsock.c:1013).  The memory stays owned by the caller;
- * it is pinned and mapped (hipHostRegister) and each in-flight slot keeps a
- * device mirror of it.  -EBUSY while a slot is in flight. */
+ * it is pinned (hipHostRegister, for the copy engines only) and each
+ * in-flight slot keeps a device mirror of it.  chunk_size (aligned mode, a
+ * power of two, 0: none) lets the host path copy only each chunk's window
+ * of frame bytes (xdpgpu_host_stats).  -EBUSY while a slot is in flight. */
 int xdpgpu_register_umem(struct xdpgpu_ctx *ctx, void *base, uint64_t size,
 			 uint32_t chunk_size, uint32_t headroom, uint32_t flags);
 
@@ -219,6 +221,23 @@ int xdpgpu_wait(struct xdpgpu_ctx *ctx, uint32_t slot);
  * failure. */
 void *xdpgpu_host_alloc(uint64_t size);
 void xdpgpu_host_free(void *p);
+
+/* What the host path moved over PCIe since the context was made (a
+ * diagnostic beside xdpsock's rx/tx counts, xdpsock.c:dump_stats): UMEM
+ * bytes copied host to device, in how many copies, descriptor bytes in and
+ * output bytes (verdict, record, tuple) back.  With a chunk size given to
+ * xdpgpu_register_umem (aligned mode), a batch moves one window of each
+ * chunk it names, the same offsets in every chunk (rows of a pitched
+ * copy); otherwise spans of nearby frames. */
+struct xdpgpu_host_stats {
+	uint64_t batches;
+	uint64_t frames;
+	uint64_t umem_h2d_bytes;
+	uint64_t umem_copies;
+	uint64_t desc_h2d_bytes;
+	uint64_t out_d2h_bytes;
+};
+int xdpgpu_host_stats(struct xdpgpu_ctx *ctx, struct xdpgpu_host_stats *out);
 
 /* Device-resident form: every pointer is device memory (d_umem is written
  * only for ICMPv6 echo rewrites; a d_umem in host memory, pinned or not, is

@@ -45,14 +45,16 @@ def ring_batches(nframes: int, nbatch: int, B: int, seed: int):
     return out
 
 
-def run_ring(umem, descs, batches, flags, tune, fmt=xdpgpu.TUPLE_NET, pinned=True, window=64):
+def run_ring(umem, descs, batches, flags, tune, fmt=xdpgpu.TUPLE_NET, pinned=True, window=64,
+             chunk=0, host_stats=None):
     """Submit the batches alternately on the two slots, waiting for a slot
-    only when it is needed again; returns outputs per batch and stats."""
+    only when it is needed again; returns outputs per batch and stats
+    (host_stats, a dict, receives xdpgpu_host_stats)."""
     n_max = max(len(b) for b in batches)
     tb = xdpgpu.TUPLE_BYTES[fmt]
     outs = []
     with xdpgpu.XdpGpu(0, flags, 0x9E3779B9, fmt, window, max_batch=n_max, tune=tune) as ctx:
-        ctx.register_umem(umem)
+        ctx.register_umem(umem, chunk)
         bufs = []
         for slot in range(2):
             if pinned:
@@ -88,6 +90,8 @@ def run_ring(umem, descs, batches, flags, tune, fmt=xdpgpu.TUPLE_NET, pinned=Tru
             if pending[slot] is not None:
                 collect(slot)
         st = ctx.stats()
+        if host_stats is not None:
+            host_stats.update(ctx.host_stats())
         for bb in bufs:
             for x in bb:
                 if hasattr(x, "close"):
@@ -328,3 +332,95 @@ def test_scattered_batch_runs(window):
     np.testing.assert_array_equal(res.view(np.uint8).reshape(-1), ores.view(np.uint8).reshape(-1))
     assert int((ov == xdpgpu.TX).sum()) > 100
     assert np.array_equal(host, ou)
+
+
+CHUNK, HEADROOM = 4096, 256     # af_xdp_user.c:56-57; XDP_PACKET_HEADROOM
+
+
+def chunked_pool(n, kind, size, seed, **kw):
+    return xdpgpu.pool_generate(n, kind, size, seed, stride=CHUNK, headroom=HEADROOM, **kw)
+
+
+def check_ring(got, want, host, ou, st, ost):
+    for k, (g, w) in enumerate(zip(got, want)):
+        np.testing.assert_array_equal(g[0], w[0], err_msg=f"batch {k} verdicts")
+        np.testing.assert_array_equal(g[1].view(np.uint8).reshape(-1), w[1],
+                                      err_msg=f"batch {k} results")
+        np.testing.assert_array_equal(g[2], w[2], err_msg=f"batch {k} tuples")
+    assert np.array_equal(host, ou), "host UMEM differs from the oracle's"
+    assert st["frames"] == ost["frames"]
+    assert [st["verdict"][x] for x in xdpgpu.VERDICT_NAMES] == ost["verdict"]
+
+
+@pytest.mark.parametrize("kind,size,ppm", [(xdpgpu.POOL_UDP4, 64, 300000),
+                                           (xdpgpu.POOL_IMIX, 64, 200000)],
+                         ids=["udp64", "imix"])
+def test_ring_chunked_umem(kind, size, ppm):
+    """The reference's UMEM geometry (4 KiB chunks, each frame at its
+    chunk's headroom) registered with its chunk size: the host path copies
+    one window of each chunk (rows of a pitched copy).  Recycled,
+    wrapping and strided batches (the scattered path merges chunk runs),
+    echo replies written back: outputs and the whole host UMEM equal the
+    oracle's."""
+    nframes = 8192
+    umem, descs, _ = chunked_pool(nframes, kind, size, 71, ppm_echo6=ppm)
+    assert int(descs["addr"][1]) == CHUNK + HEADROOM
+    batches = ring_batches(nframes, 12, 1024, 72)
+    host = umem.copy()
+    hs = {}
+    got, st = run_ring(host, descs, batches, ECHO, 0, window=0, chunk=CHUNK, host_stats=hs)
+    ou = umem.copy()
+    want, ost = oracle_ring(ou, descs, batches, ECHO)
+    check_ring(got, want, host, ou, st, ost)
+    ntx = sum(int((w[0] == xdpgpu.TX).sum()) for w in want)
+    assert ntx > 100
+    assert hs["frames"] == sum(len(b) for b in batches)
+    # a window of each chunk: far below the chunk per frame
+    assert hs["umem_h2d_bytes"] < hs["frames"] * CHUNK // 2, hs
+
+
+def test_chunked_consecutive_bytes():
+    """Consecutive 64 B frames in 4 KiB chunks: exactly one row of the
+    batch's window (its longest frame and udp_csum's over-read byte) per
+    chunk, one copy per batch; outputs equal the oracle's."""
+    nframes, B = 4096, 1024
+    umem, descs, _ = chunked_pool(nframes, xdpgpu.POOL_UDP4, 64, 73)
+    batches = [np.arange(k, k + B) for k in range(0, nframes, B)]
+    host = umem.copy()
+    hs = {}
+    got, st = run_ring(host, descs, batches, 0x5, 0, fmt=xdpgpu.TUPLE_V4, window=0,
+                       chunk=CHUNK, host_stats=hs)
+    ou = umem.copy()
+    want, ost = oracle_ring(ou, descs, batches, 0x5, fmt=xdpgpu.TUPLE_V4)
+    check_ring(got, want, host, ou, st, ost)
+    lens = descs["len"].astype(np.int64)
+    # every frame sits at the chunk's headroom: a batch's window is its
+    # longest frame + 1, once per chunk
+    assert hs["umem_h2d_bytes"] == sum(len(b) * (int(lens[b].max()) + 1) for b in batches), hs
+    assert hs["umem_copies"] == len(batches), hs
+    assert hs["desc_h2d_bytes"] == nframes * 16
+
+
+def test_chunked_fallbacks_and_umem_end():
+    """The rows' edges: a frame whose over-read byte lies in the next chunk
+    (the batch falls back to span copies), and a UMEM whose size is not a
+    whole number of chunks, its last frame cut by the UMEM's end (the last
+    row is copied clamped, never read past the host UMEM)."""
+    nframes = 600
+    umem, descs, _ = chunked_pool(nframes, xdpgpu.POOL_UDP4, 64, 74)
+    # frame 5 fills its chunk to the last byte: udp_csum reads one past it
+    d = descs.copy()
+    d["addr"][5] = 5 * CHUNK + HEADROOM
+    d["len"][5] = CHUNK - HEADROOM
+    cut = (nframes - 1) * CHUNK + HEADROOM + 40          # the last frame cut at 40 bytes
+    small = np.ascontiguousarray(umem[:cut])
+    for name, u, batch in (("over-read into the next chunk", umem, np.arange(0, 64)),
+                           ("UMEM end", small, np.arange(nframes - 300, nframes))):
+        host = u.copy()
+        hs = {}
+        got, st = run_ring(host, d, [batch], 0x5, 0, fmt=xdpgpu.TUPLE_V4, window=0,
+                           chunk=CHUNK, host_stats=hs)
+        ou = u.copy()
+        want, ost = oracle_ring(ou, d, [batch], 0x5, fmt=xdpgpu.TUPLE_V4)
+        check_ring(got, want, host, ou, st, ost)
+        assert hs["frames"] == len(batch), name

@@ -120,3 +120,28 @@ def test_bench_two_rank_rehearsal():
     assert js["n_gpus"] == 2 and js["verdicts_ok"] is True and js["value"] > 0
     assert js["scaling"] == "weak" and js["config"]["parallelism"] == "shard2"
     assert js["config"]["frames_per_gpu"] == 1 << 20
+
+
+@pytest.mark.gpu
+def test_bench_self_launch():
+    """`python bench.py --gpus 2` with no outer launcher, as the driver may
+    run it: the process launches its two ranks itself (ranks sharing cuda:0
+    under XDPGPU_BENCH_REHEARSE=1), and the one rank-0 line reports both
+    ranks' frames."""
+    import json
+    import subprocess
+    import sys
+    env = dict(os.environ, XDPGPU_BENCH_REHEARSE="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--frames", str(1 << 20),
+                        "--steps", "3", "--warmup", "1", "--no-cpu", "--no-secondary",
+                        "--no-e2e"], capture_output=True, text=True, timeout=240, env=env,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    js = json.loads(lines[0])
+    assert js["n_gpus"] == 2 and js["verdicts_ok"] is True and js["value"] > 0
+    assert js["config"]["parallelism"] == "shard2"
+    assert js["config"]["frames_per_gpu"] == 1 << 20
