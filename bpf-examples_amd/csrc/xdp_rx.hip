@@ -2637,25 +2637,33 @@ template <int N>
 __device__ __forceinline__ void read_tile_db(const uint4 *win, const uint4 *dslot,
 					     int lane, uint32_t (&F)[18], uint4 &dn)
 {
+	/* one address VGPR per buffer: the lane's slot 4 lane + (c ^ sw) is
+	 * p ^ 16 c for p = its slot sw (the per-wave buffers are 64-byte
+	 * aligned, so the XOR touches only bits 4-5); the chunk addresses are
+	 * made in the asm, so that the compiler keeps no four-register set of
+	 * loop-invariant LDS addresses live over the tile loop (they were what
+	 * the 128-VGPR budget spilled) */
 	const int sw = (lane >> 2) & 3;
 	const lds_uint4_t *lw = (const lds_uint4_t *)win;
 	const lds_uint4_t *ld = (const lds_uint4_t *)dslot;
-	const uint32_t a0 = (uint32_t)(uintptr_t)(lw + 4 * lane + (0 ^ sw));
-	const uint32_t a1 = (uint32_t)(uintptr_t)(lw + 4 * lane + (1 ^ sw));
-	const uint32_t a2 = (uint32_t)(uintptr_t)(lw + 4 * lane + (2 ^ sw));
-	const uint32_t a3 = (uint32_t)(uintptr_t)(lw + 4 * lane + (3 ^ sw));
+	const uint32_t p = (uint32_t)(uintptr_t)(lw + 4 * lane + sw);
 	const uint32_t ad = (uint32_t)(uintptr_t)(ld + lane);
 	v4u_t v0, v1, v2, v3, vd;
+	uint32_t t1, t2, t3;
 #define XDP_READ_TILE(N)                                                        \
 	asm volatile("s_waitcnt vmcnt(" #N ")\n\t"                              \
-		     "ds_read_b128 %0, %5\n\t"                                  \
-		     "ds_read_b128 %1, %6\n\t"                                  \
-		     "ds_read_b128 %2, %7\n\t"                                  \
-		     "ds_read_b128 %3, %8\n\t"                                  \
+		     "v_xor_b32 %5, 16, %8\n\t"                                \
+		     "v_xor_b32 %6, 32, %8\n\t"                                \
+		     "v_xor_b32 %7, 48, %8\n\t"                                \
+		     "ds_read_b128 %0, %8\n\t"                                  \
+		     "ds_read_b128 %1, %5\n\t"                                  \
+		     "ds_read_b128 %2, %6\n\t"                                  \
+		     "ds_read_b128 %3, %7\n\t"                                  \
 		     "ds_read_b128 %4, %9\n\t"                                  \
 		     "s_waitcnt lgkmcnt(0)"                                     \
-		     : "=&v"(v0), "=&v"(v1), "=&v"(v2), "=&v"(v3), "=&v"(vd)    \
-		     : "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(ad)              \
+		     : "=&v"(v0), "=&v"(v1), "=&v"(v2), "=&v"(v3), "=&v"(vd),   \
+		       "=&v"(t1), "=&v"(t2), "=&v"(t3)                          \
+		     : "v"(p), "v"(ad)                                          \
 		     : "memory")
 	if constexpr (N == 10)
 		XDP_READ_TILE(10);
@@ -2680,34 +2688,35 @@ __device__ __forceinline__ void read_tile_w2(const RxArgs &a, const uint4 *win0,
 					     uint32_t (&F)[18], WinHi &wh, uint4 &dn, uint4 dv,
 					     bool st_ok)
 {
+	/* the addresses as in read_tile_db: one VGPR for the lane's window
+	 * slots (win1 is win0 + 4 KiB: the instructions' offset field) */
 	const int sw = (lane >> 2) & 3;
 	const lds_uint4_t *l0 = (const lds_uint4_t *)win0;
-	const lds_uint4_t *l1 = (const lds_uint4_t *)win1;
 	const lds_uint4_t *ld = (const lds_uint4_t *)dslot;
-	uint32_t ad[9];
-#pragma unroll
-	for (int c = 0; c < 4; c++) {
-		ad[c] = (uint32_t)(uintptr_t)(l0 + 4 * lane + (c ^ sw));
-		ad[4 + c] = (uint32_t)(uintptr_t)(l1 + 4 * lane + (c ^ sw));
-	}
-	ad[8] = (uint32_t)(uintptr_t)(ld + lane);
+	(void)win1;
+	const uint32_t p = (uint32_t)(uintptr_t)(l0 + 4 * lane + sw);
+	const uint32_t ad = (uint32_t)(uintptr_t)(ld + lane);
 	v4u_t v0, v1, v2, v3, v4, v5, v6, v7, vd;
+	uint32_t x1, x2, x3;
 #define XDP_READ_W2(N)                                                          \
 	asm volatile("s_waitcnt vmcnt(" #N ")\n\t"                             \
-		     "ds_read_b128 %0, %9\n\t"                                 \
-		     "ds_read_b128 %1, %10\n\t"                                \
-		     "ds_read_b128 %2, %11\n\t"                                \
-		     "ds_read_b128 %3, %12\n\t"                                \
-		     "ds_read_b128 %4, %13\n\t"                                \
-		     "ds_read_b128 %5, %14\n\t"                                \
-		     "ds_read_b128 %6, %15\n\t"                                \
-		     "ds_read_b128 %7, %16\n\t"                                \
-		     "ds_read_b128 %8, %17\n\t"                                \
+		     "v_xor_b32 %9, 16, %12\n\t"                               \
+		     "v_xor_b32 %10, 32, %12\n\t"                              \
+		     "v_xor_b32 %11, 48, %12\n\t"                              \
+		     "ds_read_b128 %0, %12\n\t"                                \
+		     "ds_read_b128 %1, %9\n\t"                                 \
+		     "ds_read_b128 %2, %10\n\t"                                \
+		     "ds_read_b128 %3, %11\n\t"                                \
+		     "ds_read_b128 %4, %12 offset:4096\n\t"                    \
+		     "ds_read_b128 %5, %9 offset:4096\n\t"                     \
+		     "ds_read_b128 %6, %10 offset:4096\n\t"                    \
+		     "ds_read_b128 %7, %11 offset:4096\n\t"                    \
+		     "ds_read_b128 %8, %13\n\t"                                \
 		     "s_waitcnt lgkmcnt(0)"                                     \
 		     : "=&v"(v0), "=&v"(v1), "=&v"(v2), "=&v"(v3), "=&v"(v4),   \
-		       "=&v"(v5), "=&v"(v6), "=&v"(v7), "=&v"(vd)               \
-		     : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3]), "v"(ad[4]), \
-		       "v"(ad[5]), "v"(ad[6]), "v"(ad[7]), "v"(ad[8])           \
+		       "=&v"(v5), "=&v"(v6), "=&v"(v7), "=&v"(vd),              \
+		       "=&v"(x1), "=&v"(x2), "=&v"(x3)                          \
+		     : "v"(p), "v"(ad)                                          \
 		     : "memory")
 	if constexpr (N == 1)
 		XDP_READ_W2(1);
@@ -2888,7 +2897,9 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 {
 	static_assert(WIN == 64 || (WIN == 128 && !FRAGS && !DIAG), "128-byte windows: the RX default only");
 	static_assert(!ECHO || (V6 && WIN == 128), "the tile loop's echo responder: V6, 128-byte windows");
-	__shared__ uint4 lds_all[kCuWaves * kDbWave];
+	/* 64-byte aligned: read_tile_db and read_tile_w2 address a lane's window
+	 * slots by XOR inside each wave's 64-byte aligned buffers */
+	__shared__ __attribute__((aligned(64))) uint4 lds_all[kCuWaves * kDbWave];
 	/* the block's tile claims, list lengths (exception, bulk) and the
 	 * tail's batch claims (its two passes) */
 	__shared__ uint32_t ctl[8];
