@@ -1259,11 +1259,32 @@ __device__ __forceinline__ bool le_is_vlan(uint32_t v)
 	return (v == 0x0081u) | (v == 0xa888u);
 }
 
-/* mask of the first nb (0..4) bytes of a dword */
+/* mask of the first nb (0..4) bytes of a dword: a clamp, one multiply-add
+ * and one 64-bit shift (0xffffffff >> 32 is 0 in 64 bits, where the 32-bit
+ * shift's count wraps) */
 __device__ __forceinline__ uint32_t first_bytes(int32_t nb)
 {
-	nb = nb < 0 ? 0 : nb > 4 ? 4 : nb;
-	return nb ? (0xffffffffu >> ((32 - 8 * nb) & 31)) : 0u;
+	const int32_t c = nb < 0 ? 0 : nb > 4 ? 4 : nb;
+	return (uint32_t)(0xffffffffull >> (32 - 8 * c));
+}
+
+/* mask's lane set ? b : a (v_cndmask_b32 on a wave-wide lane mask) */
+__device__ __forceinline__ uint32_t lane_sel(uint64_t mask, uint32_t a, uint32_t b)
+{
+	uint32_t r;
+	asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(mask));
+	return r;
+}
+
+/* acc plus the two 16-bit halves of x (v_sad_u16 against zero): the
+ * one's-complement sums accumulate 16-bit halves in 32 bits, congruent mod
+ * 0xffff to the 32-bit words' sum and zero exactly when it is, so fold16
+ * gives the same result with one instruction a word instead of a 64-bit
+ * add.  acc must stay far below 2^32 (2^32 is 1 mod 0xffff: a wrap would
+ * change the sum): start chains from 0 or a small raw term. */
+__device__ __forceinline__ uint32_t add_halves(uint32_t acc, uint32_t x)
+{
+	return __builtin_amdgcn_sad_u16(x, 0u, acc);
 }
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -2072,6 +2093,14 @@ struct WinHi {
 #ifndef XDP_TAIL_SHARE
 #define XDP_TAIL_SHARE 1
 #endif
+/* diagnostic builds only (instruction-count and timing probes, wrong
+ * outputs): parts of the tile loop's compute left out.  1 the second half's
+ * reduction (read_tile_w2), 2 the jhash, 4 the IPv6 shape, 8 the quick
+ * classification, 16 the counters, 32 the deferrals (no tail work), 64 the
+ * 128-byte tile loop's output stores */
+#ifndef XDP_TILE_DIAG
+#define XDP_TILE_DIAG 0
+#endif
 constexpr bool kTailShare = XDP_TAIL_SHARE != 0;
 
 /* ECHO (128-byte windows with the echo responder on): an untagged ICMPv6
@@ -2107,12 +2136,13 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 		for (int j = 3; j < 16; j++)
 			r[j] = F[j];
 	} else {
-		const uint32_t m2 = 0u - (uint32_t)v2;
-		const uint32_t m1 = (0u - (uint32_t)v1) & ~m2;
-		const uint32_t m0 = ~(m1 | m2);
+		/* two selects a word on the lanes' tag masks, as asm: written
+		 * as C selects the compiler turns the words into a dynamically
+		 * indexed private array (scratch) */
+		const uint64_t k1 = __ballot(v1), k2 = __ballot(v2);
 #pragma unroll
 		for (int j = 3; j < 16; j++)
-			r[j] = (F[j] & m0) | (F[j + 1] & m1) | (F[j + 2] & m2);
+			r[j] = lane_sel(k2, lane_sel(k1, F[j], F[j + 1]), F[j + 2]);
 	}
 	const uint32_t l3 = 14 + 4 * nv, l4 = l3 + 20;
 	const uint32_t tot = bswap16(r[4] & 0xffff);
@@ -2162,7 +2192,7 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 	 * from frame bytes [64, 80). */
 	bool v6 = false, i6 = false, t6 = false, full6 = false, fast6 = false, echo_el = false;
 	uint32_t ulen6 = 0, nh6 = 0;
-	if constexpr (V6) {
+	if constexpr (V6 && !(XDP_TILE_DIAG & 4)) {
 		const uint32_t plen = bswap16(r[4] >> 16);
 		nh6 = r[5] & 0xff;
 		const uint32_t ity = (r[13] >> 16) & 0xff;
@@ -2218,7 +2248,7 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 	 * Every other frame the fast shape does not take stays an exception. */
 	bool quick = false;
 	uint32_t qv = XDPGPU_ABORTED;
-	if (!LQ && kQuick && (!XDP_QUICK_SKIP || __ballot(active & !fast & !bulk))) {
+	if (!LQ && kQuick && !(XDP_TILE_DIAG & 8) && (!XDP_QUICK_SKIP || __ballot(active & !fast & !bulk))) {
 		const uint32_t et = r[3] & 0xffff;
 		const bool big = (!a.force_generic) & staged & (len >= 64);
 		const bool arp = big & (et == 0x0608u);
@@ -2251,9 +2281,11 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 		defer_append(active && !fast && !bulk, i, w.xq, w.xq_n, w.xl, w.xout, lane);
 		defer_append(bulk, i, w.bq, w.bq_n, w.bl, w.bout, lane);
 	} else {
-		defer_direct(active && !fast && !bulk && !quick, i, w.xl, w.lcount, lane,
-			     a.xregion);
-		defer_direct(bulk, i, w.bl, w.lcount + 1, lane, a.xregion);
+		if constexpr (!(XDP_TILE_DIAG & 32)) {
+			defer_direct(active && !fast && !bulk && !quick, i, w.xl, w.lcount, lane,
+				     a.xregion);
+			defer_direct(bulk, i, w.bl, w.lcount + 1, lane, a.xregion);
+		}
 	}
 
 	/* 4. fast frames: flow key, hash, tuple, checksums, verdict */
@@ -2261,8 +2293,10 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 	const uint32_t da = (r[7] >> 16) | (r[8] << 16);
 	const uint32_t ports = icmp ? 0u : (r[8] >> 16) | (r[9] << 16);
 	/* IPv4 header sum, check word (r6 low half) excluded */
-	const uint64_t s3 = (uint64_t)(r[3] & 0xffff0000u) + r[4] + r[5] +
-			    (r[6] & 0xffff0000u) + r[7] + (r[8] & 0xffffu);
+	/* (the sums are of 16-bit halves in 32 bits, add_halves: congruent
+	 * mod 0xffff to the words' sums, so every fold16 below is unchanged) */
+	const uint32_t s3 = add_halves(add_halves(add_halves(add_halves(add_halves(
+		r[3] >> 16, r[4]), r[5]), r[6] >> 16), r[7]), r[8] & 0xffffu);
 	const uint32_t c3 = r[6] & 0xffff;
 	const uint32_t c4 = udp ? (r[10] & 0xffff) : icmp ? (r[9] & 0xffff) : (r[12] >> 16);
 	/* L4 sum over [34, end) of the shifted frame with the pseudo
@@ -2273,36 +2307,40 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 	 * frame words up to 15 + nv; those past 15 count only for hi. */
 	const int32_t e0 = (int32_t)(34 + cl + over);
 	const int32_t e = (NW == 16 || hi) ? e0 : min(e0, (int32_t)(64 - 4 * nv));
-	uint64_t s4 = (uint64_t)(r[8] & 0xffff0000u) +
-		      (icmp ? 0ull : (uint64_t)sa + da + ((uint64_t)(proto + cl) << 8));
+	uint32_t s4 = add_halves(icmp ? 0u : add_halves(add_halves((proto + cl) << 8, sa), da),
+				 r[8] >> 16);
 	if constexpr (NW == 32)
-		s4 += hi ? wh->s2 : 0ull;
+		s4 += hi ? (uint32_t)wh->s2 : 0u;
+	/* first_bytes(e - 4 j) as one clamp and one 64-bit shift */
+	const int32_t sb = 32 - 8 * e;
 #pragma unroll
 	for (int j = 9; j < 16; j++) {
-		uint32_t m = first_bytes(e - 4 * j);
+		uint32_t m = (uint32_t)(0xffffffffull >> min(max(sb + 32 * j, 0), 32));
 		if (j == 9)
 			m &= icmp ? 0xffff0000u : 0xffffffffu;
 		if (j == 10)
 			m &= udp ? 0xffff0000u : 0xffffffffu;
 		if (j == 12)
 			m &= udp || icmp ? 0xffffffffu : 0x0000ffffu;
-		s4 += r[j] & m;
+		s4 = add_halves(s4, r[j] & m);
 	}
 	uint32_t key[11] = {0, 0, 0xffff0000u, sa, ports & 0xffff,
 			    0, 0, 0xffff0000u, da, ports >> 16,
 			    proto | (2u << 16)};
-	uint64_t s3v = s3, s4v = s4;
+	uint32_t s3v = s3, s4v = s4;
 	uint32_t c3v = c3, c4v = c4, clv = cl, l4v = l4, protov = proto;
 	bool udpv = udp;
-	if constexpr (V6) {
+	if constexpr (V6 && !(XDP_TILE_DIAG & 4)) {
 		/* the v6 frame's terms (selected per lane: branch free), in the
 		 * shifted words: L4 at 54, addresses at 22-53 */
-		uint64_t p6 = (uint64_t)__builtin_bswap32(ulen6) + __builtin_bswap32(nh6);
+		/* (from 0: a raw first term near 2^32 would wrap the 32-bit sum) */
+		uint32_t p6 = add_halves(add_halves(0u, __builtin_bswap32(ulen6)),
+					 __builtin_bswap32(nh6));
 #pragma unroll
 		for (int k = 0; k < 4; k++) {
 			const uint32_t sk = (r[5 + k] >> 16) | (r[6 + k] << 16);
 			const uint32_t dk = (r[9 + k] >> 16) | (r[10 + k] << 16);
-			p6 += (uint64_t)sk + dk;
+			p6 = add_halves(add_halves(p6, sk), dk);
 			key[k] = v6 ? sk : key[k];
 			key[5 + k] = v6 ? dk : key[5 + k];
 		}
@@ -2315,18 +2353,18 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 		 * 64-byte windows they are zero) */
 		const uint32_t r14 = (NW == 16 || nv < 2 || full6) ? r[14] : 0u;
 		const uint32_t r15 = (NW == 16 || nv < 1 || full6) ? r[15] : 0u;
-		uint64_t s46 = p6 + (r[13] & 0xffff0000u) +
-			       (r14 & first_bytes(e6 - 56) & (i6 ? 0xffff0000u : ~0u)) +
-			       (r15 & first_bytes(e6 - 60) & (u6 ? 0xffff0000u : ~0u));
+		uint32_t s46 = add_halves(add_halves(add_halves(p6, r[13] >> 16),
+					   r14 & first_bytes(e6 - 56) & (i6 ? 0xffff0000u : ~0u)),
+					   r15 & first_bytes(e6 - 60) & (u6 ? 0xffff0000u : ~0u));
 		if constexpr (NW == 32)
 			/* the second half (TCP's check word left out by the
 			 * read) */
-			s46 += full6 ? wh->s2 : 0ull;
+			s46 += full6 ? (uint32_t)wh->s2 : 0u;
 		key[4] = v6 ? (i6 ? 0u : r[13] >> 16) : key[4];
 		key[9] = v6 ? (i6 ? 0u : r[14] & 0xffffu) : key[9];
 		key[10] = v6 ? (nh6 | (10u << 16)) : key[10];
 		s4v = v6 ? s46 : s4v;
-		s3v = v6 ? 0xffffull : s3v;      /* no IPv6 header checksum: l3 ok */
+		s3v = v6 ? 0xffffu : s3v;        /* no IPv6 header checksum: l3 ok */
 		c3v = v6 ? 0u : c3v;
 		/* the check word where the window holds it (0: late, the bulk
 		 * pass loads it) */
@@ -2351,7 +2389,7 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 		s4v += tshare ? (wh->tail & 0xffffu) : 0u;
 	}
 	const uint32_t l3c = v6 ? 0u : ~fold16(s3v) & 0xffff;
-	const bool l3_ok = fold16(s3v + c3v) == 0xffff;
+	const bool l3_ok = fold16((uint64_t)s3v + c3v) == 0xffff;
 	const uint32_t sum4 = fold16(s4v);
 	const uint32_t l4c = ~sum4 & 0xffff;
 	const bool absent = udpv && c4v == 0;
@@ -2371,7 +2409,7 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 	/* a bulk frame's record carries its window sum in the l4_csum field
 	 * and its check word in l4_off until the bulk pass completes it */
 	uint4 rec;
-	rec.x = jhash_key44(key, a.initval);
+	rec.x = (XDP_TILE_DIAG & 2) ? key[0] ^ key[8] : jhash_key44(key, a.initval);
 	rec.y = l3c | ((fast ? l4c : sum4) << 16);
 	rec.z = XDPGPU_F_IP | XDPGPU_F_L4 | (nv ? XDPGPU_F_VLAN : 0u) |
 		(v6 ? XDPGPU_F_IPV6 : 0u) |
@@ -2446,7 +2484,7 @@ __device__ __forceinline__ void fast_tile(const RxArgs &a, const uint32_t (&F)[1
 	}
 	w.my_bytes += fast || quick ? len : 0;
 	/* counters (wave-uniform: ballots outside divergent code) */
-	if (a.stats) {
+	if (!(XDP_TILE_DIAG & 16) && a.stats) {
 		w.cnt[CNT_FRAMES] += __popcll(__ballot(fast || quick));
 		if constexpr (!LQ && kQuick) {
 			w.cnt[CNT_VERDICT0 + XDPGPU_PASS] += __popcll(__ballot(quick && qv == XDPGPU_PASS));
@@ -2746,10 +2784,20 @@ __device__ __forceinline__ void read_tile_w2(const RxArgs &a, const uint4 *win0,
 		F[k] = A[k];
 	const bool t1 = le_is_vlan(A[3] & 0xffff);
 	const bool t2 = t1 & le_is_vlan(A[4] & 0xffff);
-	const uint32_t M2 = t2 ? ~0u : 0u, M1 = (t1 ? ~0u : 0u) & ~M2, M0 = ~(M1 | M2);
+	const uint32_t nvt = (uint32_t)t1 + (uint32_t)t2;
+	/* a header word past the tags: two selects (the frame's words are not
+	 * shifted: the sums below move the range end by the tags instead) */
+	const uint64_t k1 = __ballot(t1), k2 = __ballot(t2);
 	auto shw = [&](int j) -> uint32_t {
-		return (A[j] & M0) | (A[j + 1] & M1) | (A[j + 2] & M2);
+		return lane_sel(k2, lane_sel(k1, A[j], A[j + 1]), A[j + 2]);
 	};
+	if constexpr ((XDP_TILE_DIAG & 1) != 0) {
+		wh.s2 = 0;
+		wh.w16 = wh.w17 = 0;
+		wh.tail = 0;
+		dn = make_uint4(vd.x, vd.y, vd.z, vd.w);
+		return;
+	}
 	const uint32_t w3 = shw(3), w4 = shw(4), w5 = shw(5);
 	const bool is6 = (w3 & 0xffff) == 0xdd86u;
 	const uint32_t proto = w5 >> 24, nh6 = w5 & 0xff;
@@ -2759,11 +2807,44 @@ __device__ __forceinline__ void read_tile_w2(const RxArgs &a, const uint4 *win0,
 	const uint32_t e6 = 54 + (nh6 == 17 ? bswap16(shw(14) >> 16) : plen);
 	const int32_t e = (int32_t)(is6 ? e6 : e4);
 	const uint32_t w16 = shw(16), w17 = shw(17);
-	uint64_t s2 = (uint64_t)(w16 & first_bytes(e - 64)) +
-		      (w17 & first_bytes(e - 68) & ((is6 && nh6 == 6) ? 0x0000ffffu : ~0u));
+	/* the tag-shifted words 16..31 masked by the range end e are the
+	 * frame's words 16 + nv..31 masked by the frame-relative end E; the
+	 * shifted word 17 of an IPv6/TCP frame keeps only its low half (the
+	 * check word at shifted bytes 70-71 is left out) */
+	const int32_t E = (e > 0 ? e : 0) + 4 * (int32_t)nvt;
+	const bool tcp6 = is6 && nh6 == 6;
+	/* words 16 and 17 count only past the tags; an IPv6/TCP frame's
+	 * shifted word 17 keeps its low half */
+	auto wmask = [&](int k) -> uint32_t {
+		uint32_t m = ~0u;
+		if (k == 16)
+			m = t1 ? 0u : m;
+		if (k == 17)
+			m = t2 ? 0u : m;
+		if (k >= 17 && k <= 19)
+			m &= (tcp6 && (uint32_t)k == 17 + nvt) ? 0x0000ffffu : ~0u;
+		return m;
+	};
+	uint32_t s2 = 0;
+	if (!__ballot((E > 64) & (E < 128))) {
+		/* no range ends inside the second half (IMIX, 1500 B: 64-byte
+		 * frames end before it, the long ones after): each lane's words
+		 * count whole or not at all */
 #pragma unroll
-	for (int j = 18; j < 32; j++)
-		s2 += shw(j) & first_bytes(e - 4 * j);
+		for (int k = 16; k < 32; k++)
+			s2 = add_halves(s2, A[k] & wmask(k));
+		s2 = E >= 128 ? s2 : 0u;
+	} else {
+		/* byte masks first_bytes(E - 4 k) as one clamp and one 64-bit
+		 * shift each: the shift 32 - 8 (E - 4 k) clamped to [0, 32] */
+		const int32_t sb = 32 - 8 * E;
+#pragma unroll
+		for (int k = 16; k < 32; k++) {
+			const int32_t sh = min(max(sb + 32 * k, 0), 32);
+			const uint32_t m = (uint32_t)(0xffffffffull >> sh) & wmask(k);
+			s2 = add_halves(s2, A[k] & m);
+		}
+	}
 	wh.s2 = s2;
 	wh.w16 = w16;
 	wh.w17 = w17;
@@ -2782,21 +2863,27 @@ __device__ __forceinline__ void read_tile_w2(const RxArgs &a, const uint4 *win0,
 		 * start wherever it ends inside that line's first half; a frame
 		 * starting 16 bytes before the line would have its window and the
 		 * next lane's half-line overlap) */
-		const uint32_t nvt = (uint32_t)t1 + (uint32_t)t2;
-		const uint64_t E = (eff & 63) ? 0ull : eff + (uint32_t)(e > 0 ? e : 0) + 4 * nvt;
+		const uint64_t Eabs = (eff & 63) ? 0ull : eff + (uint32_t)E;
 		const uint64_t Ep =
-			((uint64_t)(uint32_t)__shfl_up((int)(uint32_t)(E >> 32), 1, kWave) << 32) |
-			(uint32_t)__shfl_up((int)(uint32_t)E, 1, kWave);
+			((uint64_t)(uint32_t)__shfl_up((int)(uint32_t)(Eabs >> 32), 1, kWave) << 32) |
+			(uint32_t)__shfl_up((int)(uint32_t)Eabs, 1, kWave);
 		/* win1 holds [eff - 64, eff) for a staged frame 64 bytes into its
 		 * line (issue_win2) */
 		const bool lo = staged & ((eff & 127) == 64) & (lane > 0) & (Ep > eff - 64) &
 				(Ep <= eff);
-		const int32_t m = lo ? (int32_t)(Ep - (eff - 64)) : 0;
-		uint64_t ts = 0;
+		uint32_t snd = 0;
+		/* (a tile with no such frame skips the sum) */
+		if (__ballot(lo)) {
+			const int32_t m = lo ? (int32_t)(Ep - (eff - 64)) : 0;
+			const int32_t sb = 32 - 8 * m;
+			uint32_t ts = 0;
 #pragma unroll
-		for (int j = 0; j < 16; j++)
-			ts += A[16 + j] & first_bytes(m - 4 * j);
-		const uint32_t snd = lo ? 0x10000u | fold16(ts) : 0u;
+			for (int j = 0; j < 16; j++) {
+				const int32_t sh = min(max(sb + 32 * j, 0), 32);
+				ts = add_halves(ts, A[16 + j] & (uint32_t)(0xffffffffull >> sh));
+			}
+			snd = lo ? 0x10000u | fold16(ts) : 0u;
+		}
 		const uint32_t rcv = (uint32_t)__shfl_down((int)snd, 1, kWave);
 		wh.tail = lane < kWave - 1 ? rcv : 0u;
 	}
@@ -3095,7 +3182,8 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
 		WinHi wh;
 		uint4 dn;
 		read_tile_w2<1, V6>(a, win0, win1, dsl, lane, F, wh, dn, dv, active && dma);
-		store_tile(a, pend);
+		if constexpr (!(XDP_TILE_DIAG & 64))
+			store_tile(a, pend);
 		issue_win2(dnext, tw < ntiles);
 		issue_desc(td, dsl);
 		tn = tile_of(claim(1));

@@ -231,7 +231,9 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.xdpgpu_host_alloc.restype = vp
     lib.xdpgpu_host_free.argtypes = [vp]
     lib.xdpgpu_host_free.restype = None
-    lib.xdpgpu_host_stats.argtypes = [vp, C.POINTER(HostStats)]
+    # (absent from libraries of earlier rounds, which A/B runs load)
+    if hasattr(lib, "xdpgpu_host_stats"):
+        lib.xdpgpu_host_stats.argtypes = [vp, C.POINTER(HostStats)]
     _lib = lib
     return lib
 
