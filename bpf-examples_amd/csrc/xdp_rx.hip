@@ -113,9 +113,19 @@ __device__ __forceinline__ uint32_t fold16(uint64_t x)
 	return y;
 }
 
+/* the sum of a dword's two 16-bit halves (v_sad_u16 against zero) */
 __device__ __forceinline__ uint32_t halves(uint32_t d)
 {
-	return (d & 0xffff) + (d >> 16);
+	return __builtin_amdgcn_sad_u16(d, 0u, 0u);
+}
+
+/* acc + the halves of a 16-byte chunk's four dwords, one v_sad_u16 each */
+__device__ __forceinline__ uint32_t add_chunk(uint32_t acc, uint4 v)
+{
+	acc = __builtin_amdgcn_sad_u16(v.x, 0u, acc);
+	acc = __builtin_amdgcn_sad_u16(v.y, 0u, acc);
+	acc = __builtin_amdgcn_sad_u16(v.z, 0u, acc);
+	return __builtin_amdgcn_sad_u16(v.w, 0u, acc);
 }
 
 __device__ __forceinline__ uint32_t bswap16(uint32_t v)
@@ -760,8 +770,7 @@ __device__ __forceinline__ uint32_t ext_sums(const RxArgs &a, bool need,
 					v[k].z &= m.z;
 					v[k].w &= m.w;
 				}
-				acc[k] += halves(v[k].x) + halves(v[k].y) +
-					  halves(v[k].z) + halves(v[k].w);
+				acc[k] = add_chunk(acc[k], v[k]);
 			}
 		}
 #pragma unroll
@@ -1475,8 +1484,7 @@ __device__ __forceinline__ void stream_groups(const RxArgs &a, const uint4 *meta
 				v[u].z &= mk.z;
 				v[u].w &= mk.w;
 			}
-			acc += halves(v[u].x) + halves(v[u].y) + halves(v[u].z) +
-			       halves(v[u].w);
+			acc = add_chunk(acc, v[u]);
 		}
 		o += 16 * G * U;
 		const bool done = live && o >= fnb;
@@ -1531,8 +1539,7 @@ __device__ __forceinline__ void stream_short(const RxArgs &a, const uint4 *meta,
 			v[u].w &= mk.w;
 		}
 		if (f < nb)
-			part[16 * f + sub] = halves(v[u].x) + halves(v[u].y) + halves(v[u].z) +
-					     halves(v[u].w);
+			part[16 * f + sub] = add_chunk(0u, v[u]);
 	}
 }
 
@@ -1591,14 +1598,16 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 	/* EC false: an instance the launcher never takes with the responder on */
 	const bool echo6 = EC && !GEN && act && r6 && (a.flags & XDPGPU_CFG_ICMP6_ECHO) &&
 			   ((rv.z >> 8) & 0xff) == 58 && (rv.z >> 24) == 0;
+	/* (an echo request's first 64 bytes are loaded after the streaming,
+	 * below: the ECHO instance answers most requests in its tile loop, so
+	 * a batch rarely holds one, and 16 registers live across the
+	 * streaming spilled) */
 	uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0, h2 = h0, h3 = h0;
-	if (tup6 || echo6) {
+	if (tup6) {
 		h1 = *reinterpret_cast<const uint4 *>(a.umem + eff + 16);
 		h2 = *reinterpret_cast<const uint4 *>(a.umem + eff + 32);
 		h3 = *reinterpret_cast<const uint4 *>(a.umem + eff + 48);
 	}
-	if (echo6)
-		h0 = *reinterpret_cast<const uint4 *>(a.umem + eff);
 	/* a "late" IPv6 frame (fast_tile): its check word (and TCP's data
 	 * offset) lie in frame bytes [64, 80), which the UMEM holds (both
 	 * before l4 + 20 <= len) */
@@ -1700,6 +1709,14 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 	 * request that was not dropped: MACs and addresses swapped, type 129,
 	 * csum_replace2 of the type word, written over the first 64 bytes as
 	 * whole 16-byte chunks; the record and tuple are the request's */
+	if (__ballot(echo6)) {
+		if (echo6) {
+			h0 = *reinterpret_cast<const uint4 *>(a.umem + eff);
+			h1 = *reinterpret_cast<const uint4 *>(a.umem + eff + 16);
+			h2 = *reinterpret_cast<const uint4 *>(a.umem + eff + 32);
+			h3 = *reinterpret_cast<const uint4 *>(a.umem + eff + 48);
+		}
+	}
 	const bool echo_tx = echo6 && ((h3.y >> 16) & 0xff) == 128 && !drop;
 	if (echo_tx && !(XDP_TAIL_DIAG & 1) &&
 	    !DBG_BAD(eff + 64 > ((a.usize + 15) & ~15ull), 10, eff)) {
