@@ -255,6 +255,39 @@ def pmc_traffic(n: int, size: int):
         return None
 
 
+def pmc_leg_traffic(pattern: str, frames: int):
+    """HBM bytes per launch of a secondary leg from the newest committed PMC
+    summary matching pattern (profiles/r<NN>_pmc_<workload>.json), scaled
+    to the leg's frame count when the summary was taken on fewer frames of
+    the same pool (the 1500 B leg lays its 2 M-frame pool down 8x): a dict
+    with the bytes, the ratio to the leg's algorithmic bytes is the
+    caller's; None when no summary exists."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
+    if not files:
+        return None
+    try:
+        with open(files[-1]) as f:
+            d = json.load(f)
+        b = float(d["hbm_bytes_per_launch"])
+        pf = int(d.get("frames") or frames)
+        return {"hbm_bytes_per_launch": b * frames / pf, "source": os.path.basename(files[-1]),
+                "pmc_frames": pf}
+    except Exception:
+        return None
+
+
+def attach_traffic(leg: dict, pattern: str, frames: int) -> dict:
+    t = pmc_leg_traffic(pattern, frames)
+    if t and leg.get("algorithmic_bytes_per_launch"):
+        t["over_algorithmic"] = round(t["hbm_bytes_per_launch"] /
+                                      leg["algorithmic_bytes_per_launch"], 3)
+        t["hbm_bytes_per_launch"] = int(t["hbm_bytes_per_launch"])
+    if t:
+        leg["traffic"] = t
+    return leg
+
+
 def kt_round(kt: dict) -> dict:
     """The launch's HIP-event times.  One RX launch is one kernel
     (xdp_rx_db_kernel): the library records its start/end pair, then two
@@ -846,6 +879,8 @@ def main():
                 "config2-geometry 16M x 1500B IPv4/UDP (a 2M-frame pool laid down 8x), V4 tuple",
                 lambda ds: len(ds) * (16 + 16 + 16 + 1) + int(ds["len"].astype(np.int64).sum()),
                 replicate=8)
+            attach_traffic(secondary["secondary_1500B"], "r[0-9][0-9]_pmc_1500_w128.json",
+                           16 << 20)
         if "imix" in legs:
             # config 3: IMIX with the 44 B network_tuple (429.3 B/frame)
             ctx3 = xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT, 0, xdpgpu.TUPLE_NET, args.window)
@@ -857,11 +892,15 @@ def main():
                 f"config3: {args.imix_frames} IMIX frames (64/570/1500 7:4:1, VLAN, IPv6), "
                 "network_tuple",
                 lambda ds: len(ds) * (16 + 16 + 44 + 1) + int(ds["len"].astype(np.int64).sum()))
+            attach_traffic(secondary["config3_imix"], "r[0-9][0-9]_pmc_config3_w128.json",
+                           args.imix_frames)
             ctx3.close()
             tctx3.close()
         if "nat64" in legs:
             secondary["config4_nat64"] = nat64_run(dev, stream, args.nat64_frames, steps2,
                                                    local)
+            attach_traffic(secondary["config4_nat64"], "r[0-9][0-9]_pmc_config4.json",
+                           args.nat64_frames)
         if "frags" in legs:
             secondary["multibuffer_9000B"] = frags_run(dev, stream, 1 << 16, steps2, local)
         if "echo" in legs:

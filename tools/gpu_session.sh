@@ -106,7 +106,7 @@ for s in "$@"; do
 	pmc)
 		# the pool's frame count and size for the summary (0: mixed sizes)
 		case $arg in
-		1500) geo="FRAMES=2097152 SIZE=1500" ;;
+		1500*) geo="FRAMES=2097152 SIZE=1500" ;;
 		imix*) geo="FRAMES=16777216 SIZE=0" ;;
 		nat64*) geo="FRAMES=16777216 SIZE=128" ;;
 		*) geo="FRAMES=16777216 SIZE=64" ;;
