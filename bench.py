@@ -289,13 +289,14 @@ def attach_traffic(leg: dict, pattern: str, frames: int) -> dict:
 
 
 def kt_round(kt: dict) -> dict:
-    """The launch's HIP-event times.  One RX launch is one kernel
-    (xdp_rx_db_kernel): the library records its start/end pair, then two
-    empty pairs (the record's exception and bulk fields, kept for the
-    struct's layout).  `launch_ms` (first to last event) is what
-    `roofline.achieved` divides by; it agrees with rocprofv3's average
-    duration of the kernel, `kernel_event_ms` (the first pair alone) reads
-    ~3 % lower."""
+    """The launch's HIP-event time: one RX launch is one kernel
+    (xdp_rx_db_kernel), and the library records one event before it and
+    one after it on the launch stream.  `launch_ms` is what
+    `roofline.achieved` divides by; the rocprofv3 --kernel-trace --stats
+    summary of the same command (profiles/r<NN>_kernel_stats_bench.csv)
+    gives the kernel's average duration to compare.  (Until round 4 the
+    library recorded two further empty pairs after the kernel, and the span
+    to the last of them read ~3 % above the kernel.)"""
     return {"launches": kt["launches"], "launch_ms": round(kt["total_ms"], 4),
             "kernel_event_ms": round(kt["fast_ms"], 4)}
 

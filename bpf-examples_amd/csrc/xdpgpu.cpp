@@ -612,16 +612,14 @@ int xdpgpu_kernel_times(xdpgpu_ctx *ctx, xdpgpu_ktimes *out)
 		return set_err(ctx, -EINVAL, "context made without XDPGPU_CFG_TIMING");
 	HIP_TRY(ctx, hipSetDevice(ctx->cfg.device));
 	for (uint32_t k = 0; k < ctx->tn; k++) {
+		/* one RX launch is one kernel: its two events (e[2], e[3] are
+		 * the struct's old exception and bulk pairs, never recorded) */
 		hipEvent_t *e = ctx->tev + 4 * k;
-		float t[3], all;
-		HIP_TRY(ctx, hipEventSynchronize(e[3]));
-		for (int j = 0; j < 3; j++)
-			HIP_TRY(ctx, hipEventElapsedTime(&t[j], e[j], e[j + 1]));
-		HIP_TRY(ctx, hipEventElapsedTime(&all, e[0], e[3]));
-		out->fast_ms += t[0];       /* the kernel; then two empty pairs */
-		out->exception_ms += t[1];
-		out->bulk_ms += t[2];
-		out->total_ms += all;
+		float t;
+		HIP_TRY(ctx, hipEventSynchronize(e[1]));
+		HIP_TRY(ctx, hipEventElapsedTime(&t, e[0], e[1]));
+		out->fast_ms += t;
+		out->total_ms += t;
 	}
 	out->launches = ctx->tn;
 	ctx->tn = 0;

@@ -323,10 +323,10 @@ int xdpgpu_ceiling_dev(struct xdpgpu_ctx *ctx, const void *d_umem,
 
 /* Diagnostic (XDPGPU_CFG_TIMING): RX launches recorded since the last call
  * and their summed durations from HIP events on the launch stream.  An RX
- * launch is one kernel (xdp_rx_db_kernel): fast_ms is its event pair;
- * exception_ms and bulk_ms stay in the struct for its layout and read ~0
- * (two empty event pairs after the kernel); total_ms spans all four
- * events.  Waits for the recorded work; resets the record.  At most
+ * launch is one kernel (xdp_rx_db_kernel) between two events: fast_ms and
+ * total_ms are that pair's span; exception_ms and bulk_ms stay in the
+ * struct for its layout and read 0.  Waits for the recorded work; resets
+ * the record.  At most
  * XDPGPU_TIMING_MAX launches are kept between calls (later ones are not
  * recorded). */
 #define XDPGPU_TIMING_MAX 1024
@@ -335,7 +335,7 @@ struct xdpgpu_ktimes {
 	double fast_ms;
 	double bulk_ms;
 	double exception_ms;
-	double total_ms;     /* first event to last event, summed per launch */
+	double total_ms;     /* the launches' event pairs, summed */
 };
 int xdpgpu_kernel_times(struct xdpgpu_ctx *ctx, struct xdpgpu_ktimes *out);
 
