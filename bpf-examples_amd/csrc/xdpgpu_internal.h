@@ -168,9 +168,9 @@ struct RxArgs {
 	uint64_t xcap;             /* entries of each deferral list        */
 };
 
-/* The RX launch (xdp_rx_db_kernel).  ev (nullable): four events, the
- * first before the kernel, the other three after it (the round-1 form timed
- * three kernels in these slots). */
+/* The RX launch (xdp_rx_db_kernel).  ev (nullable): four event slots, the
+ * first recorded before the kernel and the second after it (the other two
+ * are the round-1 form's, never recorded). */
 hipError_t launch_rx(const RxArgs &a, uint32_t max_blocks, hipStream_t stream, uint32_t tune,
 		     hipEvent_t *ev);
 /* multi-buffer packets read in place (after launch_frag_count): every

@@ -47,7 +47,7 @@ def main():
         if v == "ceil":
             ctxs[v] = xdpgpu.XdpGpu(0)
         else:
-            w, t = (int(x) for x in v.split(":"))
+            w, t = (int(x, 0) for x in v.split(":"))
             ctxs[v] = xdpgpu.XdpGpu(0, xdpgpu.CFG_DEFAULT, 0, args.fmt, w, tune=t)
     s = torch.cuda.Stream(dev)
     times = {v: [] for v in ctxs}
@@ -69,7 +69,7 @@ def main():
     for v in ctxs:
         if v == "ceil":
             continue
-        w, t = (int(x) for x in v.split(":"))
+        w, t = (int(x, 0) for x in v.split(":"))
         with xdpgpu.XdpGpu(0, xdpgpu.CFG_DEFAULT | xdpgpu.CFG_TIMING, 0, args.fmt, w,
                            tune=t) as tc:
             tc.process_dev(d_umem, umem.nbytes, d_desc, n, d_v, d_res, d_tup, s)
