@@ -1353,13 +1353,6 @@ __device__ __forceinline__ uint32_t u16_at(uint4 x, uint32_t o)
 #define XDP_TAIL_REC_NT 1
 #endif
 constexpr bool kTailRecNt = XDP_TAIL_REC_NT != 0;
-/* the record store write-through (build knob: 1 sc1, 2 sc0 sc1; 0
- * XDP_TAIL_REC_NT's policy), as inline asm: 2 M x 1500 B 0.579 / 0.579 vs
- * 0.586 / 0.585 ms, IMIX unchanged (profiles/r04_ab_rec_sc1.txt); not the
- * default until its parity run */
-#ifndef XDP_TAIL_REC_SC
-#define XDP_TAIL_REC_SC 0
-#endif
 /* the bulk pass's verdict bytes non-temporal (build knob): IMIX 2.260 vs
  * 2.252 ms plain, alternating processes (tools/gpu_ab_outnt.sh) */
 #ifndef XDP_TAIL_VERDICT_NT
@@ -1749,13 +1742,6 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 		rv.w = l4 | (cl << 16);
 		if constexpr (XDP_TAIL_DIAG & 4) {
 			/* diagnostic: no record store */
-		} else if constexpr (XDP_TAIL_REC_SC != 0) {
-			const v4u_t v = {rv.x, rv.y, rv.z, rv.w};
-			void *p = a.res + i;
-			if constexpr (XDP_TAIL_REC_SC == 1)
-				asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 2" :: "v"(p), "v"(v) : "memory");
-			else
-				asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 2" :: "v"(p), "v"(v) : "memory");
 		} else if constexpr (kTailRecNt)
 			st_nt16(a.res + i, rv);
 		else
