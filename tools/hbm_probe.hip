@@ -11,6 +11,8 @@
  *               (16 B descriptor + 64 B frame; 16 B + 16 B + 1 B stores)
  *   rx_mix_nt : the same with non-temporal loads and stores
  *   syn       : the SYN proxy leg's in-place shape (argument "syn")
+ *   imix      : config 3's two read patterns and the tile loop's head+outputs
+ *               shape (argument "imix")
  *
  * Build: hipcc --offload-arch=gfx950 -O3 -o tools/hbm_probe tools/hbm_probe.hip
  */
@@ -18,6 +20,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <vector>
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint4 ntl(const uint4 *p)
@@ -622,8 +625,171 @@ static int stride_main()
 	return 0;
 }
 
+/*
+ * IMIX's two read patterns (argument "imix"): a pool of 16 M frames of
+ * 64/570/1500 bytes (7:4:1, seeded order) packed at a 64-byte-rounded
+ * stride, as config 3's.  Set A is every frame's first 128 bytes (the
+ * lines the RX tile loop's windows read), set B the lines after them (the
+ * bulk pass's); each is read from a list of 64-byte line numbers, four
+ * lanes a line, U lines a lane-quad in flight.  "split" runs A on even
+ * workgroups and B on odd ones at once (the two passes overlapped).
+ */
+template <int U>
+__global__ __launch_bounds__(256) void k_lines(const uint4 *pool, const uint32_t *l0, size_t n0,
+					       const uint32_t *l1, size_t n1, int split, uint32_t *out)
+{
+	const uint32_t *l = l0;
+	size_t n = n0, b = blockIdx.x, g = gridDim.x;
+	if (split) {
+		g >>= 1;
+		if (b & 1) { l = l1; n = n1; }
+		b >>= 1;
+	}
+	const size_t q = b * 64 + (threadIdx.x >> 2), nq = g * 64;
+	const uint32_t sub = threadIdx.x & 3;
+	uint32_t x = 0;
+	size_t i = q;
+	for (; i + (U - 1) * nq < n; i += U * nq) {
+		uint4 v[U];
+#pragma unroll
+		for (int u = 0; u < U; u++)
+			v[u] = pool[(size_t)l[i + u * nq] * 4 + sub];
+#pragma unroll
+		for (int u = 0; u < U; u++)
+			x ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+	}
+	for (; i < n; i += nq) {
+		uint4 v = pool[(size_t)l[i] * 4 + sub];
+		x ^= v.x ^ v.y ^ v.z ^ v.w;
+	}
+	if (x == 0x12345678u)
+		out[0] = x;
+}
+
+/* set A as the tile loop moves it: a lane quad per frame reads the frame's
+ * first two lines (a 64-byte frame's second is its neighbour's first) and
+ * writes the frame's outputs, 16 B result + 44 B tuple + 1 B verdict, into
+ * packed per-frame arrays */
+__global__ __launch_bounds__(256) void k_headw(const uint4 *pool, const uint32_t *first,
+					       size_t nframes, uint4 *res, uint32_t *tup,
+					       uint8_t *verd, int write)
+{
+	const size_t nq = (size_t)gridDim.x * 64;
+	const uint32_t sub = threadIdx.x & 3;
+	for (size_t f = blockIdx.x * 64ull + (threadIdx.x >> 2); f < nframes; f += 2 * nq) {
+		const size_t f2 = f + nq < nframes ? f + nq : f;
+		const uint4 *p = pool + (size_t)first[f] * 4, *p2 = pool + (size_t)first[f2] * 4;
+		uint4 v0 = p[sub], v1 = p[4 + sub], v2 = p2[sub], v3 = p2[4 + sub];
+		uint32_t x = v0.x ^ v0.y ^ v0.z ^ v0.w ^ v1.x ^ v1.y ^ v1.z ^ v1.w;
+		uint32_t y = v2.x ^ v2.y ^ v2.z ^ v2.w ^ v3.x ^ v3.y ^ v3.z ^ v3.w;
+		if (!write) {
+			if ((x ^ y) == 0x12345678u)
+				verd[0] = 1;
+			continue;
+		}
+		for (int k = 0; k < 2; k++) {
+			const size_t g = k ? f2 : f;
+			const uint32_t z = k ? y : x;
+			if (sub == 0) {
+				res[g] = make_uint4(z, z, z, z);
+				verd[g] = (uint8_t)z;
+			}
+			for (uint32_t d = sub; d < 11; d += 4)
+				tup[g * 11 + d] = z + d;
+		}
+	}
+}
+
+static struct {
+	uint4 *pool, *res;
+	uint32_t *a, *b, *all, *first, *tup;
+	uint8_t *verd;
+	size_t na, nb, nall, n16, frames;
+} IM;
+static int headw_write;
+static void run_headw(void *) { hipLaunchKernelGGL(k_headw, dim3(C.grid), dim3(256), 0, 0, IM.pool, IM.first, IM.frames, IM.res, IM.tup, IM.verd, headw_write); }
+template <int U>
+static void run_la(void *) { hipLaunchKernelGGL(k_lines<U>, dim3(C.grid), dim3(256), 0, 0, IM.pool, IM.a, IM.na, IM.a, 0, 0, C.out); }
+template <int U>
+static void run_lb(void *) { hipLaunchKernelGGL(k_lines<U>, dim3(C.grid), dim3(256), 0, 0, IM.pool, IM.b, IM.nb, IM.b, 0, 0, C.out); }
+template <int U>
+static void run_lall(void *) { hipLaunchKernelGGL(k_lines<U>, dim3(C.grid), dim3(256), 0, 0, IM.pool, IM.all, IM.nall, IM.all, 0, 0, C.out); }
+template <int U>
+static void run_lsplit(void *) { hipLaunchKernelGGL(k_lines<U>, dim3(C.grid), dim3(256), 0, 0, IM.pool, IM.a, IM.na, IM.b, IM.nb, 1, C.out); }
+static void run_pool(void *) { hipLaunchKernelGGL(k_read<false>, dim3(C.grid), dim3(256), 0, 0, IM.pool, IM.n16, C.out); }
+
+static int imix_main()
+{
+	const size_t frames = 16ull << 20;
+	uint64_t s = 0x5EED0003ull, lines = 0;
+	std::vector<uint32_t> a, b, all, first;
+	first.reserve(frames);
+	a.reserve(frames * 3 / 2);
+	b.reserve(frames * 9 / 2);
+	for (size_t f = 0; f < frames; f++) {
+		s ^= s << 13; s ^= s >> 7; s ^= s << 17;
+		const uint32_t r = (uint32_t)(s >> 32) % 12;
+		const uint32_t len = r < 7 ? 64 : r < 11 ? 570 : 1500;
+		const uint32_t nl = (len + 63) / 64;
+		first.push_back((uint32_t)lines);
+		for (uint32_t k = 0; k < nl; k++) {
+			(k < 2 ? a : b).push_back((uint32_t)(lines + k));
+			all.push_back((uint32_t)(lines + k));
+		}
+		lines += nl;
+	}
+	IM.na = a.size(); IM.nb = b.size(); IM.nall = all.size();
+	IM.n16 = lines * 4;
+	CK(hipMalloc(&IM.pool, lines * 64));
+	CK(hipMemset(IM.pool, 1, lines * 64));
+	CK(hipMalloc(&IM.a, IM.na * 4));
+	CK(hipMalloc(&IM.b, IM.nb * 4));
+	CK(hipMalloc(&IM.all, IM.nall * 4));
+	CK(hipMemcpy(IM.a, a.data(), IM.na * 4, hipMemcpyHostToDevice));
+	CK(hipMemcpy(IM.b, b.data(), IM.nb * 4, hipMemcpyHostToDevice));
+	CK(hipMemcpy(IM.all, all.data(), IM.nall * 4, hipMemcpyHostToDevice));
+	IM.frames = frames;
+	CK(hipMalloc(&IM.first, frames * 4));
+	CK(hipMemcpy(IM.first, first.data(), frames * 4, hipMemcpyHostToDevice));
+	CK(hipMalloc(&IM.res, frames * 16));
+	CK(hipMalloc(&IM.tup, frames * 44));
+	CK(hipMalloc(&IM.verd, frames));
+	CK(hipMalloc(&C.out, 64));
+	const double ga = IM.na * 64 / 1e9, gbb = IM.nb * 64 / 1e9, gp = lines * 64 / 1e9;
+	printf("imix pool %.3f GB (%zu lines), A %.3f GB (%.2f lines/frame), B %.3f GB\n",
+	       gp, (size_t)lines, ga, (double)IM.na / frames, gbb);
+	for (int rep = 0; rep < 2; rep++)
+		for (int grid : {2048, 8192}) {
+			C.grid = grid;
+			float t;
+			t = time_it(run_pool, 0, 10);
+			printf("grid %5d pool_seq  %.4f ms %7.1f GB/s\n", grid, t, gp / t * 1e3);
+			t = time_it(run_lall<4>, 0, 10);
+			printf("grid %5d list_all  %.4f ms %7.1f GB/s\n", grid, t, gp / t * 1e3);
+			t = time_it(run_la<2>, 0, 10);
+			printf("grid %5d A u2      %.4f ms %7.1f GB/s\n", grid, t, ga / t * 1e3);
+			t = time_it(run_la<4>, 0, 10);
+			printf("grid %5d A u4      %.4f ms %7.1f GB/s\n", grid, t, ga / t * 1e3);
+			t = time_it(run_lb<4>, 0, 10);
+			printf("grid %5d B u4      %.4f ms %7.1f GB/s\n", grid, t, gbb / t * 1e3);
+			t = time_it(run_lsplit<4>, 0, 10);
+			printf("grid %5d A|B split %.4f ms %7.1f GB/s\n", grid, t, gp / t * 1e3);
+			const double gh = frames * 128 / 1e9, gw = frames * 61 / 1e9;
+			headw_write = 0;
+			t = time_it(run_headw, 0, 10);
+			printf("grid %5d head      %.4f ms %7.1f GB/s (128 B a frame)\n", grid, t, gh / t * 1e3);
+			headw_write = 1;
+			t = time_it(run_headw, 0, 10);
+			printf("grid %5d head+out  %.4f ms %7.1f GB/s (128 B read, 61 B written)\n", grid, t,
+			       (gh + gw) / t * 1e3);
+		}
+	return 0;
+}
+
 int main(int argc, char **argv)
 {
+	if (argc > 1 && !strcmp(argv[1], "imix"))
+		return imix_main();
 	if (argc > 1 && !strcmp(argv[1], "bulk"))
 		return bulk_main();
 	if (argc > 1 && !strcmp(argv[1], "stride"))
