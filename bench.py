@@ -632,7 +632,7 @@ def pcie_ceiling(dev, mib: int = 256, reps: int = 10) -> dict:
 
 
 def e2e_run(local, umem, descs, expect, B: int, nbatches: int, chunk: int, window: int,
-            ceil: dict) -> dict:
+            ceil: dict, flags: int = xdpgpu.CFG_DEFAULT) -> dict:
     """The host path as an RX loop drives it (xdpgpu_submit / xdpgpu_wait,
     two batches in flight): each batch's frames copied from the pinned host
     UMEM into the slot's device mirror (rows of chunks when chunk is given:
@@ -640,10 +640,11 @@ def e2e_run(local, umem, descs, expect, B: int, nbatches: int, chunk: int, windo
     records and tuples back into page-locked per-slot buffers.  Batches of B
     consecutive descriptors cycle over the pool.  One pass checks every
     batch's verdicts, a second is timed; the PCIe bytes per frame come from
-    xdpgpu_host_stats over the timed pass."""
+    xdpgpu_host_stats over the timed pass.  flags: XDPGPU_CFG_UMEM_GATHER
+    moves a chunked UMEM's frames by the gather kernel instead."""
     n = len(descs)
     per = max(1, n // B)
-    h = xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT, 0, xdpgpu.TUPLE_V4, window, max_batch=B)
+    h = xdpgpu.XdpGpu(local, flags, 0, xdpgpu.TUPLE_V4, window, max_batch=B)
     h.register_umem(umem, chunk)
     # the descriptors as the RX ring holds them (page-locked), and
     # page-locked per-slot outputs, as an RX loop keeps them
@@ -689,6 +690,8 @@ def e2e_run(local, umem, descs, expect, B: int, nbatches: int, chunk: int, windo
     d2h_gbps = d2h / te / 1e9
     return {"mpps": round(fr / te / 1e6, 1), "frames": fr, "batch": B, "batches": nbatches,
             "chunk": chunk, "pinned_buffers": True,
+            "umem_gather": bool(flags & xdpgpu.CFG_UMEM_GATHER) and
+            s1["umem_gathers"] > s0["umem_gathers"],
             "h2d_bytes_per_frame": round(h2d / fr, 1),
             "umem_copies_per_batch": round((s1["umem_copies"] - s0["umem_copies"]) /
                                            max(1, s1["batches"] - s0["batches"]), 1),
@@ -912,6 +915,7 @@ def main():
 
     e2e = None
     e2e_chunked = None
+    e2e_gather = None
     if not args.no_e2e and rank == 0 and world == 1:
         ceil = pcie_ceiling(dev)
         # host path, the packed pool: pinned UMEM, H2D span + descs, kernel,
@@ -932,6 +936,12 @@ def main():
                                        f"at headroom 256 ({cu.nbytes >> 20} MiB host UMEM, "
                                        "registered with chunk_size 4096), batches of half "
                                        "the UMEM cycling over it")
+            # the same with XDPGPU_CFG_UMEM_GATHER: a kernel reads each
+            # frame's bytes through the UMEM's GPU mapping
+            e2e_gather = e2e_run(local, cu, cd, ce, nc // 2, args.e2e_batches, 4096,
+                                 args.window, ceil,
+                                 xdpgpu.CFG_DEFAULT | xdpgpu.CFG_UMEM_GATHER)
+            e2e_gather["workload"] = e2e_chunked["workload"] + ", XDPGPU_CFG_UMEM_GATHER"
             del cu, cd, ce
 
     cpu = None
@@ -981,6 +991,8 @@ def main():
             line["e2e_host_path"] = e2e
         if e2e_chunked:
             line["e2e_host_path_chunked"] = e2e_chunked
+        if e2e_gather:
+            line["e2e_host_path_chunked_gather"] = e2e_gather
         print(json.dumps(line), flush=True)
     ctx.close()
     tctx.close()

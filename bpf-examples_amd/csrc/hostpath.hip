@@ -1,6 +1,7 @@
 // SPDX-License-Identifier: GPL-2.0
 /*
- * hostpath.hip - the host path's write-back of ICMPv6 echo replies.
+ * hostpath.hip - the host path's write-back of ICMPv6 echo replies, and
+ * its opt-in gather of a chunked UMEM's frames (umem_gather_kernel below).
  *
  * xdpgpu_submit runs the RX kernels on the slot's device mirror of the
  * host UMEM.  The echo responder (process_packet, af_xdp_user.c:968-1040)
@@ -11,8 +12,8 @@
  * batch whose verdict is TX this kernel copies bytes [0, min(len, 64)) of
  * its frame, and nothing else, as compact 80-byte records (EchoRec) that
  * xdpgpu_wait scatters on the host.  (Until round 4 the kernel could also
- * write them straight into the mapped pinned UMEM; no kernel touches host
- * memory any more)
+ * write them straight into the mapped pinned UMEM; no kernel writes host
+ * memory any more, and only the opt-in gather reads it)
  * Multi-buffer packets: each fragment of a TX packet has verdict TX, and
  * packet byte p < 64 lies at offset <= p of its fragment, so the fragments'
  * first 64 bytes cover the rewrite.
@@ -74,7 +75,71 @@ __global__ __launch_bounds__(kEchoBlock) void echo_writeback_kernel(EchoArgs a)
 	}
 }
 
+/*
+ * UMEM gather (XDPGPU_CFG_UMEM_GATHER): the bytes each
+ * descriptor names, [eff, eff + len), and udp_csum's over-read byte
+ * eff + len (lib_checksum.h:175-176) where it can lie past the frame,
+ * copied from the host UMEM's GPU mapping into the mirror, in the 16-byte
+ * pieces that cover them.  The over-read byte: a checksum range starts at
+ * an even offset (14 + 4 * tags, + the IPv4 header's 4 * ihl or IPv6's 40
+ * + 8k) and the parse bounds its end by len, so it ends at len only with
+ * len odd; a multi-buffer packet's byte follows its last fragment, whose
+ * own length says nothing, so there every fragment takes it (over_all).
+ * The caller (copy_batch) uses this for chunked UMEMs only, where every
+ * piece lies in the frame's chunk: [eff & ~15, round_up(eff + len + 1, 16))
+ * inside [chunk, chunk + chunk_size), as batch_rows checked.  Plain loads,
+ * nothing written to host memory; a piece the UMEM's end cuts goes byte by
+ * byte.  8 lanes a frame, 8 frames a wave, each lane one piece in flight.
+ * With hdesc the descriptors come from the caller's page-locked array (read
+ * here, through its GPU mapping) and lane 0 of each frame's group writes
+ * the device copy the RX kernel reads.
+ */
+constexpr int kGatherLanes = 8;
+__global__ __launch_bounds__(256) void umem_gather_kernel(GatherArgs a)
+{
+	const uint32_t sub = threadIdx.x & (kGatherLanes - 1);
+	const uint64_t step = (uint64_t)gridDim.x * (256 / kGatherLanes);
+	for (uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / kGatherLanes; i < a.n;
+	     i += step) {
+		xdpgpu_desc d;
+		if (a.hdesc) {
+			d = a.hdesc[i];
+			if (sub == 0)
+				a.desc[i] = d;
+		} else {
+			d = a.desc[i];
+		}
+		const uint64_t eff = d.addr;
+		/* descriptors outside the UMEM (and offset-field addresses, which
+		 * batch_rows never hands here) name no bytes */
+		if (eff >= a.usize || (uint64_t)d.len > a.usize - eff)
+			continue;
+		uint64_t hi = eff + d.len + ((a.over_all | d.len) & 1);
+		if (hi > a.usize)
+			hi = a.usize;
+		for (uint64_t p = (eff & ~15ull) + 16 * sub; p < hi; p += 16 * kGatherLanes) {
+			if (p + 16 <= a.usize) {
+				const uint4 v = *reinterpret_cast<const uint4 *>(a.src + p);
+				*reinterpret_cast<uint4 *>(a.mirror + p) = v;
+			} else {
+				for (uint64_t b = p; b < a.usize; b++)
+					a.mirror[b] = a.src[b];
+			}
+		}
+	}
+}
+
 } // namespace
+
+hipError_t launch_umem_gather(const GatherArgs &a, hipStream_t stream)
+{
+	if (!a.n)
+		return hipSuccess;
+	const uint64_t want = ((uint64_t)a.n * kGatherLanes + 255) / 256;
+	const uint32_t blocks = (uint32_t)(want < 4096 ? want : 4096);
+	hipLaunchKernelGGL(umem_gather_kernel, dim3(blocks), dim3(256), 0, stream, a);
+	return hipGetLastError();
+}
 
 hipError_t launch_echo_writeback(const EchoArgs &a, hipStream_t stream)
 {

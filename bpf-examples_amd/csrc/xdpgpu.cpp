@@ -93,6 +93,9 @@ struct xdpgpu_ctx {
 	 * one, else 0: the host path then copies rows of chunks */
 	uint32_t chunk = 0;
 	uint32_t chunk_shift = 0;
+	/* XDPGPU_CFG_UMEM_GATHER on a chunked UMEM: its GPU mapping (the
+	 * gather kernel's source), else null */
+	const uint8_t *d_hview = nullptr;
 	/* host-path copy accounting (xdpgpu_host_stats) */
 	struct xdpgpu_host_stats hstats{};
 	/* XDPGPU_CFG_TIMING: 4 events per recorded launch */
@@ -358,6 +361,7 @@ static void release_umem(xdpgpu_ctx *ctx)
 		(void)hipHostUnregister(ctx->h_umem);
 	ctx->pinned = false;
 	ctx->h_umem = nullptr;
+	ctx->d_hview = nullptr;
 	ctx->umem_size = 0;
 }
 
@@ -403,15 +407,25 @@ int xdpgpu_register_umem(xdpgpu_ctx *ctx, void *base, uint64_t size,
 			ctx->chunk_shift++;
 	}
 	/* pin the caller's UMEM for the copy engines (pageable memory still
-	 * works, only slower).  No kernel reads or writes it: every batch's
-	 * frames are copied into the slot's device mirror and the echo
-	 * replies come back as compact records (the host
-	 * memory faults of rounds 2-3 all followed kernels that dereferenced
-	 * this UMEM through its GPU mapping) */
+	 * works, only slower).  No kernel writes it: every batch's frames go
+	 * into the slot's device mirror and the echo replies come back as
+	 * compact records (the host memory faults of rounds
+	 * 2-3 all followed kernels that read and wrote this UMEM through its
+	 * GPU mapping, with LDS-DMA and non-temporal loads).  Only the
+	 * opt-in gather (XDPGPU_CFG_UMEM_GATHER, chunked UMEMs) reads it
+	 * there, with plain loads. */
 	if (hipHostRegister(base, size, hipHostRegisterDefault) == hipSuccess)
 		ctx->pinned = true;
 	else
 		(void)hipGetLastError();
+	if ((ctx->cfg.flags & XDPGPU_CFG_UMEM_GATHER) && ctx->chunk) {
+		/* memory pinned here or by the caller (xdpgpu_host_alloc) */
+		void *p = nullptr;
+		if (hipHostGetDevicePointer(&p, base, 0) == hipSuccess && p)
+			ctx->d_hview = (const uint8_t *)p;
+		else
+			(void)hipGetLastError();
+	}
 	/* slot 0's mirror now, so that a size the device cannot hold fails
 	 * here; slot 1's on its first batch */
 	const int rc = ensure_mirror(ctx, ctx->slot[0]);
@@ -1228,6 +1242,78 @@ static bool batch_rows(const xdpgpu_ctx *ctx, const xdpgpu_desc *descs, uint32_t
 	}
 }
 
+/* XDPGPU_CFG_UMEM_GATHER: whether the gather kernel can take the batch
+ * (every frame and its over-read byte inside its own chunk, no offset
+ * field: umem_gather_kernel's pieces then stay in the frames' chunks).
+ * Sets used and the bytes the gather will read. */
+static bool gather_holds(const xdpgpu_ctx *ctx, const xdpgpu_desc *descs, uint32_t n,
+			 uint64_t &used, uint64_t &bytes)
+{
+	/* one pass (the RX thread's own time between a slot's wait and its
+	 * next gather): the bytes umem_gather_kernel's pieces move, too */
+	used = 0;
+	bytes = 0;
+	const uint64_t mask = ctx->chunk - 1, us = ctx->umem_size;
+	const uint64_t odd = (ctx->cfg.flags & XDPGPU_CFG_FRAGS) ? 1u : 0u;
+	for (uint32_t i = 0; i < n; i++) {
+		const uint64_t eff = descs[i].addr, len = descs[i].len;
+		if (eff >> 48)
+			return false;
+		if (eff >= us)
+			continue;
+		if ((eff & mask) + len + 1 > ctx->chunk)
+			return false;
+		used += len;
+		if (len > us - eff)
+			continue;
+		const uint64_t hi = std::min<uint64_t>(eff + len + ((odd | len) & 1), us);
+		bytes += std::min<uint64_t>((hi + 15) & ~15ull, us) - (eff & ~15ull);
+	}
+	return true;
+}
+
+/* The device view of a page-locked host array (hipHostMalloc'd or
+ * registered), else null (pageable memory) */
+static const void *host_view(const void *p)
+{
+	hipPointerAttribute_t at;
+	memset(&at, 0, sizeof(at));
+	if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+		(void)hipGetLastError();
+		return nullptr;
+	}
+	return at.type == hipMemoryTypeHost ? at.devicePointer : nullptr;
+}
+
+/* XDPGPU_CFG_UMEM_GATHER: the gather kernel moves the batch's frame bytes
+ * into the slot's mirror.  hdesc: the descriptors' device view when the
+ * caller's array is page-locked; the kernel then also writes their device
+ * copy (s.d_desc), so that no descriptor copy waits on the copy engine
+ * behind the other slot's output copies (rocprof timeline,
+ * profiles/r05_gather: one engine runs every copy in order, and a
+ * descriptor upload queued behind the previous batch's results kept the
+ * next gather from starting).  Otherwise s.d_desc was uploaded first.
+ * (The two slots' gathers run at once; one stream for both, the gathers
+ * back to back, held each slot's kernels behind the other slot's gather:
+ * 226 vs 239 M frames/s.) */
+static int gather_batch(xdpgpu_ctx *ctx, Slot &s, uint32_t n, const xdpgpu_desc *hdesc,
+			uint64_t bytes)
+{
+	GatherArgs g;
+	g.src = ctx->d_hview;
+	g.mirror = s.d_mirror;
+	g.usize = ctx->umem_size;
+	g.desc = s.d_desc;
+	g.hdesc = hdesc;
+	g.n = n;
+	g.over_all = (ctx->cfg.flags & XDPGPU_CFG_FRAGS) ? 1u : 0u;
+	HIP_TRY(ctx, launch_umem_gather(g, s.stream));
+	ctx->hstats.umem_h2d_bytes += bytes;
+	ctx->hstats.umem_copies++;
+	ctx->hstats.umem_gathers++;
+	return 0;
+}
+
 /* Copy a batch's frames into the slot's mirror: rows of chunks where they
  * pay (batch_rows), else spans (batch_runs).  Sets used (the bytes the
  * descriptors name) and adds the copy's bytes to the host stats. */
@@ -1316,13 +1402,17 @@ int xdpgpu_submit(xdpgpu_ctx *ctx, uint32_t slot, const xdpgpu_desc *descs,
 
 	/* the frames go to this slot's own mirror: a batch in flight on the
 	 * other slot never sees them, whatever the two batches' addresses */
-	uint64_t used = 0;
-	rc = copy_batch(ctx, s, descs, n, used);
+	uint64_t used = 0, gbytes = 0;
+	const bool gather = ctx->d_hview && gather_holds(ctx, descs, n, used, gbytes);
+	const xdpgpu_desc *hdesc =
+		gather ? (const xdpgpu_desc *)host_view(descs) : nullptr;
+	if (!hdesc)
+		HIP_TRY(ctx, hipMemcpyAsync(s.d_desc, descs, (size_t)n * sizeof(*descs),
+					    hipMemcpyHostToDevice, s.stream));
+	rc = gather ? gather_batch(ctx, s, n, hdesc, gbytes) : copy_batch(ctx, s, descs, n, used);
 	if (rc)
 		return rc;
 	const bool echo = ctx->cfg.flags & XDPGPU_CFG_ICMP6_ECHO;
-	HIP_TRY(ctx, hipMemcpyAsync(s.d_desc, descs, (size_t)n * sizeof(*descs),
-				    hipMemcpyHostToDevice, s.stream));
 	uint8_t *d_tup = (tuples && ctx->cfg.tuple_fmt) ? s.d_tup : nullptr;
 	/* the mean frame length picks the window (xdpgpu.h: 128 bytes when
 	 * the frames average at least 128) */

@@ -224,6 +224,23 @@ struct EchoArgs {
 };
 hipError_t launch_echo_writeback(const EchoArgs &a, hipStream_t stream);
 
+/* XDPGPU_CFG_UMEM_GATHER: a batch's frame bytes from the registered host
+ * UMEM (its GPU mapping, read only) into the slot's mirror at the same
+ * offsets, 16-byte pieces (hostpath.hip) */
+struct GatherArgs {
+	const uint8_t *src;        /* the host UMEM's device view            */
+	uint8_t *mirror;
+	uint64_t usize;
+	xdpgpu_desc *desc;         /* device copy of the batch's descriptors */
+	const xdpgpu_desc *hdesc;  /* non-null: the caller's page-locked array
+				    * (device view), read here and copied into
+				    * desc for the kernels after */
+	uint32_t n;
+	uint32_t over_all;         /* 1: every frame's byte len (multi-buffer
+				    * packets); 0: odd lengths only          */
+};
+hipError_t launch_umem_gather(const GatherArgs &a, hipStream_t stream);
+
 /* jhash (include/jhash.h:25-52) mixing steps, for the device kernels */
 __device__ __forceinline__ uint32_t rol32(uint32_t w, uint32_t s)
 {

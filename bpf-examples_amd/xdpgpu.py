@@ -42,6 +42,7 @@ CFG_ICMP6_ECHO = 0x2
 CFG_TIMING = 0x8
 CFG_STATS = 0x4
 CFG_FRAGS = 0x10      # multi-buffer packets (include/xdpgpu.h)
+CFG_UMEM_GATHER = 0x20   # host path: chunked UMEMs gathered by a kernel
 PKT_CONTD = 0x1       # xdp_desc.options: the packet continues
 CFG_DEFAULT = CFG_VERIFY_CSUM | CFG_STATS
 
@@ -108,7 +109,8 @@ class HostStats(C.Structure):
     """struct xdpgpu_host_stats"""
     _fields_ = [("batches", C.c_uint64), ("frames", C.c_uint64),
                 ("umem_h2d_bytes", C.c_uint64), ("umem_copies", C.c_uint64),
-                ("desc_h2d_bytes", C.c_uint64), ("out_d2h_bytes", C.c_uint64)]
+                ("desc_h2d_bytes", C.c_uint64), ("out_d2h_bytes", C.c_uint64),
+                ("umem_gathers", C.c_uint64)]
 
 
 class KTimes(C.Structure):

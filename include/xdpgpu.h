@@ -126,6 +126,15 @@ struct xdpgpu_network_tuple {
  * every descriptor is a frame, as process_packet does. */
 #define XDPGPU_CFG_FRAGS       0x10
 #define XDPGPU_PKT_CONTD       0x1 /* xdp_desc.options: the packet continues  */
+/* Host path on a chunked UMEM (register_umem's chunk_size): a batch's
+ * frame bytes reach the slot's device mirror through a gather kernel that
+ * reads the registered UMEM through its GPU mapping (plain 16-byte loads,
+ * read only, the frames' own bytes), instead of the copy engine's pitched
+ * copies of one window per chunk.  About twice the rows per second for
+ * small frames in 4 KiB chunks.  Ignored (the copies
+ * are used) for a UMEM without chunk_size, one the GPU cannot map, or a
+ * batch the rows do not hold. */
+#define XDPGPU_CFG_UMEM_GATHER 0x20
 #define XDPGPU_CFG_DEFAULT     (XDPGPU_CFG_VERIFY_CSUM | XDPGPU_CFG_STATS)
 
 struct xdpgpu_cfg {
@@ -205,8 +214,11 @@ int xdpgpu_process(struct xdpgpu_ctx *ctx, const struct xdpgpu_desc *descs,
 		   void *tuples);
 
 /* Asynchronous form of xdpgpu_process on one of two in-flight slots
- * (double buffering of the RX batches).  Output buffers must stay valid
- * until xdpgpu_wait(ctx, slot) returns, and the batch's frames must not be
+ * (double buffering of the RX batches).  The descriptor array and the
+ * output buffers must stay valid until xdpgpu_wait(ctx, slot) returns
+ * (page-locked ones are read and written by the copies and, with
+ * XDPGPU_CFG_UMEM_GATHER, the gather kernel after xdpgpu_submit has
+ * returned), and the batch's frames must not be
  * handed back to the kernel (fill or TX ring) before it returns.  The two
  * slots are independent: their batches may name the same UMEM frames
  * (each slot reads its own device mirror), and each writes back only its
@@ -228,7 +240,9 @@ void xdpgpu_host_free(void *p);
  * output bytes (verdict, record, tuple) back.  With a chunk size given to
  * xdpgpu_register_umem (aligned mode), a batch moves one window of each
  * chunk it names, the same offsets in every chunk (rows of a pitched
- * copy); otherwise spans of nearby frames. */
+ * copy); otherwise spans of nearby frames.  With XDPGPU_CFG_UMEM_GATHER the
+ * batches a gather kernel moved count in umem_gathers (their bytes, the
+ * 16-byte pieces read, in umem_h2d_bytes; umem_copies counts one a batch). */
 struct xdpgpu_host_stats {
 	uint64_t batches;
 	uint64_t frames;
@@ -236,13 +250,14 @@ struct xdpgpu_host_stats {
 	uint64_t umem_copies;
 	uint64_t desc_h2d_bytes;
 	uint64_t out_d2h_bytes;
+	uint64_t umem_gathers;
 };
 int xdpgpu_host_stats(struct xdpgpu_ctx *ctx, struct xdpgpu_host_stats *out);
 
 /* Device-resident form: every pointer is device memory (d_umem is written
  * only for ICMPv6 echo rewrites; a d_umem in host memory, pinned or not, is
  * refused with -EINVAL: no kernel of the library dereferences host
- * memory).  stream is a hipStream_t (NULL: the
+ * memory but XDPGPU_CFG_UMEM_GATHER's reads).  stream is a hipStream_t (NULL: the
  * context's stream).  Returns after the launch is enqueued, also with
  * XDPGPU_CFG_FRAGS (no host round trip).  d_umem must be readable up to
  * round_up(umem_size, 16) (the kernel loads 16-byte aligned chunks and

@@ -352,13 +352,30 @@ def check_ring(got, want, host, ou, st, ost):
     assert [st["verdict"][x] for x in xdpgpu.VERDICT_NAMES] == ost["verdict"]
 
 
+def gather_bytes(descs, batches, usize, over_all=False):
+    """The 16-byte pieces umem_gather_kernel reads for the batches."""
+    tot = 0
+    for b in batches:
+        a = descs["addr"][b].astype(np.int64)
+        ln = descs["len"][b].astype(np.int64)
+        ok = (a < usize) & (ln <= usize - a)
+        hi = np.minimum(a + ln + (1 if over_all else (ln & 1)), usize)
+        tot += int((np.minimum((hi + 15) & ~15, usize) - (a & ~15))[ok].sum())
+    return tot
+
+
+@pytest.mark.parametrize("gather,pinned", [(False, True), (True, True), (True, False)],
+                         ids=["rows", "gather", "gather_pageable_descs"])
 @pytest.mark.parametrize("kind,size,ppm", [(xdpgpu.POOL_UDP4, 64, 300000),
                                            (xdpgpu.POOL_IMIX, 64, 200000)],
                          ids=["udp64", "imix"])
-def test_ring_chunked_umem(kind, size, ppm):
+def test_ring_chunked_umem(kind, size, ppm, gather, pinned):
     """The reference's UMEM geometry (4 KiB chunks, each frame at its
     chunk's headroom) registered with its chunk size: the host path copies
-    one window of each chunk (rows of a pitched copy).  Recycled,
+    one window of each chunk (rows of a pitched copy), or with
+    XDPGPU_CFG_UMEM_GATHER a kernel gathers each frame's bytes (reading
+    page-locked descriptor arrays through their GPU mapping, pageable ones
+    after their copy).  Recycled,
     wrapping and strided batches (the scattered path merges chunk runs),
     echo replies written back: outputs and the whole host UMEM equal the
     oracle's."""
@@ -368,13 +385,20 @@ def test_ring_chunked_umem(kind, size, ppm):
     batches = ring_batches(nframes, 12, 1024, 72)
     host = umem.copy()
     hs = {}
-    got, st = run_ring(host, descs, batches, ECHO, 0, window=0, chunk=CHUNK, host_stats=hs)
+    flags = ECHO | (xdpgpu.CFG_UMEM_GATHER if gather else 0)
+    got, st = run_ring(host, descs, batches, flags, 0, window=0, chunk=CHUNK, host_stats=hs,
+                       pinned=pinned)
     ou = umem.copy()
     want, ost = oracle_ring(ou, descs, batches, ECHO)
     check_ring(got, want, host, ou, st, ost)
     ntx = sum(int((w[0] == xdpgpu.TX).sum()) for w in want)
     assert ntx > 100
     assert hs["frames"] == sum(len(b) for b in batches)
+    if gather:
+        assert hs["umem_gathers"] == len(batches), hs
+        assert hs["umem_h2d_bytes"] == gather_bytes(descs, batches, umem.size), hs
+        return
+    assert hs["umem_gathers"] == 0, hs
     # at most one window of every chunk per batch (random recycled batches
     # merge their chunk runs, copying the rows between), always below the
     # span copy's whole chunks
@@ -384,33 +408,102 @@ def test_ring_chunked_umem(kind, size, ppm):
     assert hs["umem_h2d_bytes"] < len(batches) * nframes * CHUNK // 2, hs
 
 
-def test_chunked_consecutive_bytes():
+@pytest.mark.parametrize("gather", [False, True], ids=["rows", "gather"])
+def test_chunked_consecutive_bytes(gather):
     """Consecutive 64 B frames in 4 KiB chunks: exactly one row of the
     batch's window (its longest frame and udp_csum's over-read byte) per
-    chunk, one copy per batch; outputs equal the oracle's."""
+    chunk, one copy per batch, or (gather) each frame's own 64 bytes;
+    outputs equal the oracle's."""
     nframes, B = 4096, 1024
     umem, descs, _ = chunked_pool(nframes, xdpgpu.POOL_UDP4, 64, 73)
     batches = [np.arange(k, k + B) for k in range(0, nframes, B)]
     host = umem.copy()
     hs = {}
-    got, st = run_ring(host, descs, batches, 0x5, 0, fmt=xdpgpu.TUPLE_V4, window=0,
+    flags = 0x5 | (xdpgpu.CFG_UMEM_GATHER if gather else 0)
+    got, st = run_ring(host, descs, batches, flags, 0, fmt=xdpgpu.TUPLE_V4, window=0,
                        chunk=CHUNK, host_stats=hs)
     ou = umem.copy()
     want, ost = oracle_ring(ou, descs, batches, 0x5, fmt=xdpgpu.TUPLE_V4)
     check_ring(got, want, host, ou, st, ost)
+    assert hs["desc_h2d_bytes"] == nframes * 16
+    if gather:
+        assert hs["umem_h2d_bytes"] == gather_bytes(descs, batches, umem.size), hs
+        assert hs["umem_h2d_bytes"] <= nframes * 64, hs
+        assert hs["umem_gathers"] == hs["umem_copies"] == len(batches), hs
+        return
     lens = descs["len"].astype(np.int64)
     # every frame sits at the chunk's headroom: a batch's window is its
     # longest frame + 1, once per chunk
     assert hs["umem_h2d_bytes"] == sum(len(b) * (int(lens[b].max()) + 1) for b in batches), hs
     assert hs["umem_copies"] == len(batches), hs
-    assert hs["desc_h2d_bytes"] == nframes * 16
 
 
-def test_chunked_fallbacks_and_umem_end():
+def udp_to_frame_end(umem, descs, length):
+    """Frames of `length` bytes whose IPv4 and UDP lengths run to the
+    frame's last byte (the pools pad odd sizes), the IPv4 header checksum
+    redone: a UDP checksum range of odd length then ends at the frame's
+    end, and udp_csum reads the byte after it."""
+    for a in descs["addr"][descs["len"] >= length].astype(np.int64):
+        f = umem[a:a + length]
+        if f[12] != 0x08 or f[13] != 0x00 or f[23] != 17:
+            continue
+        f[16:18] = np.frombuffer((length - 14).to_bytes(2, "big"), np.uint8)
+        f[38:40] = np.frombuffer((length - 34).to_bytes(2, "big"), np.uint8)
+        f[24:26] = 0
+        w = f[14:34].astype(np.uint32)
+        c = int((w[0::2] << 8).sum() + w[1::2].sum())
+        while c >> 16:
+            c = (c & 0xffff) + (c >> 16)
+        f[24:26] = np.frombuffer((~c & 0xffff).to_bytes(2, "big"), np.uint8)
+    descs["len"][descs["len"] >= length] = length
+
+
+@pytest.mark.parametrize("size", [64, 65, 67, 600, 601])
+def test_gather_over_read_byte(size):
+    """The gather copies a frame's own bytes and, for odd lengths, the byte
+    after it (udp_csum's over-read, lib_checksum.h:175-176): frames whose
+    UDP range runs to their last byte, every other byte of the 4 KiB chunks
+    random, so a byte the kernels read but the gather left out would show
+    as the mirror's stale value.  Outputs equal the oracle's on the host
+    UMEM; for odd sizes the over-read byte is shown to matter (changing it
+    changes the oracle's records)."""
+    nframes, B = 2048, 512
+    umem, descs, _ = chunked_pool(nframes, xdpgpu.POOL_UDP4, size + (size & 1), 75)
+    udp_to_frame_end(umem, descs, size)
+    lens = descs["len"].astype(np.int64)
+    addr = descs["addr"].astype(np.int64)
+    assert (lens == size).mean() > 0.9
+    inr = addr + lens <= umem.size
+    keep = np.zeros(umem.size + 1, np.int64)
+    np.add.at(keep, addr[inr], 1)
+    np.add.at(keep, (addr + lens)[inr], -1)
+    noise = ~np.cumsum(keep)[:-1].astype(bool)
+    umem[noise] = np.random.default_rng(size).integers(0, 256, int(noise.sum()), np.uint8)
+    batches = [np.arange(k, k + B) for k in range(0, nframes, B)]
+    host = umem.copy()
+    hs = {}
+    got, st = run_ring(host, descs, batches, 0x4 | xdpgpu.CFG_UMEM_GATHER, 0,
+                       fmt=xdpgpu.TUPLE_V4, window=0, chunk=CHUNK, host_stats=hs)
+    ou = umem.copy()
+    want, ost = oracle_ring(ou, descs, batches, 0x4, fmt=xdpgpu.TUPLE_V4)
+    check_ring(got, want, host, ou, st, ost)
+    assert hs["umem_gathers"] == len(batches), hs
+    assert hs["umem_h2d_bytes"] == gather_bytes(descs, batches, umem.size), hs
+    assert ost["verdict"][xdpgpu.REDIRECT] > 0.9 * nframes
+    z = umem.copy()
+    idx = (addr + lens)[inr & (addr + lens < umem.size)]
+    z[idx] = umem[idx] + 1
+    w2, _ = oracle_ring(z, descs, batches, 0x4, fmt=xdpgpu.TUPLE_V4)
+    assert (size & 1) == any(not np.array_equal(a[1], b[1]) for a, b in zip(want, w2))
+
+
+@pytest.mark.parametrize("gather", [False, True], ids=["rows", "gather"])
+def test_chunked_fallbacks_and_umem_end(gather):
     """The rows' edges: a frame whose over-read byte lies in the next chunk
-    (the batch falls back to span copies), and a UMEM whose size is not a
-    whole number of chunks, its last frame cut by the UMEM's end (the last
-    row is copied clamped, never read past the host UMEM)."""
+    (the batch falls back to span copies, gather or not), and a UMEM whose
+    size is not a whole number of chunks, its last frame cut by the UMEM's
+    end (the last row is copied clamped, never read past the host UMEM;
+    the gather skips the frame the UMEM does not hold)."""
     nframes = 600
     umem, descs, _ = chunked_pool(nframes, xdpgpu.POOL_UDP4, 64, 74)
     # frame 5 fills its chunk to the last byte: udp_csum reads one past it
@@ -423,9 +516,10 @@ def test_chunked_fallbacks_and_umem_end():
                            ("UMEM end", small, np.arange(nframes - 300, nframes))):
         host = u.copy()
         hs = {}
-        got, st = run_ring(host, d, [batch], 0x5, 0, fmt=xdpgpu.TUPLE_V4, window=0,
-                           chunk=CHUNK, host_stats=hs)
+        got, st = run_ring(host, d, [batch], 0x5 | (xdpgpu.CFG_UMEM_GATHER if gather else 0),
+                           0, fmt=xdpgpu.TUPLE_V4, window=0, chunk=CHUNK, host_stats=hs)
         ou = u.copy()
         want, ost = oracle_ring(ou, d, [batch], 0x5, fmt=xdpgpu.TUPLE_V4)
         check_ring(got, want, host, ou, st, ost)
         assert hs["frames"] == len(batch), name
+        assert hs["umem_gathers"] == (1 if gather and name == "UMEM end" else 0), (name, hs)

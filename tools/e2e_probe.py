@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+# SPDX-License-Identifier: GPL-2.0
+"""The chunked host-path leg of bench.py alone (4 KiB chunks, 64 B frames
+at headroom 256), with and without XDPGPU_CFG_UMEM_GATHER, and the host
+time xdpgpu_submit takes per batch: for rocprofv3 (--kernel-trace
+--memory-copy-trace --stats) and A/B runs.
+
+    python3 tools/e2e_probe.py [--frames N] [--batches K] [--gather-only]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "bpf-examples_amd"))
+
+import bench  # noqa: E402
+import xdpgpu  # noqa: E402
+
+
+def submit_cost(cu, cd, B, flags, reps=8):
+    """Host seconds per xdpgpu_submit call (the GPU work left queued)."""
+    h = xdpgpu.XdpGpu(0, flags, 0, xdpgpu.TUPLE_V4, 0, max_batch=B)
+    h.register_umem(cu, 4096)
+    hd = xdpgpu.HostBuffer(B, xdpgpu.DESC_DTYPE)
+    hd.array[:] = cd[:B]
+    outs = [xdpgpu.HostBuffer(B, dt) for dt in (np.uint8, xdpgpu.RESULT_DTYPE,
+                                                 xdpgpu.TUPLE4_DTYPE)]
+    v, r, t = (b.array for b in outs)
+    tot = 0.0
+    for k in range(reps):
+        t0 = time.perf_counter()
+        h.submit(0, hd.array, v, r, t)
+        tot += time.perf_counter() - t0
+        h.wait(0)
+    h.close()
+    hd.close()
+    for b in outs:
+        b.close()
+    return tot / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=1 << 20)
+    ap.add_argument("--batches", type=int, default=32)
+    ap.add_argument("--gather-only", action="store_true")
+    args = ap.parse_args()
+    import torch
+    torch.cuda.set_device(0)
+    nc = args.frames
+    cu, cd, ce = xdpgpu.pool_generate(nc, xdpgpu.POOL_UDP4, 64, 0x5EED0032, stride=4096,
+                                      headroom=256)
+    ceil = {"h2d_gbps": 57.0, "d2h_gbps": 57.0}
+    modes = [("gather", xdpgpu.CFG_DEFAULT | xdpgpu.CFG_UMEM_GATHER)]
+    if not args.gather_only:
+        modes.insert(0, ("rows", xdpgpu.CFG_DEFAULT))
+    for name, flags in modes:
+        r = bench.e2e_run(0, cu, cd, ce, nc // 2, args.batches, 4096, 0, ceil, flags)
+        r.pop("pcie_ceiling", None)
+        r["mode"] = name
+        r["submit_host_ms"] = round(submit_cost(cu, cd, nc // 2, flags) * 1e3, 3)
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()

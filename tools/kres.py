@@ -19,29 +19,36 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "bpf-examples_amd", "csrc", "libxdpgpu.so")
 
 
-def code_object(lib: str, arch: str = "gfx950") -> bytes:
+def code_objects(lib: str, arch: str = "gfx950") -> list:
+    """The arch's code object of every offload bundle in the library (one
+    per .hip translation unit)."""
     b = open(lib, "rb").read()
+    objs = []
     i = b.find(b"__CLANG_OFFLOAD_BUNDLE__")
-    if i < 0:
-        raise RuntimeError(f"{lib}: no offload bundle")
-    n = struct.unpack_from("<Q", b, i + 24)[0]
-    p = i + 32
-    for _ in range(n):
-        off, size, tl = struct.unpack_from("<QQQ", b, p)
-        p += 24
-        triple = b[p:p + tl].decode()
-        p += tl
-        if triple.endswith(arch):
-            return b[i + off:i + off + size]
-    raise RuntimeError(f"{lib}: no {arch} code object")
+    while i >= 0:
+        n = struct.unpack_from("<Q", b, i + 24)[0]
+        p = i + 32
+        for _ in range(n):
+            off, size, tl = struct.unpack_from("<QQQ", b, p)
+            p += 24
+            triple = b[p:p + tl].decode()
+            p += tl
+            if triple.endswith(arch):
+                objs.append(b[i + off:i + off + size])
+        i = b.find(b"__CLANG_OFFLOAD_BUNDLE__", i + 24)
+    if not objs:
+        raise RuntimeError(f"{lib}: no {arch} code object")
+    return objs
 
 
 def kernels(lib: str = LIB) -> dict:
-    with tempfile.NamedTemporaryFile(suffix=".elf") as f:
-        f.write(code_object(lib))
-        f.flush()
-        out = subprocess.run([READELF, "--notes", f.name], capture_output=True, text=True,
-                             check=True).stdout
+    out = ""
+    for obj in code_objects(lib):
+        with tempfile.NamedTemporaryFile(suffix=".elf") as f:
+            f.write(obj)
+            f.flush()
+            out += subprocess.run([READELF, "--notes", f.name], capture_output=True,
+                                  text=True, check=True).stdout
     res = {}
     for blk in out.split(".name:")[1:]:
         name = blk.split()[0]
