@@ -21,7 +21,11 @@ pytestmark = pytest.mark.skipif(not os.path.exists(kres.READELF) or
 
 def test_no_scratch_or_vgpr_spills():
     ks = kres.kernels()
-    assert any("xdp_rx_db_kernel" in k for k in ks)
+    # every translation unit's code object (one offload bundle each)
+    for part in ("xdp_rx_db_kernel", "xdp_nat64_kernel", "xdp_nat64_fast_kernel",
+                 "synproxy_kernel", "frag_count_kernel", "hints_kernel",
+                 "echo_writeback_kernel", "umem_gather_kernel"):
+        assert any(part in k for k in ks), part
     bad = {k: v for k, v in ks.items() if v["scratch"] or v["vgpr_spill"]}
     assert not bad, f"kernels with scratch or VGPR spills: {bad}"
 

@@ -50,11 +50,16 @@ def kernels(lib: str = LIB) -> dict:
             out += subprocess.run([READELF, "--notes", f.name], capture_output=True,
                                   text=True, check=True).stdout
     res = {}
-    for blk in out.split(".name:")[1:]:
-        name = blk.split()[0]
+    # one record per kernel map (keys in alphabetical order: .args, whose
+    # entries may carry .name too, come before the kernel's own .name)
+    for blk in re.split(r"\n\s+- \.agpr_count:", out)[1:]:
+        names = re.findall(r"\n    \.name:\s+(\S+)", blk)
+        if not names:
+            continue
+        name = names[-1]
 
         def g(k):
-            m = re.search(r"\." + k + r":\s+(\d+)", blk)
+            m = re.search(r"\n    \." + k + r":\s+(\d+)", blk)
             return int(m.group(1)) if m else None
         res[name] = {"vgpr": g("vgpr_count"), "sgpr": g("sgpr_count"),
                      "vgpr_spill": g("vgpr_spill_count"), "sgpr_spill": g("sgpr_spill_count"),
