@@ -80,25 +80,27 @@ __global__ __launch_bounds__(kEchoBlock) void echo_writeback_kernel(EchoArgs a)
  * descriptor names, [eff, eff + len), and udp_csum's over-read byte
  * eff + len (lib_checksum.h:175-176) where it can lie past the frame,
  * copied from the host UMEM's GPU mapping into the mirror, in the 16-byte
- * pieces that cover them.  The over-read byte: a checksum range starts at
+ * pieces that cover them (clamped to the UMEM; the pieces' other bytes are
+ * the UMEM's own, copied to the same offsets of this slot's mirror, which
+ * no other batch reads).  The over-read byte: a checksum range starts at
  * an even offset (14 + 4 * tags, + the IPv4 header's 4 * ihl or IPv6's 40
  * + 8k) and the parse bounds its end by len, so it ends at len only with
  * len odd; a multi-buffer packet's byte follows its last fragment, whose
  * own length says nothing, so there every fragment takes it (over_all).
- * The caller (copy_batch) uses this for chunked UMEMs only, where every
- * piece lies in the frame's chunk: [eff & ~15, round_up(eff + len + 1, 16))
- * inside [chunk, chunk + chunk_size), as batch_rows checked.  Plain loads,
- * nothing written to host memory; a piece the UMEM's end cuts goes byte by
- * byte.  8 lanes a frame, 8 frames a wave, each lane one piece in flight.
- * With hdesc the descriptors come from the caller's page-locked array (read
- * here, through its GPU mapping) and lane 0 of each frame's group writes
- * the device copy the RX kernel reads.
+ * Offsets decode as the RX kernel's (addr & (2^48 - 1)) + (addr >> 48).
+ * Plain loads, nothing written to host memory; a piece the UMEM's end cuts
+ * goes byte by byte.  8 lanes a frame, 8 frames a wave, each lane one
+ * piece in flight.  With hdesc the descriptors come from the caller's
+ * page-locked array (read here, through its GPU mapping) and lane 0 of
+ * each frame's group writes the device copy the RX kernel reads.  The
+ * bytes read are summed per wave into *nbytes (xdpgpu_host_stats).
  */
 constexpr int kGatherLanes = 8;
 __global__ __launch_bounds__(256) void umem_gather_kernel(GatherArgs a)
 {
 	const uint32_t sub = threadIdx.x & (kGatherLanes - 1);
 	const uint64_t step = (uint64_t)gridDim.x * (256 / kGatherLanes);
+	uint64_t mine = 0;
 	for (uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / kGatherLanes; i < a.n;
 	     i += step) {
 		xdpgpu_desc d;
@@ -109,15 +111,19 @@ __global__ __launch_bounds__(256) void umem_gather_kernel(GatherArgs a)
 		} else {
 			d = a.desc[i];
 		}
-		const uint64_t eff = d.addr;
-		/* descriptors outside the UMEM (and offset-field addresses, which
-		 * batch_rows never hands here) name no bytes */
+		const uint64_t eff = (d.addr & ((1ull << 48) - 1)) + (d.addr >> 48);
+		/* descriptors outside the UMEM name no bytes */
 		if (eff >= a.usize || (uint64_t)d.len > a.usize - eff)
 			continue;
 		uint64_t hi = eff + d.len + ((a.over_all | d.len) & 1);
 		if (hi > a.usize)
 			hi = a.usize;
-		for (uint64_t p = (eff & ~15ull) + 16 * sub; p < hi; p += 16 * kGatherLanes) {
+		const uint64_t lo = eff & ~15ull;
+		if (sub == 0) {
+			const uint64_t r = (hi + 15) & ~15ull;
+			mine += (r < a.usize ? r : a.usize) - lo;
+		}
+		for (uint64_t p = lo + 16 * sub; p < hi; p += 16 * kGatherLanes) {
 			if (p + 16 <= a.usize) {
 				const uint4 v = *reinterpret_cast<const uint4 *>(a.src + p);
 				*reinterpret_cast<uint4 *>(a.mirror + p) = v;
@@ -127,6 +133,10 @@ __global__ __launch_bounds__(256) void umem_gather_kernel(GatherArgs a)
 			}
 		}
 	}
+	for (int o = 32; o; o >>= 1)
+		mine += __shfl_down(mine, o, 64);
+	if ((threadIdx.x & 63) == 0 && mine)
+		atomicAdd(a.nbytes, (unsigned long long)mine);
 }
 
 } // namespace

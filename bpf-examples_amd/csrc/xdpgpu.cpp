@@ -96,6 +96,9 @@ struct xdpgpu_ctx {
 	/* XDPGPU_CFG_UMEM_GATHER on a chunked UMEM: its GPU mapping (the
 	 * gather kernel's source), else null */
 	const uint8_t *d_hview = nullptr;
+	/* the bytes the gather kernels read (device counter, added in by
+	 * xdpgpu_host_stats) */
+	unsigned long long *d_gbytes = nullptr;
 	/* host-path copy accounting (xdpgpu_host_stats) */
 	struct xdpgpu_host_stats hstats{};
 	/* XDPGPU_CFG_TIMING: 4 events per recorded launch */
@@ -259,6 +262,8 @@ void xdpgpu_fini(xdpgpu_ctx *ctx)
 	(void)hipDeviceSynchronize();
 	for (uint32_t i = 0; i < kSlots; i++)
 		free_slot(ctx->slot[i]);
+	if (ctx->d_gbytes)
+		(void)hipFree(ctx->d_gbytes);
 	if (ctx->tev) {
 		for (uint32_t i = 0; i < 4 * XDPGPU_TIMING_MAX; i++)
 			if (ctx->tev[i])
@@ -421,11 +426,20 @@ int xdpgpu_register_umem(xdpgpu_ctx *ctx, void *base, uint64_t size,
 	if ((ctx->cfg.flags & XDPGPU_CFG_UMEM_GATHER) && ctx->chunk) {
 		/* memory pinned here or by the caller (xdpgpu_host_alloc) */
 		void *p = nullptr;
-		if (hipHostGetDevicePointer(&p, base, 0) == hipSuccess && p)
+		if (hipHostGetDevicePointer(&p, base, 0) == hipSuccess && p) {
+			if (!ctx->d_gbytes) {
+				if (hipMalloc(&ctx->d_gbytes, sizeof(*ctx->d_gbytes)) != hipSuccess) {
+					release_umem(ctx);
+					return set_err(ctx, -ENOMEM, "gather byte counter");
+				}
+				HIP_TRY(ctx, hipMemset(ctx->d_gbytes, 0, sizeof(*ctx->d_gbytes)));
+			}
 			ctx->d_hview = (const uint8_t *)p;
-		else
+		} else {
 			(void)hipGetLastError();
+		}
 	}
+
 	/* slot 0's mirror now, so that a size the device cannot hold fails
 	 * here; slot 1's on its first batch */
 	const int rc = ensure_mirror(ctx, ctx->slot[0]);
@@ -1242,34 +1256,18 @@ static bool batch_rows(const xdpgpu_ctx *ctx, const xdpgpu_desc *descs, uint32_t
 	}
 }
 
-/* XDPGPU_CFG_UMEM_GATHER: whether the gather kernel can take the batch
- * (every frame and its over-read byte inside its own chunk, no offset
- * field: umem_gather_kernel's pieces then stay in the frames' chunks).
- * Sets used and the bytes the gather will read. */
-static bool gather_holds(const xdpgpu_ctx *ctx, const xdpgpu_desc *descs, uint32_t n,
-			 uint64_t &used, uint64_t &bytes)
+/* XDPGPU_CFG_UMEM_GATHER: the RX launch's window wants the batch's mean
+ * frame length (xdpgpu.h: a performance choice, the outputs are the same
+ * whatever the window), which a sample of up to 4096 descriptors gives;
+ * the gather itself needs no pass over the batch on the host (its bytes are
+ * counted on the device). */
+static uint64_t sampled_used(const xdpgpu_desc *descs, uint32_t n)
 {
-	/* one pass (the RX thread's own time between a slot's wait and its
-	 * next gather): the bytes umem_gather_kernel's pieces move, too */
-	used = 0;
-	bytes = 0;
-	const uint64_t mask = ctx->chunk - 1, us = ctx->umem_size;
-	const uint64_t odd = (ctx->cfg.flags & XDPGPU_CFG_FRAGS) ? 1u : 0u;
-	for (uint32_t i = 0; i < n; i++) {
-		const uint64_t eff = descs[i].addr, len = descs[i].len;
-		if (eff >> 48)
-			return false;
-		if (eff >= us)
-			continue;
-		if ((eff & mask) + len + 1 > ctx->chunk)
-			return false;
-		used += len;
-		if (len > us - eff)
-			continue;
-		const uint64_t hi = std::min<uint64_t>(eff + len + ((odd | len) & 1), us);
-		bytes += std::min<uint64_t>((hi + 15) & ~15ull, us) - (eff & ~15ull);
-	}
-	return true;
+	const uint32_t step = n > 4096 ? n / 4096 : 1;
+	uint64_t sum = 0, cnt = 0;
+	for (uint32_t i = 0; i < n; i += step, cnt++)
+		sum += descs[i].len;
+	return cnt ? sum * n / cnt : 0;
 }
 
 /* The device view of a page-locked host array (hipHostMalloc'd or
@@ -1296,8 +1294,7 @@ static const void *host_view(const void *p)
  * (The two slots' gathers run at once; one stream for both, the gathers
  * back to back, held each slot's kernels behind the other slot's gather:
  * 226 vs 239 M frames/s.) */
-static int gather_batch(xdpgpu_ctx *ctx, Slot &s, uint32_t n, const xdpgpu_desc *hdesc,
-			uint64_t bytes)
+static int gather_batch(xdpgpu_ctx *ctx, Slot &s, uint32_t n, const xdpgpu_desc *hdesc)
 {
 	GatherArgs g;
 	g.src = ctx->d_hview;
@@ -1307,8 +1304,8 @@ static int gather_batch(xdpgpu_ctx *ctx, Slot &s, uint32_t n, const xdpgpu_desc 
 	g.hdesc = hdesc;
 	g.n = n;
 	g.over_all = (ctx->cfg.flags & XDPGPU_CFG_FRAGS) ? 1u : 0u;
+	g.nbytes = ctx->d_gbytes;
 	HIP_TRY(ctx, launch_umem_gather(g, s.stream));
-	ctx->hstats.umem_h2d_bytes += bytes;
 	ctx->hstats.umem_copies++;
 	ctx->hstats.umem_gathers++;
 	return 0;
@@ -1375,6 +1372,14 @@ int xdpgpu_host_stats(xdpgpu_ctx *ctx, struct xdpgpu_host_stats *out)
 	if (!ctx || !out)
 		return -EINVAL;
 	*out = ctx->hstats;
+	if (ctx->d_gbytes) {
+		/* the gather kernels' bytes, counted on the device (batches
+		 * still in flight may not be in yet) */
+		unsigned long long b = 0;
+		HIP_TRY(ctx, hipSetDevice(ctx->cfg.device));
+		HIP_TRY(ctx, hipMemcpy(&b, ctx->d_gbytes, sizeof(b), hipMemcpyDeviceToHost));
+		out->umem_h2d_bytes += b;
+	}
 	return 0;
 }
 
@@ -1402,14 +1407,16 @@ int xdpgpu_submit(xdpgpu_ctx *ctx, uint32_t slot, const xdpgpu_desc *descs,
 
 	/* the frames go to this slot's own mirror: a batch in flight on the
 	 * other slot never sees them, whatever the two batches' addresses */
-	uint64_t used = 0, gbytes = 0;
-	const bool gather = ctx->d_hview && gather_holds(ctx, descs, n, used, gbytes);
+	uint64_t used = 0;
+	const bool gather = ctx->d_hview != nullptr;
+	if (gather)
+		used = sampled_used(descs, n);
 	const xdpgpu_desc *hdesc =
 		gather ? (const xdpgpu_desc *)host_view(descs) : nullptr;
 	if (!hdesc)
 		HIP_TRY(ctx, hipMemcpyAsync(s.d_desc, descs, (size_t)n * sizeof(*descs),
 					    hipMemcpyHostToDevice, s.stream));
-	rc = gather ? gather_batch(ctx, s, n, hdesc, gbytes) : copy_batch(ctx, s, descs, n, used);
+	rc = gather ? gather_batch(ctx, s, n, hdesc) : copy_batch(ctx, s, descs, n, used);
 	if (rc)
 		return rc;
 	const bool echo = ctx->cfg.flags & XDPGPU_CFG_ICMP6_ECHO;

@@ -238,6 +238,7 @@ struct GatherArgs {
 	uint32_t n;
 	uint32_t over_all;         /* 1: every frame's byte len (multi-buffer
 				    * packets); 0: odd lengths only          */
+	unsigned long long *nbytes;   /* += the bytes read (host stats)    */
 };
 hipError_t launch_umem_gather(const GatherArgs &a, hipStream_t stream);
 

@@ -132,8 +132,8 @@ struct xdpgpu_network_tuple {
  * read only, the frames' own bytes), instead of the copy engine's pitched
  * copies of one window per chunk.  About twice the rows per second for
  * small frames in 4 KiB chunks.  Ignored (the copies
- * are used) for a UMEM without chunk_size, one the GPU cannot map, or a
- * batch the rows do not hold. */
+ * are used) for a UMEM registered without chunk_size or one the GPU cannot
+ * map. */
 #define XDPGPU_CFG_UMEM_GATHER 0x20
 #define XDPGPU_CFG_DEFAULT     (XDPGPU_CFG_VERIFY_CSUM | XDPGPU_CFG_STATS)
 
@@ -242,7 +242,8 @@ void xdpgpu_host_free(void *p);
  * chunk it names, the same offsets in every chunk (rows of a pitched
  * copy); otherwise spans of nearby frames.  With XDPGPU_CFG_UMEM_GATHER the
  * batches a gather kernel moved count in umem_gathers (their bytes, the
- * 16-byte pieces read, in umem_h2d_bytes; umem_copies counts one a batch). */
+ * 16-byte pieces read, in umem_h2d_bytes, counted on the device: a batch
+ * still in flight may be missing; umem_copies counts one a batch). */
 struct xdpgpu_host_stats {
 	uint64_t batches;
 	uint64_t frames;

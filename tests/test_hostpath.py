@@ -356,7 +356,8 @@ def gather_bytes(descs, batches, usize, over_all=False):
     """The 16-byte pieces umem_gather_kernel reads for the batches."""
     tot = 0
     for b in batches:
-        a = descs["addr"][b].astype(np.int64)
+        raw = descs["addr"][b].astype(np.uint64)
+        a = ((raw & np.uint64((1 << 48) - 1)) + (raw >> np.uint64(48))).astype(np.int64)
         ln = descs["len"][b].astype(np.int64)
         ok = (a < usize) & (ln <= usize - a)
         hi = np.minimum(a + ln + (1 if over_all else (ln & 1)), usize)
@@ -500,10 +501,11 @@ def test_gather_over_read_byte(size):
 @pytest.mark.parametrize("gather", [False, True], ids=["rows", "gather"])
 def test_chunked_fallbacks_and_umem_end(gather):
     """The rows' edges: a frame whose over-read byte lies in the next chunk
-    (the batch falls back to span copies, gather or not), and a UMEM whose
-    size is not a whole number of chunks, its last frame cut by the UMEM's
-    end (the last row is copied clamped, never read past the host UMEM;
-    the gather skips the frame the UMEM does not hold)."""
+    (the batch falls back to span copies; the gather reads the byte from
+    the next chunk), and a UMEM whose size is not a whole number of chunks,
+    its last frame cut by the UMEM's end (the last row is copied clamped,
+    never read past the host UMEM; the gather skips the frame the UMEM does
+    not hold)."""
     nframes = 600
     umem, descs, _ = chunked_pool(nframes, xdpgpu.POOL_UDP4, 64, 74)
     # frame 5 fills its chunk to the last byte: udp_csum reads one past it
@@ -522,4 +524,6 @@ def test_chunked_fallbacks_and_umem_end(gather):
         want, ost = oracle_ring(ou, d, [batch], 0x5, fmt=xdpgpu.TUPLE_V4)
         check_ring(got, want, host, ou, st, ost)
         assert hs["frames"] == len(batch), name
-        assert hs["umem_gathers"] == (1 if gather and name == "UMEM end" else 0), (name, hs)
+        assert hs["umem_gathers"] == (1 if gather else 0), (name, hs)
+        if gather:
+            assert hs["umem_h2d_bytes"] == gather_bytes(d, [batch], u.size), (name, hs)
