@@ -3,8 +3,9 @@
 """The echo leg's launch (bench.py echo_run) timed three ways: right after
 the device-to-device restore of the pool on the same stream (as bench.py
 did), after a synchronize that ends the restore first, and after the
-restore, a synchronize and a small kernel of its own: how much of the
-events' span is the kernel and how much the restore's aftermath.
+restore, a synchronize and a small kernel of its own, and after the
+restore and a 512 MiB read (the restore's dirty lines evicted): how much of
+the events' span is the kernel and how much the restore's aftermath.
 
     python3 tools/restore_probe.py [--frames N] [--steps K]
 """
@@ -41,16 +42,23 @@ def main():
     d_res = torch.empty(n * 16, dtype=torch.uint8, device=dev)
     d_tup = torch.empty(n * 16, dtype=torch.uint8, device=dev)
     small = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
+    # 512 MiB read after the restore: the restore's dirty lines written back
+    # (evicted by clean ones) before the timed launch
+    flush = torch.ones(64 << 20, dtype=torch.int64, device=dev)
     out = {}
     with xdpgpu.XdpGpu(0, xdpgpu.CFG_DEFAULT | xdpgpu.CFG_ICMP6_ECHO, 0,
                        xdpgpu.TUPLE_V4, 0) as g:
         for rnd in range(2):
-            for mode in ("same_stream", "sync", "sync_small_kernel"):
+            for mode in ("same_stream", "sync", "sync_small_kernel", "flush_read"):
                 ms = []
                 for k in range(args.steps + 2):
                     with torch.cuda.stream(stream):
                         work.copy_(pristine, non_blocking=True)
                     if mode != "same_stream":
+                        torch.cuda.synchronize()
+                    if mode == "flush_read":
+                        with torch.cuda.stream(stream):
+                            small[:8].view(torch.int64)[0] = flush.sum()
                         torch.cuda.synchronize()
                     if mode == "sync_small_kernel":
                         with torch.cuda.stream(stream):
