@@ -38,6 +38,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -725,6 +726,27 @@ def e2e_run(local, umem, descs, expect, B: int, nbatches: int, chunk: int, windo
             "verdicts_ok": ok}
 
 
+def gather_leg(frames: int, batches: int, ceil: dict) -> dict:
+    """e2e_run with XDPGPU_CFG_UMEM_GATHER on the chunked leg's workload,
+    run by tools/e2e_probe.py as a child process (its own GPU context):
+    the JSON of its gather line, or the failure."""
+    cmd = [sys.executable, os.path.join(ROOT, "tools", "e2e_probe.py"), "--gather-only",
+           "--no-submit-cost", "--frames", str(frames), "--batches", str(batches),
+           "--h2d-ceil", str(ceil["h2d_gbps"]), "--d2h-ceil", str(ceil["d2h_gbps"])]
+    try:
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    except subprocess.TimeoutExpired:
+        return {"error": "timed out after 300 s"}
+    for line in reversed(p.stdout.splitlines()):
+        if line.startswith("{"):
+            r = json.loads(line)
+            r.pop("mode", None)
+            r["pcie_ceiling"] = ceil
+            r["process"] = "child (tools/e2e_probe.py)"
+            return r
+    return {"error": f"exit {p.returncode}: {p.stderr.strip()[-300:]}"}
+
+
 def free_port() -> int:
     import socket
     s = socket.socket()
@@ -759,7 +781,6 @@ def launch_ranks(cmd: list, n: int, base_env: dict | None = None, poll_s: float 
     left waiting in a collective would never finish); the return code is
     the first failure's, else 0."""
     import signal
-    import subprocess
     envs = rank_envs(n, dict(os.environ if base_env is None else base_env), free_port())
     procs = [subprocess.Popen(cmd, env=e, start_new_session=True) for e in envs]
     rc = 0
@@ -959,13 +980,13 @@ def main():
                                        f"at headroom 256 ({cu.nbytes >> 20} MiB host UMEM, "
                                        "registered with chunk_size 4096), batches of half "
                                        "the UMEM cycling over it")
-            # the same with XDPGPU_CFG_UMEM_GATHER: a kernel reads each
-            # frame's bytes through the UMEM's GPU mapping
-            e2e_gather = e2e_run(local, cu, cd, ce, nc // 2, args.e2e_batches, 4096,
-                                 args.window, ceil,
-                                 xdpgpu.CFG_DEFAULT | xdpgpu.CFG_UMEM_GATHER)
-            e2e_gather["workload"] = e2e_chunked["workload"] + ", XDPGPU_CFG_UMEM_GATHER"
             del cu, cd, ce
+            # the same with XDPGPU_CFG_UMEM_GATHER (a kernel reads each
+            # frame's bytes through the UMEM's GPU mapping), in a child
+            # process: the one kernel that reads host memory (DESIGN.md
+            # §5.3) cannot take this line down with it
+            e2e_gather = gather_leg(nc, args.e2e_batches, ceil)
+            e2e_gather["workload"] = e2e_chunked["workload"] + ", XDPGPU_CFG_UMEM_GATHER"
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:

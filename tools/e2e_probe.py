@@ -6,6 +6,10 @@ time xdpgpu_submit takes per batch: for rocprofv3 (--kernel-trace
 --memory-copy-trace --stats) and A/B runs.
 
     python3 tools/e2e_probe.py [--frames N] [--batches K] [--gather-only]
+
+bench.py runs the gather leg through it as a child process: the gather is
+the one kernel that reads host memory, and a fault there
+then ends only the child, not the bench's line.
 """
 import argparse
 import json
@@ -50,13 +54,17 @@ def main():
     ap.add_argument("--frames", type=int, default=1 << 20)
     ap.add_argument("--batches", type=int, default=32)
     ap.add_argument("--gather-only", action="store_true")
+    ap.add_argument("--no-submit-cost", action="store_true")
+    ap.add_argument("--h2d-ceil", type=float, default=57.0,
+                    help="the box's pinned H2D GB/s (bench.py pcie_ceiling)")
+    ap.add_argument("--d2h-ceil", type=float, default=57.0)
     args = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
     nc = args.frames
     cu, cd, ce = xdpgpu.pool_generate(nc, xdpgpu.POOL_UDP4, 64, 0x5EED0032, stride=4096,
                                       headroom=256)
-    ceil = {"h2d_gbps": 57.0, "d2h_gbps": 57.0}
+    ceil = {"h2d_gbps": args.h2d_ceil, "d2h_gbps": args.d2h_ceil}
     modes = [("gather", xdpgpu.CFG_DEFAULT | xdpgpu.CFG_UMEM_GATHER)]
     if not args.gather_only:
         modes.insert(0, ("rows", xdpgpu.CFG_DEFAULT))
@@ -64,7 +72,8 @@ def main():
         r = bench.e2e_run(0, cu, cd, ce, nc // 2, args.batches, 4096, 0, ceil, flags)
         r.pop("pcie_ceiling", None)
         r["mode"] = name
-        r["submit_host_ms"] = round(submit_cost(cu, cd, nc // 2, flags) * 1e3, 3)
+        if not args.no_submit_cost:
+            r["submit_host_ms"] = round(submit_cost(cu, cd, nc // 2, flags) * 1e3, 3)
         print(json.dumps(r), flush=True)
 
 
