@@ -656,7 +656,7 @@ def pcie_ceiling(dev, mib: int = 256, reps: int = 10) -> dict:
 
 
 def e2e_run(local, umem, descs, expect, B: int, nbatches: int, chunk: int, window: int,
-            ceil: dict, flags: int = xdpgpu.CFG_DEFAULT) -> dict:
+            ceil: dict, flags: int = xdpgpu.CFG_DEFAULT, slots: int = 2) -> dict:
     """The host path as an RX loop drives it (xdpgpu_submit / xdpgpu_wait,
     two batches in flight): each batch's frames copied from the pinned host
     UMEM into the slot's device mirror (rows of chunks when chunk is given:
@@ -665,7 +665,8 @@ def e2e_run(local, umem, descs, expect, B: int, nbatches: int, chunk: int, windo
     consecutive descriptors cycle over the pool.  One pass checks every
     batch's verdicts, a second is timed; the PCIe bytes per frame come from
     xdpgpu_host_stats over the timed pass.  flags: XDPGPU_CFG_UMEM_GATHER
-    moves a chunked UMEM's frames by the gather kernel instead."""
+    moves a chunked UMEM's frames by the gather kernel instead; slots:
+    batches in flight (xdpgpu_submit's slots, 2 = double buffering)."""
     n = len(descs)
     per = max(1, n // B)
     h = xdpgpu.XdpGpu(local, flags, 0, xdpgpu.TUPLE_V4, window, max_batch=B)
@@ -675,14 +676,14 @@ def e2e_run(local, umem, descs, expect, B: int, nbatches: int, chunk: int, windo
     hd = xdpgpu.HostBuffer(per * B, xdpgpu.DESC_DTYPE)
     hd.array[:] = descs[: per * B]
     outs = [[xdpgpu.HostBuffer(B, dt) for dt in (np.uint8, xdpgpu.RESULT_DTYPE,
-                                                 xdpgpu.TUPLE4_DTYPE)] for _ in range(2)]
+                                                 xdpgpu.TUPLE4_DTYPE)] for _ in range(slots)]
 
     def one_pass(check: bool):
         ok = True
-        pending = [None, None]
+        pending = [None] * slots
         t0 = time.perf_counter()
-        for k in range(nbatches + 2):
-            slot = k & 1
+        for k in range(nbatches + slots):
+            slot = k % slots
             if pending[slot] is not None:
                 h.wait(slot)
                 if check:
@@ -713,7 +714,7 @@ def e2e_run(local, umem, descs, expect, B: int, nbatches: int, chunk: int, windo
     h2d_gbps = h2d / te / 1e9
     d2h_gbps = d2h / te / 1e9
     return {"mpps": round(fr / te / 1e6, 1), "frames": fr, "batch": B, "batches": nbatches,
-            "chunk": chunk, "pinned_buffers": True,
+            "slots": slots, "chunk": chunk, "pinned_buffers": True,
             "umem_gather": bool(flags & xdpgpu.CFG_UMEM_GATHER) and
             s1["umem_gathers"] > s0["umem_gathers"],
             "h2d_bytes_per_frame": round(h2d / fr, 1),

@@ -58,6 +58,7 @@ def main():
     ap.add_argument("--h2d-ceil", type=float, default=57.0,
                     help="the box's pinned H2D GB/s (bench.py pcie_ceiling)")
     ap.add_argument("--d2h-ceil", type=float, default=57.0)
+    ap.add_argument("--slots", default="2", help="batches in flight, e.g. 2,3,4")
     args = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
@@ -68,13 +69,15 @@ def main():
     modes = [("gather", xdpgpu.CFG_DEFAULT | xdpgpu.CFG_UMEM_GATHER)]
     if not args.gather_only:
         modes.insert(0, ("rows", xdpgpu.CFG_DEFAULT))
-    for name, flags in modes:
-        r = bench.e2e_run(0, cu, cd, ce, nc // 2, args.batches, 4096, 0, ceil, flags)
-        r.pop("pcie_ceiling", None)
-        r["mode"] = name
-        if not args.no_submit_cost:
-            r["submit_host_ms"] = round(submit_cost(cu, cd, nc // 2, flags) * 1e3, 3)
-        print(json.dumps(r), flush=True)
+    for slots in (int(x) for x in args.slots.split(",")):
+        for name, flags in modes:
+            r = bench.e2e_run(0, cu, cd, ce, nc // 2, args.batches, 4096, 0, ceil, flags,
+                              slots)
+            r.pop("pcie_ceiling", None)
+            r["mode"] = name
+            if not args.no_submit_cost:
+                r["submit_host_ms"] = round(submit_cost(cu, cd, nc // 2, flags) * 1e3, 3)
+            print(json.dumps(r), flush=True)
 
 
 if __name__ == "__main__":
