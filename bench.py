@@ -955,8 +955,11 @@ def main():
         if "echo" in legs:
             secondary["icmp6_echo"] = echo_run(dev, stream, 8 << 20, steps2, local,
                                                tune=args.tune, window=args.window)
+            attach_traffic(secondary["icmp6_echo"], "r[0-9][0-9]_pmc_echo_leg.json", 8 << 20)
         if "synproxy" in legs:
             secondary["synproxy"] = synproxy_run(dev, stream, 8 << 20, steps2, local)
+            attach_traffic(secondary["synproxy"], "r[0-9][0-9]_pmc_synproxy_leg.json",
+                           8 << 20)
 
     e2e = None
     e2e_chunked = None

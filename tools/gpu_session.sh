@@ -72,6 +72,8 @@ workload() {
 	frags_bounce) echo "python3 tools/frags_probe.py --reps 5 --tune 0x1000000" ;;
 	synproxy) echo "python3 bench.py --no-cpu --no-e2e --legs synproxy --steps 5 --warmup 2" ;;
 	echo) echo "python3 bench.py --no-cpu --no-e2e --legs echo --steps 5 --warmup 2" ;;
+	echo_leg) echo "python3 tools/leg_probe.py --leg echo" ;;
+	synproxy_leg) echo "python3 tools/leg_probe.py --leg synproxy" ;;
 	bench) echo "python3 bench.py --no-cpu --no-secondary --no-e2e --steps 20" ;;
 	bench50) echo "python3 bench.py --no-cpu --no-secondary --no-e2e --steps 50" ;;
 	*) echo "unknown workload $1" >&2; exit 2 ;;
@@ -109,6 +111,8 @@ for s in "$@"; do
 		1500*) geo="FRAMES=2097152 SIZE=1500" ;;
 		imix*) geo="FRAMES=16777216 SIZE=0" ;;
 		nat64*) geo="FRAMES=16777216 SIZE=128" ;;
+		echo_leg) geo="FRAMES=8388608 SIZE=128 PMC_ONLY=xdp_rx_db_kernel" ;;
+		synproxy_leg) geo="FRAMES=8388608 SIZE=74 PMC_ONLY=synproxy_kernel" ;;
 		*) geo="FRAMES=16777216 SIZE=64" ;;
 		esac
 		# shellcheck disable=SC2086

@@ -3,7 +3,8 @@
 """Summarise rocprofv3 --pmc passes (tools/pmc_profile.sh) per kernel:
 average counter value per dispatch.  HBM traffic per launch is
 2 * FETCH_SIZE + WRITE_SIZE (KiB -> bytes): on gfx950 FETCH_SIZE reads half
-the bytes of a wide coalesced stream (MI355X_MICROARCH.md §HBM)."""
+the bytes of a wide coalesced stream (MI355X_MICROARCH.md §HBM).  PMC_ONLY:
+sum only the kernels whose name holds it (default: the RX kernels)."""
 import csv
 import glob
 import json
@@ -22,7 +23,7 @@ def main(out, dest=None, frames=16 << 20, size=64, label=None):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 k = row.get("Kernel_Name", "?")
-                if "xdp_" not in k:
+                if "xdp_" not in k and "synproxy" not in k:
                     continue
                 name = row.get("Counter_Name")
                 val = float(row.get("Counter_Value", 0))
@@ -43,8 +44,10 @@ def main(out, dest=None, frames=16 << 20, size=64, label=None):
     with open(os.path.join(out, "summary.json"), "w") as fh:
         json.dump(summary, fh, indent=1)
     # bench.py form: HBM bytes per launch = sum over the launch's kernels
+    only = os.environ.get("PMC_ONLY")
     rx = {k: v for k, v in summary.items()
-          if any(k.split("<")[0].split("(")[0].endswith(r) for r in RX)}
+          if (only in k if only else
+              any(k.split("<")[0].split("(")[0].endswith(r) for r in RX))}
     tot = sum(v.get("hbm_bytes_per_launch", 0.0) for v in rx.values())
     doc = {"workload": label or (f"config2 pool: {frames} x {size} B IPv4/UDP "
                                  "(tools/tune_rx.py, V4 tuples)"),
