@@ -44,7 +44,7 @@ def kind(l):
 
 def loops(path, pats, top=3):
     with tempfile.NamedTemporaryFile(suffix=".elf") as f:
-        f.write(kres.code_object(path))
+        f.write(kres.code_objects(path)[0])
         f.flush()
         txt = subprocess.run([OBJDUMP, "-d", "--symbolize-operands", f.name],
                              capture_output=True, text=True, check=True).stdout
