@@ -1280,7 +1280,14 @@ static const void *host_view(const void *p)
 		(void)hipGetLastError();
 		return nullptr;
 	}
-	return at.type == hipMemoryTypeHost ? at.devicePointer : nullptr;
+	if (at.type != hipMemoryTypeHost || !at.devicePointer)
+		return nullptr;
+	/* p may lie inside the allocation: the same offset from the device
+	 * view of the host pointer the attributes name */
+	if (at.hostPointer && (const char *)p >= (const char *)at.hostPointer)
+		return (const char *)at.devicePointer +
+		       ((const char *)p - (const char *)at.hostPointer);
+	return at.devicePointer;
 }
 
 /* XDPGPU_CFG_UMEM_GATHER: the gather kernel moves the batch's frame bytes

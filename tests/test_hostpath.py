@@ -459,6 +459,37 @@ def udp_to_frame_end(umem, descs, length):
     descs["len"][descs["len"] >= length] = length
 
 
+def test_gather_descs_inside_pinned_buffer():
+    """The gather reads page-locked descriptors through their GPU mapping:
+    a batch handed over as a slice from the middle of a page-locked array
+    (an RX loop's descriptor ring) is read at its own offset."""
+    nframes, B = 4096, 1000
+    umem, descs, _ = chunked_pool(nframes, xdpgpu.POOL_UDP4, 64, 76)
+    ring = xdpgpu.HostBuffer(3 * B, xdpgpu.DESC_DTYPE)
+    outs = [xdpgpu.HostBuffer(B, dt) for dt in (np.uint8, xdpgpu.RESULT_DTYPE,
+                                                  xdpgpu.TUPLE4_DTYPE)]
+    try:
+        with xdpgpu.XdpGpu(0, 0x5 | xdpgpu.CFG_UMEM_GATHER, 0, xdpgpu.TUPLE_V4, 0,
+                           max_batch=B) as ctx:
+            ctx.register_umem(umem, CHUNK)
+            for k, lo in enumerate((B + 13, 7, 2 * B - 1)):
+                b = np.arange(k * B, (k + 1) * B) % nframes
+                ring.array[lo:lo + B] = descs[b]
+                v, r, t = (o.array for o in outs)
+                ctx.submit(0, ring.array[lo:lo + B], v, r, t)
+                ctx.wait(0)
+                ov, ores, otup, _ = oracle.process(umem.copy(), np.ascontiguousarray(descs[b]),
+                                                   0x5, 0, xdpgpu.TUPLE_V4)
+                np.testing.assert_array_equal(v, ov, err_msg=f"batch at {lo}")
+                np.testing.assert_array_equal(r.view(np.uint8).reshape(-1),
+                                              ores.view(np.uint8).reshape(-1))
+            assert ctx.host_stats()["umem_gathers"] == 3
+    finally:
+        ring.close()
+        for o in outs:
+            o.close()
+
+
 @pytest.mark.parametrize("size", [64, 65, 67, 600, 601])
 def test_gather_over_read_byte(size):
     """The gather copies a frame's own bytes and, for odd lengths, the byte
