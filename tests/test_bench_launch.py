@@ -63,3 +63,36 @@ def test_launch_ranks_failure_stops_the_rest(tmp_path):
     assert rc == 3
     assert time.time() - t0 < 30
     assert not (tmp_path / "done").exists()
+
+
+def test_gather_leg_child(monkeypatch):
+    """The gather leg runs in a child process (tools/e2e_probe.py): its last
+    JSON line becomes the leg, a failing or hung child becomes an error
+    entry, and the bench's line survives either way."""
+    import json
+    import subprocess
+    ceil = {"h2d_gbps": 57.0, "d2h_gbps": 56.0}
+    seen = {}
+
+    def ok(cmd, **kw):
+        seen["cmd"] = cmd
+        line = json.dumps({"mpps": 250.0, "mode": "gather", "verdicts_ok": True})
+        return subprocess.CompletedProcess(cmd, 0, "log line\n" + line + "\n", "")
+    monkeypatch.setattr(bench.subprocess, "run", ok)
+    r = bench.gather_leg(1 << 20, 32, ceil)
+    assert r["mpps"] == 250.0 and "mode" not in r and r["pcie_ceiling"] == ceil
+    cmd = seen["cmd"]
+    assert cmd[1].endswith(os.path.join("tools", "e2e_probe.py"))
+    assert "--gather-only" in cmd and cmd[cmd.index("--frames") + 1] == str(1 << 20)
+    assert cmd[cmd.index("--h2d-ceil") + 1] == "57.0"
+
+    def fault(cmd, **kw):
+        return subprocess.CompletedProcess(cmd, -6, "", "illegal memory access\n")
+    monkeypatch.setattr(bench.subprocess, "run", fault)
+    r = bench.gather_leg(1 << 20, 32, ceil)
+    assert "error" in r and "-6" in r["error"] and "illegal" in r["error"]
+
+    def hang(cmd, **kw):
+        raise subprocess.TimeoutExpired(cmd, kw.get("timeout"))
+    monkeypatch.setattr(bench.subprocess, "run", hang)
+    assert "timed out" in bench.gather_leg(1 << 20, 32, ceil)["error"]
