@@ -561,6 +561,10 @@ def frags_run(dev, stream, n, steps, local, size=9000, chunk=4096):
            "packets": n, "descriptors": m, "mpps": round(n / t / 1e6, 1),
            "ms_per_launch": round(t * 1e3, 4),
            "packet_gbps": round(float(lens.sum()) / t / 1e9, 1), "verdicts_ok": ok}
+    # descriptors in, packet bytes, verdict + record + tuple out per descriptor
+    algo = m * (16 + 1 + 16 + 16) + int(lens.sum())
+    out.update({"algorithmic_bytes_per_launch": algo, "gbps": round(algo / t / 1e9, 1),
+                "roofline_frac": round(algo / t / 1e9 / HBM_PEAK_GBS, 4)})
     del g_umem, g_desc, g_v, g_res, g_tup
     torch.cuda.empty_cache()
     return out
@@ -951,7 +955,7 @@ def main():
             attach_traffic(secondary["config4_nat64"], "r[0-9][0-9]_pmc_config4.json",
                            args.nat64_frames)
         if "frags" in legs:
-            secondary["multibuffer_9000B"] = frags_run(dev, stream, 1 << 16, steps2, local)
+            secondary["multibuffer_9000B"] = frags_run(dev, stream, 1 << 18, steps2, local)
         if "echo" in legs:
             secondary["icmp6_echo"] = echo_run(dev, stream, 8 << 20, steps2, local,
                                                tune=args.tune, window=args.window)
