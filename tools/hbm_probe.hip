@@ -13,6 +13,7 @@
  *   syn       : the SYN proxy leg's in-place shape (argument "syn")
  *   imix      : config 3's two read patterns and the tile loop's head+outputs
  *               shape (argument "imix")
+ *   rec       : the bulk pass's 16-byte record stores (argument "rec")
  *
  * Build: hipcc --offload-arch=gfx950 -O3 -o tools/hbm_probe tools/hbm_probe.hip
  */
@@ -786,8 +787,77 @@ static int imix_main()
 	return 0;
 }
 
+/*
+ * The bulk pass's record stores (argument "rec"): 16 M 16-byte records
+ * written whole (the tile loop), then 16 bytes at a sorted 42 % of them
+ * (one store a record, as the bulk pass writes its frames' records), or
+ * the 64-byte aligned groups holding those records written whole: whether
+ * a lone 16-byte store costs its ECC word's read-modify-write.
+ */
+__global__ __launch_bounds__(256) void k_rec_all(uint4 *rec, size_t n)
+{
+	for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+		rec[i] = make_uint4((uint32_t)i, 1, 2, 3);
+}
+__global__ __launch_bounds__(256) void k_rec_some(uint4 *rec, const uint32_t *idx, size_t m,
+						  int group)
+{
+	for (size_t k = blockIdx.x * 256ull + threadIdx.x; k < m; k += (size_t)gridDim.x * 256) {
+		const uint32_t i = idx[k];
+		if (group) {
+			uint4 *g = rec + (i & ~3u);
+			for (int j = 0; j < 4; j++)
+				g[j] = make_uint4(i, (uint32_t)j, 5, 6);
+		} else {
+			rec[i] = make_uint4(i, 4, 5, 6);
+		}
+	}
+}
+
+static int rec_main()
+{
+	const size_t n = 16ull << 20;
+	uint4 *rec;
+	CK(hipMalloc(&rec, n * 16));
+	std::vector<uint32_t> idx;
+	uint64_t s = 0x5EED0003ull;
+	for (size_t i = 0; i < n; i++) {
+		s ^= s << 13; s ^= s >> 7; s ^= s << 17;
+		if ((s >> 32) % 12 >= 7)   /* the 570 / 1500-byte frames of IMIX */
+			idx.push_back((uint32_t)i);
+	}
+	uint32_t *d_idx;
+	CK(hipMalloc(&d_idx, idx.size() * 4));
+	CK(hipMemcpy(d_idx, idx.data(), idx.size() * 4, hipMemcpyHostToDevice));
+	hipEvent_t e0, e1, e2;
+	CK(hipEventCreate(&e0));
+	CK(hipEventCreate(&e1));
+	CK(hipEventCreate(&e2));
+	printf("records %zu, rewritten %zu (%.1f %%)\n", n, idx.size(), 100.0 * idx.size() / n);
+	for (int rep = 0; rep < 3; rep++)
+		for (int group = 0; group < 2; group++) {
+			CK(hipDeviceSynchronize());
+			CK(hipEventRecord(e0, 0));
+			hipLaunchKernelGGL(k_rec_all, dim3(8192), dim3(256), 0, 0, rec, n);
+			CK(hipEventRecord(e1, 0));
+			hipLaunchKernelGGL(k_rec_some, dim3(8192), dim3(256), 0, 0, rec, d_idx,
+					   idx.size(), group);
+			CK(hipEventRecord(e2, 0));
+			CK(hipEventSynchronize(e2));
+			float a, b;
+			CK(hipEventElapsedTime(&a, e0, e1));
+			CK(hipEventElapsedTime(&b, e1, e2));
+			printf("all-records %.4f ms, then %s %.4f ms (%zu B stored)\n", a,
+			       group ? "their 64-B groups whole" : "16 B a record  ", b,
+			       idx.size() * (group ? 64 : 16));
+		}
+	return 0;
+}
+
 int main(int argc, char **argv)
 {
+	if (argc > 1 && !strcmp(argv[1], "rec"))
+		return rec_main();
 	if (argc > 1 && !strcmp(argv[1], "imix"))
 		return imix_main();
 	if (argc > 1 && !strcmp(argv[1], "bulk"))
