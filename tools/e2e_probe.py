@@ -59,10 +59,38 @@ def main():
                     help="the box's pinned H2D GB/s (bench.py pcie_ceiling)")
     ap.add_argument("--d2h-ceil", type=float, default=57.0)
     ap.add_argument("--slots", default="2", help="batches in flight, e.g. 2,3,4")
+    ap.add_argument("--packed", action="store_true",
+                    help="the packed leg instead (config-2 frames at a 64 B stride, "
+                         "batches of 1 M, no chunk size)")
     args = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
     nc = args.frames
+    if args.packed:
+        cu, cd, ce = xdpgpu.pool_generate(nc, xdpgpu.POOL_UDP4, 64, 0x5EED0002)
+        for slots in (int(x) for x in args.slots.split(",")):
+            r = bench.e2e_run(0, cu, cd, ce, 1 << 20, args.batches, 0, 0,
+                              {"h2d_gbps": args.h2d_ceil, "d2h_gbps": args.d2h_ceil},
+                              xdpgpu.CFG_DEFAULT, slots)
+            r.pop("pcie_ceiling", None)
+            r["mode"] = "packed"
+            h = xdpgpu.XdpGpu(0, xdpgpu.CFG_DEFAULT, 0, xdpgpu.TUPLE_V4, 0, max_batch=1 << 20)
+            h.register_umem(cu, 0)
+            hd = xdpgpu.HostBuffer(1 << 20, xdpgpu.DESC_DTYPE)
+            hd.array[:] = cd[:1 << 20]
+            outs = [xdpgpu.HostBuffer(1 << 20, dt) for dt in (np.uint8, xdpgpu.RESULT_DTYPE,
+                                                             xdpgpu.TUPLE4_DTYPE)]
+            v, rr, t = (b.array for b in outs)
+            tot = 0.0
+            for _ in range(8):
+                t0 = time.perf_counter()
+                h.submit(0, hd.array, v, rr, t)
+                tot += time.perf_counter() - t0
+                h.wait(0)
+            h.close()
+            r["submit_host_ms"] = round(tot / 8 * 1e3, 3)
+            print(json.dumps(r), flush=True)
+        return
     cu, cd, ce = xdpgpu.pool_generate(nc, xdpgpu.POOL_UDP4, 64, 0x5EED0032, stride=4096,
                                       headroom=256)
     ceil = {"h2d_gbps": args.h2d_ceil, "d2h_gbps": args.d2h_ceil}
