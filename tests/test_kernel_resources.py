@@ -38,3 +38,14 @@ def test_rx_instances_occupancy():
     assert len(rx) >= 5
     for k, v in rx.items():
         assert v["vgpr"] <= 128, (k, v)
+
+
+def test_nat64_general_kernel_occupancy():
+    """nat64's general kernel, the reference's translation, is held to 4
+    waves a SIMD with its headers in registers (csrc/nat64.hip
+    __launch_bounds__)."""
+    ks = kres.kernels()
+    gen = {k: v for k, v in ks.items() if "xdp_nat64_kernelILb0E" in k}
+    assert gen
+    for k, v in gen.items():
+        assert v["vgpr"] <= 128 and not v["scratch"], (k, v)
