@@ -279,7 +279,12 @@ void xdpgpu_fini(xdpgpu_ctx *ctx)
 		if (p)
 			(void)hipFree(p);
 	if (ctx->pinned)
-		(void)hipHostUnregister(ctx->h_umem);
+		if (hipHostUnregister(ctx->h_umem) != hipSuccess)
+			/* another context's registration of the same memory
+			 * (several RX queues on one UMEM) may have gone first:
+			 * the failure must not linger as the thread's last
+			 * error, which the next launch check would report */
+			(void)hipGetLastError();
 	delete ctx;
 }
 
@@ -363,7 +368,12 @@ static void release_umem(xdpgpu_ctx *ctx)
 		s.mirror_cap = 0;
 	}
 	if (ctx->pinned)
-		(void)hipHostUnregister(ctx->h_umem);
+		if (hipHostUnregister(ctx->h_umem) != hipSuccess)
+			/* another context's registration of the same memory
+			 * (several RX queues on one UMEM) may have gone first:
+			 * the failure must not linger as the thread's last
+			 * error, which the next launch check would report */
+			(void)hipGetLastError();
 	ctx->pinned = false;
 	ctx->h_umem = nullptr;
 	ctx->d_hview = nullptr;

@@ -459,6 +459,37 @@ def udp_to_frame_end(umem, descs, length):
     descs["len"][descs["len"] >= length] = length
 
 
+def test_two_queues_share_a_umem():
+    """Two contexts (two RX queues) register the same UMEM, as the
+    reference's sockets share one; both run batches, one closes first, the
+    other still runs, and a context made afterwards runs too: a failed
+    second unregistration must not surface as the next launch's error."""
+    nframes = 4096
+    umem, descs, _ = xdpgpu.pool_generate(nframes, xdpgpu.POOL_UDP4, 64, 77)
+    want, _, _, _ = oracle.process(umem.copy(), descs, 0x5, 0, xdpgpu.TUPLE_V4)
+
+    def batch(ctx, lo, hi):
+        v, _, _ = ctx.process(descs[lo:hi], want_res=False, want_tup=False)
+        np.testing.assert_array_equal(v, want[lo:hi])
+
+    a = xdpgpu.XdpGpu(0, 0x5, 0, xdpgpu.TUPLE_V4, 0)
+    b = xdpgpu.XdpGpu(0, 0x5, 0, xdpgpu.TUPLE_V4, 0)
+    try:
+        a.register_umem(umem)
+        b.register_umem(umem)
+        batch(a, 0, 2048)
+        batch(b, 2048, 4096)
+        a.close()
+        batch(b, 0, 4096)
+        b.close()
+        with xdpgpu.XdpGpu(0, 0x5, 0, xdpgpu.TUPLE_V4, 0) as c:
+            c.register_umem(umem.copy())
+            batch(c, 0, 4096)
+    finally:
+        a.close()
+        b.close()
+
+
 def test_gather_descs_inside_pinned_buffer():
     """The gather reads page-locked descriptors through their GPU mapping:
     a batch handed over as a slice from the middle of a page-locked array

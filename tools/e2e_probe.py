@@ -49,6 +49,69 @@ def submit_cost(cu, cd, B, flags, reps=8):
     return tot / reps
 
 
+def e2e_queues(umem, descs, expect, queues: int, batches: int, B: int = 1 << 20,
+               local: int = 0) -> dict:
+    """Q RX queues on one GPU, as the reference runs one socket per queue:
+    Q contexts on the same UMEM, each driven by its own thread (ctypes
+    releases the GIL in the library), two batches in flight on each; the
+    batches dealt round robin.  Aggregate frames / wall time."""
+    import threading
+    per = len(descs) // B
+    ctxs, bufs = [], []
+    for q in range(queues):
+        h = xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT, 0, xdpgpu.TUPLE_V4, 0, max_batch=B)
+        h.register_umem(umem, 0)
+        hd = xdpgpu.HostBuffer(per * B, xdpgpu.DESC_DTYPE)
+        hd.array[:] = descs[: per * B]
+        outs = [[xdpgpu.HostBuffer(B, dt) for dt in (np.uint8, xdpgpu.RESULT_DTYPE,
+                                                     xdpgpu.TUPLE4_DTYPE)] for _ in range(2)]
+        ctxs.append(h)
+        bufs.append((hd, outs))
+    oks = [True] * queues
+
+    def run(q, nb, check):
+        h, (hd, outs) = ctxs[q], bufs[q]
+        pending = [None, None]
+        for k in range(nb + 2):
+            slot = k & 1
+            if pending[slot] is not None:
+                h.wait(slot)
+                if check:
+                    lo = pending[slot]
+                    oks[q] &= bool(np.array_equal(outs[slot][0].array, expect[lo:lo + B]))
+                pending[slot] = None
+            if k >= nb:
+                continue
+            lo = ((k * queues + q) % per) * B
+            v, r, t = (b.array for b in outs[slot])
+            h.submit(slot, hd.array[lo:lo + B], v, r, t)
+            pending[slot] = lo
+
+    def once(check):
+        ths = [threading.Thread(target=run, args=(q, batches // queues, check))
+               for q in range(queues)]
+        t0 = time.perf_counter()
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        return time.perf_counter() - t0
+
+    once(True)
+    te = once(False)
+    for h in ctxs:
+        h.close()
+    for hd, outs in bufs:
+        hd.close()
+        for o in outs:
+            for b in o:
+                b.close()
+    fr = (batches // queues) * queues * B
+    return {"queues": queues, "frames": fr, "batch": B, "mpps": round(fr / te / 1e6, 1),
+            "h2d_gbps": round(fr * 80 / te / 1e9, 1), "d2h_gbps": round(fr * 33 / te / 1e9, 1),
+            "verdicts_ok": all(oks)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=1 << 20)
@@ -59,6 +122,9 @@ def main():
                     help="the box's pinned H2D GB/s (bench.py pcie_ceiling)")
     ap.add_argument("--d2h-ceil", type=float, default=57.0)
     ap.add_argument("--slots", default="2", help="batches in flight, e.g. 2,3,4")
+    ap.add_argument("--queues", type=int, default=1,
+                    help="RX queues: contexts, each driven by its own thread over its "
+                         "share of the batches (packed leg)")
     ap.add_argument("--packed", action="store_true",
                     help="the packed leg instead (config-2 frames at a 64 B stride, "
                          "batches of 1 M, no chunk size)")
@@ -66,6 +132,10 @@ def main():
     import torch
     torch.cuda.set_device(0)
     nc = args.frames
+    if args.packed and args.queues > 1:
+        cu, cd, ce = xdpgpu.pool_generate(nc, xdpgpu.POOL_UDP4, 64, 0x5EED0002)
+        print(json.dumps(e2e_queues(cu, cd, ce, args.queues, args.batches)), flush=True)
+        return
     if args.packed:
         cu, cd, ce = xdpgpu.pool_generate(nc, xdpgpu.POOL_UDP4, 64, 0x5EED0002)
         for slots in (int(x) for x in args.slots.split(",")):
