@@ -169,9 +169,13 @@ def test_tx_only_write_back():
     assert np.array_equal(host, ou)
 
 
-def test_frags_ring_host_path():
+@pytest.mark.parametrize("gather", [False, True], ids=["copies", "gather"])
+def test_frags_ring_host_path(gather):
     """Multi-buffer packets on the host path, two slots in flight, echo on:
-    every fragment's bytes only as the oracle writes them."""
+    every fragment's bytes only as the oracle writes them.  With the gather
+    (the UMEM registered with a chunk size) every fragment takes the byte
+    after it, so the packet's over-read byte after its last fragment is
+    there."""
     import test_frags as TF
     umem, descs = TF.pool("echo6")
     u2, d2, _ = TF.split_pool(umem, descs, 3)
@@ -183,8 +187,11 @@ def test_frags_ring_host_path():
     for p0 in range(0, len(heads), per):
         batches.append(np.arange(bounds[p0], bounds[min(p0 + per, len(heads))]))
     host = u2.copy()
-    got, st = run_ring(host, d2, batches, ECHO | xdpgpu.CFG_FRAGS, 0,
-                       fmt=xdpgpu.TUPLE_V4)
+    hs = {}
+    got, st = run_ring(host, d2, batches,
+                       ECHO | xdpgpu.CFG_FRAGS | (xdpgpu.CFG_UMEM_GATHER if gather else 0), 0,
+                       fmt=xdpgpu.TUPLE_V4, chunk=4096 if gather else 0, host_stats=hs)
+    assert hs["umem_gathers"] == (len(batches) if gather else 0), hs
     ou = u2.copy()
     want, ost = oracle_ring(ou, d2, batches, ECHO | xdpgpu.CFG_FRAGS, fmt=xdpgpu.TUPLE_V4)
     for k, (g, w) in enumerate(zip(got, want)):
