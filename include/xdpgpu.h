@@ -192,8 +192,9 @@ void xdpgpu_fini(struct xdpgpu_ctx *ctx);
 
 /* Register the host UMEM (replaces xsk_umem__create's buffer argument,
  * af_xdp_user.c:433 / xdpsock.c:1013).  The memory stays owned by the caller;
- * it is pinned (hipHostRegister, for the copy engines only) and each
- * in-flight slot keeps a device mirror of it.  chunk_size (aligned mode, a
+ * it is pinned (hipHostRegister: for the copy engines, and with
+ * XDPGPU_CFG_UMEM_GATHER for the gather kernel's reads) and each in-flight
+ * slot keeps a device mirror of it.  chunk_size (aligned mode, a
  * power of two, 0: none) lets the host path copy only each chunk's window
  * of frame bytes (xdpgpu_host_stats).  -EBUSY while a slot is in flight. */
 int xdpgpu_register_umem(struct xdpgpu_ctx *ctx, void *base, uint64_t size,
