@@ -36,6 +36,7 @@ with SYN-ACKs).
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import subprocess
@@ -56,6 +57,9 @@ import xdpgpu  # noqa: E402
 BYTES_PER_FRAME = 16 + 64 + 16 + 16 + 1   # desc + frame + result + tuple + verdict
 RX_KERNELS = ("xdp_rx_db_kernel",)
 HBM_PEAK_GBS = 8000.0                      # MI355X HBM3E, MI355X_MICROARCH.md
+# the rendezvous and every control collective of the N-rank path end with
+# an error after this long instead of hanging (XDPGPU_BENCH_PG_TIMEOUT)
+PG_TIMEOUT_S = int(os.environ.get("XDPGPU_BENCH_PG_TIMEOUT", "600"))
 METRIC = ("Mpps + GB/s device-resident parse+csum+jhash, 64B & 1500B frames, "
           "1/2/4/8 GPU")
 
@@ -90,34 +94,67 @@ def settle(dev, stream):
     torch.cuda.synchronize()
 
 
-def time_device(ctx, d_umem, usize, d_desc, n, d_v, d_res, d_tup, stream,
-                steps, warmup, world):
-    """W untimed + K timed launches between barrier + synchronize; returns
-    wall seconds.  The launches go to the context's own stream (stream
-    None), as an RX loop over one context does: a caller's stream costs
-    the library an event record per launch (xdpgpu.cpp scratch_leave)."""
+def out_sets(n: int, tuple_bytes: int, dev, sets: int = 2) -> list:
+    """One (verdict, record, tuple) output set per slot in flight."""
+    return [(torch.empty(n, dtype=torch.uint8, device=dev),
+             torch.empty(n * 16, dtype=torch.uint8, device=dev),
+             torch.empty(n * tuple_bytes, dtype=torch.uint8, device=dev))
+            for _ in range(sets)]
+
+
+def time_device(ctx, d_umem, usize, d_desc, n, outs, steps, warmup, world):
+    """W untimed + K timed launches between barrier + synchronize, as a
+    device-resident RX loop keeps two batches in flight: launch k goes to
+    slot k mod 2 (xdpgpu_submit_dev: that slot's stream and scratch) with
+    that slot's output set, so that a launch starts on the CUs the one
+    before leaves while its last tiles finish.  Returns
+    (wall seconds, GPU span of the K timed launches in ms): one event on
+    slot 0's stream before the first launch (slot 1's stream waits for it)
+    and one on each slot's stream after the last, none between launches."""
+    dev = d_umem.device
+    ss = [torch.cuda.ExternalStream(ctx.slot_stream(i), device=dev) for i in range(2)]
+
+    def launch(k):
+        v, r, t = outs[k & 1]
+        ctx.submit_dev(k & 1, d_umem, usize, d_desc, n, v, r, t)
+
     torch.cuda.synchronize()   # the inputs, made on torch's streams
-    for _ in range(warmup):
-        ctx.process_dev(d_umem, usize, d_desc, n, d_v, d_res, d_tup, stream)
+    for k in range(warmup):
+        launch(k)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = [torch.cuda.Event(enable_timing=True) for _ in ss]
+    e0.record(ss[0])
+    ss[1].wait_event(e0)
     t0 = time.perf_counter()
-    for _ in range(steps):
-        ctx.process_dev(d_umem, usize, d_desc, n, d_v, d_res, d_tup, stream)
+    for k in range(steps):
+        launch(k)
+    for e, st in zip(e1, ss):
+        e.record(st)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    span = max(e0.elapsed_time(e) for e in e1)
     if world > 1:
         dist.barrier()
-    return t1 - t0
+    return t1 - t0, span
+
+
+def outputs_ok(outs, expect) -> bool:
+    """Every slot's verdicts equal the generator's (both output sets were
+    written by timed launches)."""
+    return all(bool(np.array_equal(v.cpu().numpy(), expect)) for v, _, _ in outs)
 
 
 def kernel_breakdown(tctx, d_umem, usize, d_desc, n, d_v, d_res, d_tup, stream,
                      steps):
     """Per-kernel average ms from the HIP events the library records on the
-    launch stream around each kernel (a context with CFG_TIMING; a pass of
-    its own, so the events do not perturb the timed steps)."""
+    launch stream around each kernel (a context with CFG_TIMING; one launch
+    at a time on one stream, a pass of its own before the timed steps, so
+    the events do not perturb them: the kernel's own duration, which
+    rocprofv3 reports for these launches)."""
     tctx.process_dev(d_umem, usize, d_desc, n, d_v, d_res, d_tup, stream)
     torch.cuda.synchronize()
     tctx.kernel_times()
@@ -125,6 +162,37 @@ def kernel_breakdown(tctx, d_umem, usize, d_desc, n, d_v, d_res, d_tup, stream,
         tctx.process_dev(d_umem, usize, d_desc, n, d_v, d_res, d_tup, stream)
     torch.cuda.synchronize()
     return tctx.kernel_times()
+
+
+def device_identity(local: int) -> dict:
+    """What this rank runs on: the device's PCI bus id and UUID (the
+    distinct-device check), its name, and the RCCL version torch carries
+    (the "nccl" backend is RCCL on ROCm)."""
+    p = torch.cuda.get_device_properties(local)
+    try:
+        rccl = ".".join(str(x) for x in torch.cuda.nccl.version())
+    except Exception as e:  # noqa: BLE001 (reported, not fatal: gloo runs)
+        rccl = f"unavailable ({type(e).__name__})"
+    return {"local_rank": local, "name": p.name,
+            "pci_bus_id": f"{getattr(p, 'pci_domain_id', 0):04x}:{p.pci_bus_id:02x}:"
+                          f"{getattr(p, 'pci_device_id', 0):02x}",
+            "uuid": str(getattr(p, "uuid", "")), "rccl": rccl}
+
+
+def check_distinct_devices(idents: list, rehearse: bool) -> None:
+    """One rank per GPU: two ranks on one device would time each other's
+    launches as their own (the scaling curve would be wrong, not slow), so
+    unless rehearsing that is an error naming the ranks."""
+    if rehearse:
+        return
+    seen = {}
+    for r, d in enumerate(idents):
+        key = d.get("uuid") or d["pci_bus_id"]
+        if key in seen:
+            raise SystemExit(f"ranks {seen[key]} and {r} share device {d['pci_bus_id']} "
+                             f"({key}): one rank per GPU (XDPGPU_BENCH_REHEARSE=1 rehearses "
+                             "ranks sharing GPUs)")
+        seen[key] = r
 
 
 def cpu_model() -> str:
@@ -256,23 +324,25 @@ def cpu_legs(oracle) -> dict:
 
 
 def pmc_traffic(n: int, size: int):
-    """HBM bytes per RX launch from the committed rocprofv3 PMC summary
-    (profiles/*_pmc.json, tools/pmc_profile.sh + tools/pmc_summary.py), if it
-    was taken on this workload; else None."""
+    """(HBM bytes per RX launch, source file) from the newest committed
+    rocprofv3 PMC summary of config 2 (profiles/r<NN>_pmc.json,
+    tools/pmc_profile.sh + tools/pmc_summary.py) when it was taken on this
+    workload, else (None, None).  It was measured on the committed kernel
+    of that round, not in this run."""
     import glob
     # the config-2 summaries only (r<NN>_pmc.json; the other workloads'
     # are r<NN>_pmc_<workload>.json)
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc.json")))
     if not files:
-        return None
+        return None, None
     try:
         with open(files[-1]) as f:
             d = json.load(f)
         if d.get("frames") != n or d.get("frame_size") != size:
-            return None
-        return d.get("hbm_bytes_per_launch")
+            return None, None
+        return d.get("hbm_bytes_per_launch"), "profiles/" + os.path.basename(files[-1])
     except Exception:
-        return None
+        return None, None
 
 
 def pmc_leg_traffic(pattern: str, frames: int):
@@ -304,7 +374,10 @@ def attach_traffic(leg: dict, pattern: str, frames: int) -> dict:
                                       leg["algorithmic_bytes_per_launch"], 3)
         t["hbm_bytes_per_launch"] = int(t["hbm_bytes_per_launch"])
     if t:
-        leg["traffic"] = t
+        # measured by rocprofv3 --pmc on the committed kernel of the
+        # profile's round, not in this run (hence its own key)
+        t["source"] = "profiles/" + t["source"]
+        leg["committed_pmc_traffic"] = t
     return leg
 
 
@@ -322,12 +395,16 @@ def kt_round(kt: dict) -> dict:
 
 
 def side_run(ctx, tctx, dev, stream, n, kind, size, seed, fmt, steps, label, bpf_fn,
-             replicate=1):
-    """One secondary workload: pool, K timed launches, kernel split,
+             replicate=1, world=1, rank=0):
+    """One secondary workload: pool, kernel event pass, K timed launches
+    (two slots in flight, barrier-bracketed over the ranks when world > 1),
     verdict check.  replicate > 1: a pool of n frames is generated on the
     host and laid down `replicate` times back to back in HBM (descriptors
     offset by the copy's base), so that a multi-GB pool costs one host
-    generation and copy; n * replicate frames are processed per launch."""
+    generation and copy; n * replicate frames are processed per launch.
+    With world > 1 every rank runs its own shard (the caller offsets the
+    seed by rank) and the rate is all ranks' frames over the slowest rank's
+    time, as for config 2; `per_rank` lists each rank's numbers."""
     u, ds, ex = xdpgpu.pool_generate(n, kind, size, seed)
     if replicate > 1:
         g_umem = torch.empty(u.nbytes * replicate + 64, dtype=torch.uint8, device=dev)
@@ -342,31 +419,49 @@ def side_run(ctx, tctx, dev, stream, n, kind, size, seed, fmt, steps, label, bpf
         ds, ex, n = rd, np.tile(ex, replicate), n * replicate
     else:
         g_umem = to_dev(u, dev)
+    del u
     g_desc = to_dev(ds, dev, 0)
-    tb = xdpgpu.TUPLE_BYTES[fmt]
-    g_v = torch.empty(n, dtype=torch.uint8, device=dev)
-    g_res = torch.empty(n * 16, dtype=torch.uint8, device=dev)
-    g_tup = torch.empty(n * tb, dtype=torch.uint8, device=dev)
+    outs = out_sets(n, xdpgpu.TUPLE_BYTES[fmt], dev)
     usize = g_umem.numel() - 64
-    w = time_device(ctx, g_umem, usize, g_desc, n, g_v, g_res, g_tup,
-                    None, steps, 2, 1)
-    kt = kernel_breakdown(tctx, g_umem, usize, g_desc, n, g_v, g_res, g_tup,
-                          None, steps)
-    ok = bool(np.array_equal(g_v.cpu().numpy(), ex))
+    kt = kernel_breakdown(tctx, g_umem, usize, g_desc, n, *outs[0], None, steps)
+    w, span = time_device(ctx, g_umem, usize, g_desc, n, outs, steps, 2, world)
+    ok = outputs_ok(outs, ex)
     algo = bpf_fn(ds)
-    out = {"workload": label, "frames": n,
-           "mpps": round(n * steps / w / 1e6, 1),
+    mine = {"rank": rank, "ms_per_launch": round(w / steps * 1e3, 4),
+            "gpu_span_ms_per_launch": round(span / steps, 4),
+            "mpps": round(n * steps / w / 1e6, 1), "verdicts_ok": ok}
+    per_rank = gather_ranks(mine, world)
+    w_max = max(r["ms_per_launch"] for r in per_rank) * steps * 1e-3
+    span_max = max(r["gpu_span_ms_per_launch"] for r in per_rank)
+    out = {"workload": label, "frames": n, "n_gpus": world,
+           "mpps": round(n * world * steps / w_max / 1e6, 1),
            "algorithmic_bytes_per_launch": int(algo),
-           "ms_per_launch": round(w / steps * 1e3, 4),
-           "gbps": round(algo / w * steps / 1e9, 1),
-           "roofline_frac": round(algo / w * steps / 1e9 / HBM_PEAK_GBS, 4),
-           # the same bytes over the HIP-event launch time (kernel_times()
-           # averages over its launches)
+           "ms_per_launch": round(w_max / steps * 1e3, 4),
+           "gbps": round(algo * world / w_max * steps / 1e9, 1),
+           "roofline_frac": round(algo / w_max * steps / 1e9 / HBM_PEAK_GBS, 4),
+           # the same bytes over the timed launches' GPU span (events at
+           # the ends of the K launches only)
+           "roofline_frac_span": round(algo / (span_max * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           # and over the kernel's own duration (its event pair, one launch
+           # at a time: kernel_times() averages over its launches)
            "roofline_frac_kernel": round(algo / (kt["total_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-           "kernel_ms": kt_round(kt), "verdicts_ok": ok}
-    del g_umem, g_desc, g_v, g_res, g_tup
+           "kernel_ms": kt_round(kt),
+           "verdicts_ok": all(r["verdicts_ok"] for r in per_rank)}
+    if world > 1:
+        out["per_rank"] = per_rank
+    del g_umem, g_desc, outs
     torch.cuda.empty_cache()
     return out
+
+
+def gather_ranks(mine: dict, world: int) -> list:
+    """Every rank's small result dict, in rank order (all_gather_object;
+    the rank's own alone at world 1)."""
+    if world <= 1:
+        return [mine]
+    got = [None] * world
+    dist.all_gather_object(got, mine)
+    return got
 
 
 def nat64_run(dev, stream, n, steps, local):
@@ -548,13 +643,11 @@ def frags_run(dev, stream, n, steps, local, size=9000, chunk=4096):
     m = len(fd)
     g_umem = to_dev(u, dev)
     g_desc = to_dev(fd, dev, 0)
-    g_v = torch.empty(m, dtype=torch.uint8, device=dev)
-    g_res = torch.empty(m * 16, dtype=torch.uint8, device=dev)
-    g_tup = torch.empty(m * 16, dtype=torch.uint8, device=dev)
+    outs = out_sets(m, 16, dev)
     with xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT | xdpgpu.CFG_FRAGS, 0, xdpgpu.TUPLE_V4,
                        64) as g:
-        w = time_device(g, g_umem, u.nbytes, g_desc, m, g_v, g_res, g_tup, None, steps, 2, 1)
-    ok = bool(np.array_equal(g_v.cpu().numpy(), ex[frame_of]))
+        w, _ = time_device(g, g_umem, u.nbytes, g_desc, m, outs, steps, 2, 1)
+    ok = outputs_ok(outs, ex[frame_of])
     t = w / steps
     out = {"workload": f"{n} x {size}B IPv4/UDP packets in {chunk}B fragments "
                        f"({m} descriptors), XDPGPU_CFG_FRAGS",
@@ -565,7 +658,7 @@ def frags_run(dev, stream, n, steps, local, size=9000, chunk=4096):
     algo = m * (16 + 1 + 16 + 16) + int(lens.sum())
     out.update({"algorithmic_bytes_per_launch": algo, "gbps": round(algo / t / 1e9, 1),
                 "roofline_frac": round(algo / t / 1e9 / HBM_PEAK_GBS, 4)})
-    del g_umem, g_desc, g_v, g_res, g_tup
+    del g_umem, g_desc, outs
     torch.cuda.empty_cache()
     return out
 
@@ -853,6 +946,8 @@ def main():
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--legs", default="1500,imix,nat64,frags,echo,synproxy",
                     help="secondary workloads: comma list of 1500, imix, nat64, frags, echo")
+    ap.add_argument("--frames-1500", type=int, default=2 << 20,
+                    help="1500 B frames generated per GPU, laid down 8x in HBM")
     ap.add_argument("--imix-frames", type=int, default=16 << 20)
     ap.add_argument("--nat64-frames", type=int, default=16 << 20)
     ap.add_argument("--tune", type=lambda x: int(x, 0), default=0,
@@ -882,9 +977,17 @@ def main():
     if rehearse:
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)      # before RCCL binds the rank
+    ident = device_identity(local)
     if world > 1:
-        dist.init_process_group("gloo" if rehearse else "nccl")
+        # an explicit timeout: a rank that never arrives (a dead device, a
+        # rendezvous that cannot resolve) ends the job with an error
+        # instead of a hang
+        dist.init_process_group("gloo" if rehearse else "nccl",
+                                timeout=datetime.timedelta(seconds=PG_TIMEOUT_S))
     dev = torch.device("cuda", local)
+    idents = gather_ranks(ident, world)
+    check_distinct_devices(idents, rehearse)
+    log(f"[rank {rank}] {ident}")
 
     # config 2 shard (config 5 at N > 1: same per-GPU content, seed offset)
     t = time.time()
@@ -894,46 +997,58 @@ def main():
     log(f"[rank {rank}] pool {n} x {args.size} B generated in {time.time() - t:.1f} s")
     d_umem = to_dev(umem, dev)
     d_desc = to_dev(descs, dev, 0)
-    d_v = torch.empty(n, dtype=torch.uint8, device=dev)
-    d_res = torch.empty(n * 16, dtype=torch.uint8, device=dev)
-    d_tup = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    outs = out_sets(n, 16, dev)
     ctx = xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT, 0, xdpgpu.TUPLE_V4, args.window)
     tctx = xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT | xdpgpu.CFG_TIMING, 0,
                          xdpgpu.TUPLE_V4, args.window)
     stream = torch.cuda.Stream(dev)
 
-    wall = time_device(ctx, d_umem, umem.nbytes, d_desc, n, d_v, d_res, d_tup,
-                       None, args.steps, args.warmup, world)
-    kt = kernel_breakdown(tctx, d_umem, umem.nbytes, d_desc, n, d_v, d_res, d_tup,
-                          None, args.steps)
+    # the kernel's own duration first (one launch at a time, an event pair
+    # around each), then the W warmup and K timed steps
+    kt = kernel_breakdown(tctx, d_umem, umem.nbytes, d_desc, n, *outs[0], None, args.steps)
     kms = kt["total_ms"]
+    wall, span = time_device(ctx, d_umem, umem.nbytes, d_desc, n, outs, args.steps,
+                             args.warmup, world)
     # correctness spot check of the timed outputs against the generator
-    v = d_v.cpu().numpy()
-    ok = bool(np.array_equal(v, expect))
+    ok = outputs_ok(outs, expect)
     # max time / summed frames over ranks (no data-path collective)
     wall_max, total_frames, all_ok = shard.reduce_timing(wall, n * args.steps, ok,
                                                          None if rehearse else dev)
+    per_rank = gather_ranks({"rank": rank, "device": ident["pci_bus_id"],
+                             "ms_per_step": round(wall / args.steps * 1e3, 4),
+                             "gpu_span_ms_per_step": round(span / args.steps, 4),
+                             "kernel_ms": round(kms, 4),
+                             "mpps": round(n * args.steps / wall / 1e6, 1),
+                             "verdicts_ok": ok}, world)
+    span_step = max(r["gpu_span_ms_per_step"] for r in per_rank)
     mpps = total_frames / wall_max / 1e6
     gbps = total_frames * BYTES_PER_FRAME / wall_max / 1e9
-    achieved = BYTES_PER_FRAME * n / (kms * 1e-3) / 1e9
+    # per GPU, over the timed launches: the slowest rank's GPU span a step
+    achieved = BYTES_PER_FRAME * n / (span_step * 1e-3) / 1e9
 
     secondary = {}
-    if not args.no_secondary and rank == 0 and world == 1:
-        del d_umem
+    if not args.no_secondary:
+        del d_umem, outs
         torch.cuda.empty_cache()
         steps2 = max(5, args.steps // 5)
         legs = set(args.legs.split(","))
         if "1500" in legs:
-            # 1500 B frames (BASELINE metric names both sizes), config 2 geometry
-            # 16 M frames as config 2 (25 GB: 2 M generated, laid down 8x)
+            # 1500 B frames (BASELINE metric names both sizes at 1/2/4/8
+            # GPUs), config 2 geometry, 16 M frames per GPU as config 2
+            # (25 GB: 2 M generated, laid down 8x); every rank its own
+            # shard, seed offset by rank
             secondary["secondary_1500B"] = side_run(
-                ctx, tctx, dev, stream, 2 << 20, xdpgpu.POOL_UDP4, 1500, 0x5EED0012,
-                xdpgpu.TUPLE_V4, steps2,
-                "config2-geometry 16M x 1500B IPv4/UDP (a 2M-frame pool laid down 8x), V4 tuple",
+                ctx, tctx, dev, stream, args.frames_1500, xdpgpu.POOL_UDP4, 1500,
+                shard.shard_seed(0x5EED0012, rank), xdpgpu.TUPLE_V4, steps2,
+                f"config2-geometry {8 * args.frames_1500} x 1500B IPv4/UDP per GPU (a "
+                f"{args.frames_1500}-frame pool laid down 8x), V4 tuple",
                 lambda ds: len(ds) * (16 + 16 + 16 + 1) + int(ds["len"].astype(np.int64).sum()),
-                replicate=8)
+                replicate=8, world=world, rank=rank)
             attach_traffic(secondary["secondary_1500B"], "r[0-9][0-9]_pmc_1500_w128.json",
-                           16 << 20)
+                           8 * args.frames_1500)
+        # the single-GPU configurations (BASELINE configs 3 and 4) and the
+        # other modes: rank 0 at N = 1 only
+        legs = legs if world == 1 else set()
         if "imix" in legs:
             # config 3: IMIX with the 44 B network_tuple (429.3 B/frame)
             ctx3 = xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT, 0, xdpgpu.TUPLE_NET, args.window)
@@ -1001,7 +1116,8 @@ def main():
         cpu = cpu_baseline(umem, descs, xdpgpu.CFG_DEFAULT, xdpgpu.TUPLE_V4)
 
     if rank == 0:
-        traffic = pmc_traffic(n, args.size)
+        traffic, traffic_src = pmc_traffic(n, args.size)
+        kernel_frac = BYTES_PER_FRAME * n / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS
         line = {
             "metric": METRIC,
             "value": round(mpps, 1),
@@ -1021,20 +1137,34 @@ def main():
                        "frames_per_gpu": n, "frame_size": args.size,
                        "header_window": args.window or (128 if args.size >= 128 else 64),
                        "parallelism": f"shard{world}",
+                       "in_flight": "2 launches (xdpgpu_submit_dev, two slots)",
                        **({"rehearsal": "ranks sharing GPUs, gloo"} if rehearse else {})},
             "gbps": round(gbps, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         # algorithmic bytes of a launch over the timed
+                         # launches' GPU span a step (events at the two ends
+                         # of the K timed launches; the slowest rank)
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "timed_span_ms_per_launch": span_step,
                          # the same bytes over the timed wall time per step
-                         # (back-to-back launches, the driver's clock)
+                         # (host clock around the K launches, the driver's)
                          "frac_wall": round(BYTES_PER_FRAME * n * args.steps / wall_max / 1e9 /
                                             HBM_PEAK_GBS, 4),
+                         # and over the kernel's own duration, one launch at
+                         # a time between its event pair (what rocprofv3
+                         # reports for those launches)
+                         "frac_kernel": round(kernel_frac, 4),
                          "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernels": "+".join(RX_KERNELS),
                          "kernel_ms": kt_round(kt),
                          "bytes_per_frame": BYTES_PER_FRAME,
                          "algorithmic_bytes_per_launch": BYTES_PER_FRAME * n},
+            "per_rank": per_rank,
+            "devices": {"pci_bus_ids": [d["pci_bus_id"] for d in idents],
+                        "name": ident["name"], "rccl": ident["rccl"],
+                        "backend": ("gloo" if rehearse else "nccl") if world > 1 else None},
             "cpu_baseline": cpu,
             "verdicts_ok": all_ok,
         }

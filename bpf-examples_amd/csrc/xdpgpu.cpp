@@ -75,6 +75,8 @@ struct Slot {
 	hipStream_t scr_last = nullptr;
 	bool scr_lazy = false;
 	bool busy = false;
+	/* a device batch (xdpgpu_submit_dev) enqueued since the last wait */
+	bool dev_pending = false;
 	/* pending host copies for xdpgpu_wait() */
 	uint32_t n = 0;
 };
@@ -88,7 +90,10 @@ struct xdpgpu_ctx {
 	/* registered host UMEM */
 	uint8_t *h_umem = nullptr;
 	uint64_t umem_size = 0;
+	/* the UMEM is page-locked by a registration this context holds a
+	 * reference on (hostreg_acquire): the base of that registration */
 	bool pinned = false;
+	uintptr_t reg_key = 0;
 	/* aligned-mode chunk size (a power of two) when register_umem gave
 	 * one, else 0: the host path then copies rows of chunks */
 	uint32_t chunk = 0;
@@ -205,6 +210,69 @@ static void free_slot(Slot &s)
 	s = Slot();
 }
 
+/* Host registrations of UMEMs, process-wide and counted.  Several RX
+ * queues share one UMEM (the reference's sockets on one xsk_umem,
+ * af_xdp_user.c:1542-1611), so several contexts register the same memory;
+ * HIP keeps one registration per range, and the first hipHostUnregister
+ * would tear it down under the others (their copies would lose the
+ * pinning, and XDPGPU_CFG_UMEM_GATHER's device view would dangle).  A
+ * context takes a reference on the registration that covers its range, or
+ * makes one; the last reference unregisters.  Memory the caller pinned
+ * (xdpgpu_host_alloc, or its own registration) cannot be registered again:
+ * the context then holds nothing and the caller owns the pinning. */
+struct HostReg {
+	uint64_t size;
+	uint32_t refs;
+};
+static std::mutex g_regmu;
+static std::map<uintptr_t, HostReg> g_regs;
+
+static bool hostreg_acquire(void *base, uint64_t size, uintptr_t *key)
+{
+	std::lock_guard<std::mutex> lk(g_regmu);
+	const uintptr_t b = (uintptr_t)base;
+	auto it = g_regs.upper_bound(b);
+	if (it != g_regs.begin()) {
+		--it;
+		if (b >= it->first && b + size <= it->first + it->second.size) {
+			it->second.refs++;
+			*key = it->first;
+			return true;
+		}
+	}
+	if (hipHostRegister(base, size, hipHostRegisterDefault) != hipSuccess) {
+		(void)hipGetLastError();
+		return false;
+	}
+	g_regs[b] = HostReg{size, 1};
+	*key = b;
+	return true;
+}
+
+static void hostreg_release(uintptr_t key)
+{
+	std::lock_guard<std::mutex> lk(g_regmu);
+	auto it = g_regs.find(key);
+	if (it == g_regs.end() || --it->second.refs)
+		return;
+	if (hipHostUnregister((void *)key) != hipSuccess)
+		(void)hipGetLastError();
+	g_regs.erase(it);
+}
+
+/* Diagnostic for the tests: the live registrations' reference counts
+ * summed over those covering p (0: none). */
+int xdpgpu_host_pin_refs(const void *p)
+{
+	std::lock_guard<std::mutex> lk(g_regmu);
+	const uintptr_t b = (uintptr_t)p;
+	int refs = 0;
+	for (const auto &r : g_regs)
+		if (b >= r.first && b < r.first + r.second.size)
+			refs += (int)r.second.refs;
+	return refs;
+}
+
 /* Per-queue counters: the live contexts, and the counters of finished ones
  * by queue (xdpgpu_queue_stats). */
 static std::mutex g_qmu;
@@ -279,12 +347,7 @@ void xdpgpu_fini(xdpgpu_ctx *ctx)
 		if (p)
 			(void)hipFree(p);
 	if (ctx->pinned)
-		if (hipHostUnregister(ctx->h_umem) != hipSuccess)
-			/* another context's registration of the same memory
-			 * (several RX queues on one UMEM) may have gone first:
-			 * the failure must not linger as the thread's last
-			 * error, which the next launch check would report */
-			(void)hipGetLastError();
+		hostreg_release(ctx->reg_key);
 	delete ctx;
 }
 
@@ -368,13 +431,9 @@ static void release_umem(xdpgpu_ctx *ctx)
 		s.mirror_cap = 0;
 	}
 	if (ctx->pinned)
-		if (hipHostUnregister(ctx->h_umem) != hipSuccess)
-			/* another context's registration of the same memory
-			 * (several RX queues on one UMEM) may have gone first:
-			 * the failure must not linger as the thread's last
-			 * error, which the next launch check would report */
-			(void)hipGetLastError();
+		hostreg_release(ctx->reg_key);
 	ctx->pinned = false;
+	ctx->reg_key = 0;
 	ctx->h_umem = nullptr;
 	ctx->d_hview = nullptr;
 	ctx->umem_size = 0;
@@ -429,10 +488,7 @@ int xdpgpu_register_umem(xdpgpu_ctx *ctx, void *base, uint64_t size,
 	 * GPU mapping, with LDS-DMA and non-temporal loads).  Only the
 	 * opt-in gather (XDPGPU_CFG_UMEM_GATHER, chunked UMEMs) reads it
 	 * there, with plain loads. */
-	if (hipHostRegister(base, size, hipHostRegisterDefault) == hipSuccess)
-		ctx->pinned = true;
-	else
-		(void)hipGetLastError();
+	ctx->pinned = hostreg_acquire(base, size, &ctx->reg_key);
 	if ((ctx->cfg.flags & XDPGPU_CFG_UMEM_GATHER) && ctx->chunk) {
 		/* memory pinned here or by the caller (xdpgpu_host_alloc) */
 		void *p = nullptr;
@@ -714,6 +770,39 @@ int xdpgpu_process_dev(xdpgpu_ctx *ctx, void *d_umem, uint64_t umem_size,
 	hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
 	return enqueue_rx(ctx, ctx->slot[0], (uint8_t *)d_umem, umem_size,
 			  d_descs, n, d_verdict, d_res, (uint8_t *)d_tuples, st);
+}
+
+/* The device-resident RX loop with two batches in flight: slot `slot`'s
+ * stream and scratch, so that the other slot's launch can take the CUs
+ * this one leaves while its last tiles finish (one block per CU: the next
+ * launch's block starts on a CU as soon as this one's has left it). */
+int xdpgpu_submit_dev(xdpgpu_ctx *ctx, uint32_t slot, void *d_umem, uint64_t umem_size,
+		      const xdpgpu_desc *d_descs, uint32_t n, uint8_t *d_verdict,
+		      xdpgpu_result *d_res, void *d_tuples)
+{
+	if (!ctx || slot >= kSlots || !d_umem || !d_descs || !d_verdict)
+		return -EINVAL;
+	Slot &s = ctx->slot[slot];
+	if (s.busy)
+		return set_err(ctx, -EBUSY, "slot %u has a host batch in flight", slot);
+	if (n == 0)
+		return 0;
+	int rc = check_dev_all(ctx, {{"UMEM", d_umem}, {"descriptors", d_descs},
+				     {"verdicts", d_verdict}, {"results", d_res},
+				     {"tuples", d_tuples}});
+	if (rc)
+		return rc;
+	HIP_TRY(ctx, hipSetDevice(ctx->cfg.device));
+	s.dev_pending = true;
+	return enqueue_rx(ctx, s, (uint8_t *)d_umem, umem_size, d_descs, n, d_verdict, d_res,
+			  (uint8_t *)d_tuples, s.stream);
+}
+
+void *xdpgpu_slot_stream(xdpgpu_ctx *ctx, uint32_t slot)
+{
+	if (!ctx || slot >= kSlots)
+		return nullptr;
+	return (void *)ctx->slot[slot].stream;
 }
 
 /* ---- nat64 ---- */
@@ -1508,6 +1597,11 @@ int xdpgpu_wait(xdpgpu_ctx *ctx, uint32_t slot)
 	if (!ctx || slot >= kSlots)
 		return -EINVAL;
 	Slot &s = ctx->slot[slot];
+	if (s.dev_pending) {
+		s.dev_pending = false;
+		HIP_TRY(ctx, hipSetDevice(ctx->cfg.device));
+		HIP_TRY(ctx, hipStreamSynchronize(s.stream));
+	}
 	if (!s.busy)
 		return 0;
 	s.busy = false;

@@ -174,7 +174,8 @@ EXPORTS = (
     "xdpgpu_host_free", "xdpgpu_jhash2_dev", "xdpgpu_jhash_nwords_dev",
     "xdpgpu_queue_stats", "xdpgpu_nat64_dynamic", "xdpgpu_nat64_clock",
     "xdpgpu_nat64_state", "xdpgpu_nat64_direction", "xdpgpu_synproxy_dev",
-    "xdpgpu_host_stats",
+    "xdpgpu_host_stats", "xdpgpu_host_pin_refs", "xdpgpu_submit_dev",
+    "xdpgpu_slot_stream",
 )
 
 # struct xdpgpu_hints (XDP hints in front of a frame)
@@ -236,6 +237,11 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     # (absent from libraries of earlier rounds, which A/B runs load)
     if hasattr(lib, "xdpgpu_host_stats"):
         lib.xdpgpu_host_stats.argtypes = [vp, C.POINTER(HostStats)]
+    if hasattr(lib, "xdpgpu_submit_dev"):
+        lib.xdpgpu_submit_dev.argtypes = [vp, u32, vp, u64, vp, u32, vp, vp, vp]
+        lib.xdpgpu_slot_stream.argtypes = [vp, u32]
+        lib.xdpgpu_slot_stream.restype = vp
+        lib.xdpgpu_host_pin_refs.argtypes = [vp]
     _lib = lib
     return lib
 
@@ -297,6 +303,12 @@ def queue_stats(queue_id: int) -> dict:
     if rc:
         raise XdpGpuError(f"xdpgpu_queue_stats: {os.strerror(-rc)} ({rc})")
     return s.as_dict()
+
+
+def host_pin_refs(a) -> int:
+    """How many contexts share the library's page-locking of a's memory
+    (xdpgpu_host_pin_refs)."""
+    return load_library().xdpgpu_host_pin_refs(_ptr(a))
 
 
 def device_count() -> int:
@@ -390,6 +402,23 @@ class XdpGpu:
         self._check(self.lib.xdpgpu_process_dev(
             self.h, _ptr(umem), umem_size, _ptr(descs), n, _ptr(verdict),
             _ptr(res), _ptr(tup), _stream_handle(stream)), "xdpgpu_process_dev")
+
+    def submit_dev(self, slot: int, umem, umem_size: int, descs, n: int, verdict,
+                   res=None, tup=None) -> None:
+        """The device-resident RX loop's double-buffered form
+        (xdpgpu_submit_dev): enqueued on slot `slot`'s stream; the two
+        slots' launches may overlap, wait(slot) or sync() waits."""
+        self._check(self.lib.xdpgpu_submit_dev(
+            self.h, slot, _ptr(umem), umem_size, _ptr(descs), n, _ptr(verdict),
+            _ptr(res), _ptr(tup)), "xdpgpu_submit_dev")
+
+    def slot_stream(self, slot: int) -> int:
+        """The hipStream_t of a slot (xdpgpu_slot_stream), e.g. for
+        torch.cuda.ExternalStream."""
+        p = self.lib.xdpgpu_slot_stream(self.h, slot)
+        if not p:
+            raise XdpGpuError(f"xdpgpu_slot_stream({slot}) failed")
+        return p
 
     def nat64_setup(self, cfg: Nat64Cfg, smap: np.ndarray) -> None:
         smap = np.ascontiguousarray(smap, NAT64_MAP_DTYPE)

@@ -256,6 +256,12 @@ struct xdpgpu_host_stats {
 };
 int xdpgpu_host_stats(struct xdpgpu_ctx *ctx, struct xdpgpu_host_stats *out);
 
+/* Diagnostic: how many contexts hold the library's page-locking of the
+ * host memory at p (several RX queues registering one UMEM share one
+ * registration, released by the last of them; 0: the library pins none,
+ * e.g. memory the caller page-locked itself). */
+int xdpgpu_host_pin_refs(const void *p);
+
 /* Device-resident form: every pointer is device memory (d_umem is written
  * only for ICMPv6 echo rewrites; a d_umem in host memory, pinned or not, is
  * refused with -EINVAL: no kernel of the library dereferences host
@@ -276,6 +282,27 @@ int xdpgpu_process_dev(struct xdpgpu_ctx *ctx, void *d_umem,
 		       uint32_t n, uint8_t *d_verdict,
 		       struct xdpgpu_result *d_res, void *d_tuples,
 		       void *stream);
+
+/* Double-buffered form of xdpgpu_process_dev: the device-resident RX loop
+ * with two batches in flight, as xdpgpu_submit is for host buffers (the
+ * reference's loop takes batch after batch off one RX ring,
+ * af_xdp_user.c:1079-1113 handle_receive_packets under rx_and_process).
+ * The launch goes to slot `slot`'s own stream with that slot's scratch, so
+ * a launch on the other slot can start on the CUs this one leaves while its
+ * last tiles finish; launches on one slot run in order.  Returns after the
+ * launch is enqueued (no host round trip); xdpgpu_wait(ctx, slot) or
+ * xdpgpu_sync(ctx, NULL) waits.  Batches in flight on the two slots must
+ * not write the same outputs or (with XDPGPU_CFG_ICMP6_ECHO) the same
+ * frames.  -EBUSY while the slot has a host batch (xdpgpu_submit) in
+ * flight.  Pointers and sizes as xdpgpu_process_dev. */
+int xdpgpu_submit_dev(struct xdpgpu_ctx *ctx, uint32_t slot, void *d_umem,
+		      uint64_t umem_size, const struct xdpgpu_desc *d_descs,
+		      uint32_t n, uint8_t *d_verdict, struct xdpgpu_result *d_res,
+		      void *d_tuples);
+
+/* The hipStream_t of a slot (NULL for a bad slot): a caller orders its own
+ * work (events, copies) with the slot's launches on it. */
+void *xdpgpu_slot_stream(struct xdpgpu_ctx *ctx, uint32_t slot);
 
 /* Counters accumulated over every launch of this context (synchronises). */
 int xdpgpu_stats(struct xdpgpu_ctx *ctx, struct xdpgpu_stats *out);

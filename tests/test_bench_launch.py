@@ -96,3 +96,48 @@ def test_gather_leg_child(monkeypatch):
         raise subprocess.TimeoutExpired(cmd, kw.get("timeout"))
     monkeypatch.setattr(bench.subprocess, "run", hang)
     assert "timed out" in bench.gather_leg(1 << 20, 32, ceil)["error"]
+
+
+def test_check_distinct_devices():
+    """One rank per GPU unless rehearsing: two ranks on one device (same
+    UUID, or the same PCI bus id when the UUID is empty) is an error naming
+    both ranks."""
+    a = {"pci_bus_id": "0000:05:00", "uuid": "u0"}
+    b = {"pci_bus_id": "0000:15:00", "uuid": "u1"}
+    bench.check_distinct_devices([a, b], False)
+    with pytest.raises(SystemExit, match="ranks 0 and 1 share"):
+        bench.check_distinct_devices([a, dict(a)], False)
+    with pytest.raises(SystemExit, match="ranks 1 and 2 share"):
+        bench.check_distinct_devices([a, dict(b, uuid=""), dict(b, uuid="")], False)
+    bench.check_distinct_devices([a, dict(a)], True)
+
+
+def _gather_rank(rank, world, port, out_dir):
+    import json
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=__import__("datetime").timedelta(seconds=60))
+    got = bench.gather_ranks({"rank": rank, "ms": 1.0 + rank}, world)
+    ident = {"pci_bus_id": f"0000:{rank:02x}:00", "uuid": f"u{rank}"}
+    idents = bench.gather_ranks(ident, world)
+    bench.check_distinct_devices(idents, False)
+    if rank == 0:
+        with open(os.path.join(out_dir, "got.json"), "w") as f:
+            json.dump({"got": got, "idents": idents}, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gather_ranks_gloo(tmp_path):
+    """The per-rank list of the N-rank line (bench.gather_ranks over gloo,
+    two processes): every rank's dict in rank order, and the distinct-device
+    check over the gathered identities."""
+    import json
+    import torch.multiprocessing as mp
+    mp.spawn(_gather_rank, args=(2, bench.free_port(), str(tmp_path)), nprocs=2, join=True)
+    js = json.loads((tmp_path / "got.json").read_text())
+    assert js["got"] == [{"rank": 0, "ms": 1.0}, {"rank": 1, "ms": 2.0}]
+    assert [d["uuid"] for d in js["idents"]] == ["u0", "u1"]
+    assert bench.gather_ranks({"rank": 0}, 1) == [{"rank": 0}]

@@ -382,6 +382,60 @@ def test_repeat_launches_identical(dev):
             assert np.array_equal(x, y), f"launch {k}: {what} differs"
 
 
+def test_submit_dev_two_slots_vs_oracle(dev):
+    """xdpgpu_submit_dev, the device-resident RX loop with two batches in
+    flight (bench.py's timed loop): consecutive batches of one pool dealt
+    to the two slots, each into its own outputs, launched without a host
+    wait between them so that they overlap on the GPU; every frame's
+    verdict, record and tuple, and the counters, against the oracle.  Then
+    the same batch on both slots at once, byte-identical; a slot with a
+    host batch in flight refuses a device batch (-EBUSY)."""
+    umem, descs, _ = xdpgpu.pool_generate(1 << 20, xdpgpu.POOL_IMIX, 64, 0x5EED0014)
+    descs = np.ascontiguousarray(descs, xdpgpu.DESC_DTYPE)
+    ov, ores, otup, ost = oracle.process(umem.copy(), descs, 0x5, 0, 2)
+    n = len(descs)
+    B = n // 8
+    d_umem, d_desc = to_dev(umem), to_dev(descs, 16)
+    d_v = torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda:0")
+    d_res = torch.full((n * 16,), 0xEE, dtype=torch.uint8, device="cuda:0")
+    d_tup = torch.full((n * 44,), 0xEE, dtype=torch.uint8, device="cuda:0")
+    with xdpgpu.XdpGpu(0, 0x5, 0, 2, 0) as ctx:
+        assert ctx.slot_stream(0) and ctx.slot_stream(1)
+        assert ctx.slot_stream(0) != ctx.slot_stream(1)
+        torch.cuda.synchronize()
+        for k in range(8):
+            lo = k * B
+            ctx.submit_dev(k & 1, d_umem, umem.nbytes, d_desc[lo * 16:], B, d_v[lo:],
+                           d_res[lo * 16:], d_tup[lo * 44:])
+        ctx.wait(0)
+        ctx.wait(1)
+        st = ctx.stats()
+        np.testing.assert_array_equal(d_v.cpu().numpy(), ov)
+        assert d_res.cpu().numpy().tobytes() == ores.tobytes()
+        assert d_tup.cpu().numpy().tobytes() == otup.tobytes()
+        assert st["frames"] == ost["frames"] == n
+        assert [st["verdict"][x] for x in xdpgpu.VERDICT_NAMES] == ost["verdict"]
+        # one batch on both slots at once, each into its own outputs
+        outs = [(torch.empty(n, dtype=torch.uint8, device="cuda:0"),
+                 torch.empty(n * 16, dtype=torch.uint8, device="cuda:0"),
+                 torch.empty(n * 44, dtype=torch.uint8, device="cuda:0")) for _ in range(2)]
+        for k in range(6):
+            ctx.submit_dev(k & 1, d_umem, umem.nbytes, d_desc, n, *outs[k & 1])
+        ctx.sync()
+        for v, r, t in outs:
+            np.testing.assert_array_equal(v.cpu().numpy(), ov)
+            assert r.cpu().numpy().tobytes() == ores.tobytes()
+            assert t.cpu().numpy().tobytes() == otup.tobytes()
+        # a host batch in flight on slot 1: its device batch is refused
+        ctx.register_umem(umem)
+        hv = np.zeros(1024, np.uint8)
+        ctx.submit(1, descs[:1024], hv)
+        with pytest.raises(xdpgpu.XdpGpuError, match="EBUSY|busy|in flight"):
+            ctx.submit_dev(1, d_umem, umem.nbytes, d_desc, n, *outs[1])
+        ctx.wait(1)
+        np.testing.assert_array_equal(hv, ov[:1024])
+
+
 def test_empty_batch(dev):
     umem, descs, _ = xdpgpu.pool_generate(4, xdpgpu.POOL_UDP4, 64, 1)
     v, res, tup, um, st = run_dev(umem, descs[:0], 0x5, 0, 1)

@@ -497,6 +497,44 @@ def test_two_queues_share_a_umem():
         b.close()
 
 
+def test_two_queues_share_a_umem_gather():
+    """The gather form of the shared UMEM (XDPGPU_CFG_UMEM_GATHER reads the
+    registered UMEM through its GPU mapping): both contexts hold the one
+    registration (xdpgpu_host_pin_refs counts them), queue A closes and
+    queue B's next gathered batch still reads mapped memory, bit-exact; the
+    last close releases the pinning."""
+    nframes, B = 4096, 2048
+    umem, descs, _ = chunked_pool(nframes, xdpgpu.POOL_UDP4, 64, 78)
+    want, wres, _, _ = oracle.process(umem.copy(), descs, 0x5, 0, xdpgpu.TUPLE_V4)
+    flags = 0x5 | xdpgpu.CFG_UMEM_GATHER
+
+    def batch(ctx, lo, hi):
+        v, r, _ = ctx.process(descs[lo:hi], want_res=True, want_tup=False)
+        np.testing.assert_array_equal(v, want[lo:hi])
+        np.testing.assert_array_equal(r.view(np.uint8).reshape(-1),
+                                      wres[lo:hi].view(np.uint8).reshape(-1))
+
+    assert xdpgpu.host_pin_refs(umem) == 0
+    a = xdpgpu.XdpGpu(0, flags, 0, xdpgpu.TUPLE_V4, 0, max_batch=nframes)
+    b = xdpgpu.XdpGpu(0, flags, 0, xdpgpu.TUPLE_V4, 0, max_batch=nframes)
+    try:
+        a.register_umem(umem, CHUNK)
+        b.register_umem(umem, CHUNK)
+        assert xdpgpu.host_pin_refs(umem) == 2
+        g0 = b.host_stats()["umem_gathers"]
+        batch(a, 0, B)
+        batch(b, B, nframes)
+        a.close()
+        assert xdpgpu.host_pin_refs(umem) == 1
+        batch(b, 0, nframes)
+        assert b.host_stats()["umem_gathers"] == g0 + 2
+        b.close()
+        assert xdpgpu.host_pin_refs(umem) == 0
+    finally:
+        a.close()
+        b.close()
+
+
 def test_gather_descs_inside_pinned_buffer():
     """The gather reads page-locked descriptors through their GPU mapping:
     a batch handed over as a slice from the middle of a page-locked array

@@ -135,8 +135,9 @@ def test_bench_self_launch():
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--frames", str(1 << 20),
-                        "--steps", "3", "--warmup", "1", "--no-cpu", "--no-secondary",
-                        "--no-e2e"], capture_output=True, text=True, timeout=240, env=env,
+                        "--steps", "3", "--warmup", "1", "--no-cpu", "--legs", "1500",
+                        "--frames-1500", str(1 << 15), "--no-e2e"],
+                       capture_output=True, text=True, timeout=240, env=env,
                        cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -145,3 +146,15 @@ def test_bench_self_launch():
     assert js["n_gpus"] == 2 and js["verdicts_ok"] is True and js["value"] > 0
     assert js["config"]["parallelism"] == "shard2"
     assert js["config"]["frames_per_gpu"] == 1 << 20
+    # per-rank numbers of the 64 B leg, and the 1500 B leg on every rank
+    assert [p["rank"] for p in js["per_rank"]] == [0, 1]
+    assert all(p["verdicts_ok"] and p["mpps"] > 0 and p["gpu_span_ms_per_step"] > 0
+               for p in js["per_rank"])
+    assert len(js["devices"]["pci_bus_ids"]) == 2 and js["devices"]["rccl"]
+    l15 = js["secondary_1500B"]
+    assert l15["n_gpus"] == 2 and l15["verdicts_ok"] is True and l15["frames"] == 8 << 15
+    assert [p["rank"] for p in l15["per_rank"]] == [0, 1]
+    assert all(p["verdicts_ok"] and p["mpps"] > 0 for p in l15["per_rank"])
+    # all ranks' frames over the slowest rank's time
+    slow = max(p["ms_per_launch"] for p in l15["per_rank"])
+    assert abs(l15["mpps"] - 2 * (8 << 15) / slow / 1e3) <= 0.1 + 1e-3 * l15["mpps"]

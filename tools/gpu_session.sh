@@ -76,6 +76,7 @@ workload() {
 	synproxy_leg) echo "python3 tools/leg_probe.py --leg synproxy" ;;
 	bench) echo "python3 bench.py --no-cpu --no-secondary --no-e2e --steps 20" ;;
 	bench50) echo "python3 bench.py --no-cpu --no-secondary --no-e2e --steps 50" ;;
+	bench20) echo "python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu --no-secondary --no-e2e" ;;
 	*) echo "unknown workload $1" >&2; exit 2 ;;
 	esac
 }
@@ -104,7 +105,11 @@ for s in "$@"; do
 	prof)
 		# shellcheck disable=SC2046
 		step "prof_$arg" 400 rocprofv3 --kernel-trace --stats --output-format csv \
-			-d "$OUT/prof_$arg" -o run -- $(workload "$arg") ;;
+			-d "$OUT/prof_$arg" -o run -- $(workload "$arg")
+		f=$(find "$OUT/prof_$arg" -name '*kernel_trace.csv' | head -1)
+		[ -n "$f" ] && python3 tools/trace_gaps.py "$f" --json "$OUT/prof_$arg/gaps.json" \
+			> "$OUT/prof_$arg/gaps.txt" 2>&1
+		true ;;
 	pmc)
 		# the pool's frame count and size for the summary (0: mixed sizes)
 		case $arg in
