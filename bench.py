@@ -102,12 +102,14 @@ def out_sets(n: int, tuple_bytes: int, dev, sets: int = 2) -> list:
             for _ in range(sets)]
 
 
-def time_device(ctx, d_umem, usize, d_desc, n, outs, steps, warmup, world):
+def time_device(ctx, d_umem, usize, d_desc, n, outs, steps, warmup, world, in_flight=2):
     """W untimed + K timed launches between barrier + synchronize, as a
-    device-resident RX loop keeps two batches in flight: launch k goes to
-    slot k mod 2 (xdpgpu_submit_dev: that slot's stream and scratch) with
-    that slot's output set, so that a launch starts on the CUs the one
-    before leaves while its last tiles finish.  Returns
+    device-resident RX loop keeps `in_flight` batches in flight: with 2,
+    launch k goes to slot k mod 2 (xdpgpu_submit_dev: that slot's stream
+    and scratch) with that slot's output set, so that a launch starts on
+    the CUs the one before leaves while its last tiles finish (config 2:
+    2-4 % a step; 16 M x 1500 B and IMIX, whose launches are 15x and 6x
+    longer, run slower so and keep one in flight).  Returns
     (wall seconds, GPU span of the K timed launches in ms): one event on
     slot 0's stream before the first launch (slot 1's stream waits for it)
     and one on each slot's stream after the last, none between launches."""
@@ -115,8 +117,9 @@ def time_device(ctx, d_umem, usize, d_desc, n, outs, steps, warmup, world):
     ss = [torch.cuda.ExternalStream(ctx.slot_stream(i), device=dev) for i in range(2)]
 
     def launch(k):
-        v, r, t = outs[k & 1]
-        ctx.submit_dev(k & 1, d_umem, usize, d_desc, n, v, r, t)
+        slot = k % in_flight
+        v, r, t = outs[slot]
+        ctx.submit_dev(slot, d_umem, usize, d_desc, n, v, r, t)
 
     torch.cuda.synchronize()   # the inputs, made on torch's streams
     for k in range(warmup):
@@ -143,7 +146,7 @@ def time_device(ctx, d_umem, usize, d_desc, n, outs, steps, warmup, world):
 
 
 def outputs_ok(outs, expect) -> bool:
-    """Every slot's verdicts equal the generator's (both output sets were
+    """Every output set's verdicts equal the generator's (each set was
     written by timed launches)."""
     return all(bool(np.array_equal(v.cpu().numpy(), expect)) for v, _, _ in outs)
 
@@ -395,9 +398,9 @@ def kt_round(kt: dict) -> dict:
 
 
 def side_run(ctx, tctx, dev, stream, n, kind, size, seed, fmt, steps, label, bpf_fn,
-             replicate=1, world=1, rank=0):
+             replicate=1, world=1, rank=0, in_flight=1):
     """One secondary workload: pool, kernel event pass, K timed launches
-    (two slots in flight, barrier-bracketed over the ranks when world > 1),
+    (`in_flight` slots, barrier-bracketed over the ranks when world > 1),
     verdict check.  replicate > 1: a pool of n frames is generated on the
     host and laid down `replicate` times back to back in HBM (descriptors
     offset by the copy's base), so that a multi-GB pool costs one host
@@ -421,13 +424,13 @@ def side_run(ctx, tctx, dev, stream, n, kind, size, seed, fmt, steps, label, bpf
         g_umem = to_dev(u, dev)
     del u
     g_desc = to_dev(ds, dev, 0)
-    outs = out_sets(n, xdpgpu.TUPLE_BYTES[fmt], dev)
+    outs = out_sets(n, xdpgpu.TUPLE_BYTES[fmt], dev, in_flight)
     usize = g_umem.numel() - 64
     kt = kernel_breakdown(tctx, g_umem, usize, g_desc, n, *outs[0], None, steps)
-    w, span = time_device(ctx, g_umem, usize, g_desc, n, outs, steps, 2, world)
+    w, span = time_device(ctx, g_umem, usize, g_desc, n, outs, steps, 2, world, in_flight)
     ok = outputs_ok(outs, ex)
     algo = bpf_fn(ds)
-    mine = {"rank": rank, "ms_per_launch": round(w / steps * 1e3, 4),
+    mine = {"rank": rank, "in_flight": in_flight, "ms_per_launch": round(w / steps * 1e3, 4),
             "gpu_span_ms_per_launch": round(span / steps, 4),
             "mpps": round(n * steps / w / 1e6, 1), "verdicts_ok": ok}
     per_rank = gather_ranks(mine, world)
@@ -643,10 +646,10 @@ def frags_run(dev, stream, n, steps, local, size=9000, chunk=4096):
     m = len(fd)
     g_umem = to_dev(u, dev)
     g_desc = to_dev(fd, dev, 0)
-    outs = out_sets(m, 16, dev)
+    outs = out_sets(m, 16, dev, 1)
     with xdpgpu.XdpGpu(local, xdpgpu.CFG_DEFAULT | xdpgpu.CFG_FRAGS, 0, xdpgpu.TUPLE_V4,
                        64) as g:
-        w, _ = time_device(g, g_umem, u.nbytes, g_desc, m, outs, steps, 2, 1)
+        w, _ = time_device(g, g_umem, u.nbytes, g_desc, m, outs, steps, 2, 1, 1)
     ok = outputs_ok(outs, ex[frame_of])
     t = w / steps
     out = {"workload": f"{n} x {size}B IPv4/UDP packets in {chunk}B fragments "
@@ -768,6 +771,7 @@ def e2e_run(local, umem, descs, expect, B: int, nbatches: int, chunk: int, windo
     per = max(1, n // B)
     h = xdpgpu.XdpGpu(local, flags, 0, xdpgpu.TUPLE_V4, window, max_batch=B)
     h.register_umem(umem, chunk)
+    threads = h.host_threads(0) if flags & xdpgpu.CFG_HOST_COMPACT else None
     # the descriptors as the RX ring holds them (page-locked), and
     # page-locked per-slot outputs, as an RX loop keeps them
     hd = xdpgpu.HostBuffer(per * B, xdpgpu.DESC_DTYPE)
@@ -814,6 +818,9 @@ def e2e_run(local, umem, descs, expect, B: int, nbatches: int, chunk: int, windo
             "slots": slots, "chunk": chunk, "pinned_buffers": True,
             "umem_gather": bool(flags & xdpgpu.CFG_UMEM_GATHER) and
             s1["umem_gathers"] > s0["umem_gathers"],
+            "host_compact": bool(flags & xdpgpu.CFG_HOST_COMPACT) and
+            s1["umem_compacted"] > s0["umem_compacted"],
+            **({"host_threads": threads} if threads else {}),
             "h2d_bytes_per_frame": round(h2d / fr, 1),
             "umem_copies_per_batch": round((s1["umem_copies"] - s0["umem_copies"]) /
                                            max(1, s1["batches"] - s0["batches"]), 1),
@@ -1083,6 +1090,7 @@ def main():
     e2e = None
     e2e_chunked = None
     e2e_gather = None
+    e2e_compact = None
     if not args.no_e2e and rank == 0 and world == 1:
         ceil = pcie_ceiling(dev)
         # host path, the packed pool: pinned UMEM, H2D span + descs, kernel,
@@ -1103,6 +1111,13 @@ def main():
                                        f"at headroom 256 ({cu.nbytes >> 20} MiB host UMEM, "
                                        "registered with chunk_size 4096), batches of half "
                                        "the UMEM cycling over it")
+            # the same with XDPGPU_CFG_HOST_COMPACT: the host threads (the
+            # CPUs the job may use, at most 16) pack each frame's bytes out
+            # of its chunk into one page-locked buffer a batch, one transfer
+            e2e_compact = e2e_run(local, cu, cd, ce, nc // 2, args.e2e_batches, 4096,
+                                  args.window, ceil,
+                                  flags=xdpgpu.CFG_DEFAULT | xdpgpu.CFG_HOST_COMPACT)
+            e2e_compact["workload"] = e2e_chunked["workload"] + ", XDPGPU_CFG_HOST_COMPACT"
             del cu, cd, ce
             # the same with XDPGPU_CFG_UMEM_GATHER (a kernel reads each
             # frame's bytes through the UMEM's GPU mapping), in a child
@@ -1173,6 +1188,8 @@ def main():
             line["e2e_host_path"] = e2e
         if e2e_chunked:
             line["e2e_host_path_chunked"] = e2e_chunked
+        if e2e_compact:
+            line["e2e_host_path_chunked_compact"] = e2e_compact
         if e2e_gather:
             line["e2e_host_path_chunked_gather"] = e2e_gather
         print(json.dumps(line), flush=True)

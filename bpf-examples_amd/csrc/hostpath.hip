@@ -94,6 +94,11 @@ __global__ __launch_bounds__(kEchoBlock) void echo_writeback_kernel(EchoArgs a)
  * page-locked array (read here, through its GPU mapping) and lane 0 of
  * each frame's group writes the device copy the RX kernel reads.  The
  * bytes read are summed per wave into *nbytes (xdpgpu_host_stats).
+ * With poff (XDPGPU_CFG_HOST_COMPACT) the same pieces come from the
+ * device copy of the host-packed buffer instead: the host threads copied
+ * each frame's pieces, the same 16-byte-aligned bytes clamped the same
+ * way, into one page-locked buffer, one transfer brought it over, and this
+ * kernel puts them at their UMEM offsets of the mirror.
  */
 constexpr int kGatherLanes = 8;
 __global__ __launch_bounds__(256) void umem_gather_kernel(GatherArgs a)
@@ -123,19 +128,22 @@ __global__ __launch_bounds__(256) void umem_gather_kernel(GatherArgs a)
 			const uint64_t r = (hi + 15) & ~15ull;
 			mine += (r < a.usize ? r : a.usize) - lo;
 		}
+		/* the piece's bytes: at their own offsets of the UMEM's view, or
+		 * packed (host compaction: the piece at 16 * poff[i]) */
+		const uint8_t *src = a.poff ? a.src + 16 * (uint64_t)a.poff[i] - lo : a.src;
 		for (uint64_t p = lo + 16 * sub; p < hi; p += 16 * kGatherLanes) {
 			if (p + 16 <= a.usize) {
-				const uint4 v = *reinterpret_cast<const uint4 *>(a.src + p);
+				const uint4 v = *reinterpret_cast<const uint4 *>(src + p);
 				*reinterpret_cast<uint4 *>(a.mirror + p) = v;
 			} else {
 				for (uint64_t b = p; b < a.usize; b++)
-					a.mirror[b] = a.src[b];
+					a.mirror[b] = src[b];
 			}
 		}
 	}
 	for (int o = 32; o; o >>= 1)
 		mine += __shfl_down(mine, o, 64);
-	if ((threadIdx.x & 63) == 0 && mine)
+	if ((threadIdx.x & 63) == 0 && mine && a.nbytes)
 		atomicAdd(a.nbytes, (unsigned long long)mine);
 }
 

@@ -21,9 +21,14 @@
 #include <algorithm>
 #include <initializer_list>
 #include <utility>
+#include <condition_variable>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <new>
+#include <thread>
+
+#include <sched.h>
 
 #include "xdpgpu.h"
 #include "xdpgpu_internal.h"
@@ -37,6 +42,75 @@ namespace {
 
 constexpr uint32_t kSlots = 2;
 constexpr uint32_t kDefaultMaxBatch = 1u << 20;
+
+/* The host threads of XDPGPU_CFG_HOST_COMPACT: a fork-join pool, the
+ * calling thread being thread 0.  run(f) calls f(t) for t in [0, size())
+ * and returns when every call has. */
+class HostPool {
+public:
+	explicit HostPool(unsigned n) : n_(n ? n : 1)
+	{
+		for (unsigned t = 1; t < n_; t++)
+			th_.emplace_back([this, t] { loop(t); });
+	}
+	~HostPool()
+	{
+		{
+			std::lock_guard<std::mutex> lk(mu_);
+			stop_ = true;
+			gen_++;
+		}
+		cv_.notify_all();
+		for (std::thread &t : th_)
+			t.join();
+	}
+	unsigned size() const { return n_; }
+	void run(const std::function<void(unsigned)> &f)
+	{
+		if (n_ == 1) {
+			f(0);
+			return;
+		}
+		{
+			std::lock_guard<std::mutex> lk(mu_);
+			job_ = &f;
+			left_ = n_ - 1;
+			gen_++;
+		}
+		cv_.notify_all();
+		f(0);
+		std::unique_lock<std::mutex> lk(mu_);
+		done_.wait(lk, [this] { return left_ == 0; });
+		job_ = nullptr;
+	}
+
+private:
+	void loop(unsigned t)
+	{
+		uint64_t seen = 0;
+		std::unique_lock<std::mutex> lk(mu_);
+		for (;;) {
+			cv_.wait(lk, [&] { return gen_ != seen; });
+			seen = gen_;
+			if (stop_)
+				return;
+			const std::function<void(unsigned)> *f = job_;
+			lk.unlock();
+			(*f)(t);
+			lk.lock();
+			if (--left_ == 0)
+				done_.notify_one();
+		}
+	}
+	unsigned n_;
+	std::vector<std::thread> th_;
+	std::mutex mu_;
+	std::condition_variable cv_, done_;
+	const std::function<void(unsigned)> *job_ = nullptr;
+	unsigned left_ = 0;
+	uint64_t gen_ = 0;
+	bool stop_ = false;
+};
 
 struct Slot {
 	hipStream_t stream = nullptr;
@@ -58,6 +132,15 @@ struct Slot {
 	 * per slot, so two batches in flight never share mirror bytes) */
 	uint8_t *d_mirror = nullptr;
 	uint64_t mirror_cap = 0;
+	/* XDPGPU_CFG_HOST_COMPACT: the batch's pieces packed by the host
+	 * threads (page-locked), their device copy, and each frame's piece
+	 * offset in 16-byte units (host and device) */
+	uint8_t *h_pack = nullptr;
+	uint8_t *d_pack = nullptr;
+	uint64_t pack_cap = 0;
+	uint32_t *h_poff = nullptr;
+	uint32_t *d_poff = nullptr;
+	uint64_t poff_cap = 0;
 	/* echo write-back as compact records (UMEM not mapped) */
 	EchoRec *d_erec = nullptr;
 	EchoRec *h_erec = nullptr;
@@ -104,6 +187,9 @@ struct xdpgpu_ctx {
 	/* the bytes the gather kernels read (device counter, added in by
 	 * xdpgpu_host_stats) */
 	unsigned long long *d_gbytes = nullptr;
+	/* XDPGPU_CFG_HOST_COMPACT's threads (made on first use) */
+	HostPool *hpool = nullptr;
+	uint32_t host_threads = 0;     /* 0: default_host_threads() */
 	/* host-path copy accounting (xdpgpu_host_stats) */
 	struct xdpgpu_host_stats hstats{};
 	/* XDPGPU_CFG_TIMING: 4 events per recorded launch */
@@ -196,6 +282,12 @@ static void free_slot(Slot &s)
 	if (s.d_ylist)
 		(void)hipFree(s.d_ylist);
 	(void)hipFree(s.d_mirror);
+	(void)hipFree(s.d_pack);
+	(void)hipFree(s.d_poff);
+	if (s.h_pack)
+		(void)hipHostFree(s.h_pack);
+	if (s.h_poff)
+		(void)hipHostFree(s.h_poff);
 	(void)hipFree(s.d_erec);
 	(void)hipFree(s.d_ecnt);
 	if (s.h_ecnt)
@@ -330,6 +422,7 @@ void xdpgpu_fini(xdpgpu_ctx *ctx)
 	(void)hipDeviceSynchronize();
 	for (uint32_t i = 0; i < kSlots; i++)
 		free_slot(ctx->slot[i]);
+	delete ctx->hpool;
 	if (ctx->d_gbytes)
 		(void)hipFree(ctx->d_gbytes);
 	if (ctx->tev) {
@@ -1417,6 +1510,199 @@ static int gather_batch(xdpgpu_ctx *ctx, Slot &s, uint32_t n, const xdpgpu_desc 
 	return 0;
 }
 
+/* XDPGPU_CFG_HOST_COMPACT's default thread count: XDPGPU_HOST_THREADS, else
+ * the CPUs this process may run on (affinity set, cgroup v2 CPU quota), at
+ * most 16. */
+static unsigned default_host_threads()
+{
+	if (const char *e = getenv("XDPGPU_HOST_THREADS")) {
+		const int v = atoi(e);
+		if (v > 0)
+			return (unsigned)std::min(v, 64);
+	}
+	unsigned n = 1;
+	cpu_set_t set;
+	CPU_ZERO(&set);
+	if (sched_getaffinity(0, sizeof(set), &set) == 0)
+		n = std::max(1, CPU_COUNT(&set));
+	if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+		char q[32];
+		long long period = 0;
+		if (fscanf(f, "%31s %lld", q, &period) == 2 && strcmp(q, "max") && period > 0)
+			n = std::min<unsigned>(n, (unsigned)std::max(1LL, atoll(q) / period));
+		fclose(f);
+	}
+	return std::min(n, 16u);
+}
+
+static HostPool *host_pool(xdpgpu_ctx *ctx)
+{
+	if (!ctx->hpool)
+		ctx->hpool = new (std::nothrow) HostPool(ctx->host_threads ? ctx->host_threads
+								: default_host_threads());
+	return ctx->hpool;
+}
+
+/* Page-locked and device staging of a slot for `bytes` packed bytes and n
+ * piece offsets (grown by a quarter more than asked; the slot is idle). */
+static int ensure_pack(xdpgpu_ctx *ctx, Slot &s, uint64_t bytes, uint32_t n)
+{
+	if (s.pack_cap < bytes + 64) {
+		const uint64_t cap = bytes + bytes / 4 + 64;
+		(void)hipFree(s.d_pack);
+		if (s.h_pack)
+			(void)hipHostFree(s.h_pack);
+		s.d_pack = nullptr;
+		s.h_pack = nullptr;
+		s.pack_cap = 0;
+		if (hipHostMalloc((void **)&s.h_pack, cap, 0) != hipSuccess ||
+		    hipMalloc(&s.d_pack, cap) != hipSuccess)
+			return set_err(ctx, -ENOMEM, "compaction staging of %llu bytes",
+				       (unsigned long long)cap);
+		s.pack_cap = cap;
+	}
+	if (s.poff_cap < n) {
+		const uint64_t cap = (uint64_t)n + n / 4 + 64;
+		(void)hipFree(s.d_poff);
+		if (s.h_poff)
+			(void)hipHostFree(s.h_poff);
+		s.d_poff = nullptr;
+		s.h_poff = nullptr;
+		s.poff_cap = 0;
+		if (hipHostMalloc((void **)&s.h_poff, cap * 4, 0) != hipSuccess ||
+		    hipMalloc(&s.d_poff, cap * 4) != hipSuccess)
+			return set_err(ctx, -ENOMEM, "compaction offsets");
+		s.poff_cap = cap;
+	}
+	return 0;
+}
+
+/* XDPGPU_CFG_HOST_COMPACT: the host threads pack the batch's pieces, the
+ * bytes umem_gather_kernel would read for each frame ([eff & ~15,
+ * round_up(end, 16)) clamped to the UMEM, end = eff + len + udp_csum's
+ * over-read byte where it can count), into the slot's page-locked staging
+ * buffer at 16-byte aligned offsets, in descriptor order: a first pass
+ * sizes each thread's share of the descriptors, a second copies it (the
+ * reference's frames sit one per 4 KiB chunk, af_xdp_user.c:56-57, so each
+ * copy is one or two cache lines from its own page; the source of the
+ * frame eight ahead is prefetched).  Then one transfer of the packed bytes
+ * and their offsets, and the gather kernel in its packed form puts each
+ * piece at its UMEM offset of the slot's mirror. */
+static int compact_batch(xdpgpu_ctx *ctx, Slot &s, const xdpgpu_desc *descs, uint32_t n,
+			 uint64_t &used)
+{
+	HostPool *pool = host_pool(ctx);
+	if (!pool)
+		return set_err(ctx, -ENOMEM, "host threads");
+	const unsigned T = pool->size();
+	const uint64_t usize = ctx->umem_size;
+	const uint32_t over_all = (ctx->cfg.flags & XDPGPU_CFG_FRAGS) ? 1u : 0u;
+	const uint8_t *umem = ctx->h_umem;
+	/* frame d's piece [lo, hi) of the UMEM; false: it names no bytes */
+	auto piece = [usize, over_all](const xdpgpu_desc &d, uint64_t &lo, uint64_t &hi) {
+		const uint64_t eff = (d.addr & ((1ull << 48) - 1)) + (d.addr >> 48);
+		if (eff >= usize || (uint64_t)d.len > usize - eff)
+			return false;
+		uint64_t end = eff + d.len + ((over_all | d.len) & 1);
+		if (end > usize)
+			end = usize;
+		lo = eff & ~15ull;
+		hi = std::min<uint64_t>((end + 15) & ~15ull, usize);
+		return true;
+	};
+	std::vector<uint64_t> base(T + 1, 0), lens(T, 0);
+	pool->run([&](unsigned t) {
+		const uint32_t i0 = (uint32_t)((uint64_t)n * t / T);
+		const uint32_t i1 = (uint32_t)((uint64_t)n * (t + 1) / T);
+		uint64_t b = 0, l = 0;
+		for (uint32_t i = i0; i < i1; i++) {
+			uint64_t lo, hi;
+			if (piece(descs[i], lo, hi)) {
+				b += (hi - lo + 15) & ~15ull;
+				l += descs[i].len;
+			}
+		}
+		base[t + 1] = b;
+		lens[t] = l;
+	});
+	used = 0;
+	for (unsigned t = 0; t < T; t++) {
+		base[t + 1] += base[t];
+		used += lens[t];
+	}
+	const uint64_t total = base[T];
+	if (total / 16 > UINT32_MAX)
+		return set_err(ctx, -E2BIG, "batch of %llu packed bytes",
+			       (unsigned long long)total);
+	if (int rc = ensure_pack(ctx, s, total, n))
+		return rc;
+	uint8_t *dst = s.h_pack;
+	uint32_t *poff = s.h_poff;
+	pool->run([&](unsigned t) {
+		const uint32_t i0 = (uint32_t)((uint64_t)n * t / T);
+		const uint32_t i1 = (uint32_t)((uint64_t)n * (t + 1) / T);
+		uint64_t o = base[t];
+		for (uint32_t i = i0; i < i1; i++) {
+			if (i + 8 < i1) {
+				const xdpgpu_desc &f = descs[i + 8];
+				const uint64_t e = (f.addr & ((1ull << 48) - 1)) + (f.addr >> 48);
+				if (e < usize) {
+					__builtin_prefetch(umem + e);
+					__builtin_prefetch(umem + std::min(e + 64, usize - 1));
+				}
+			}
+			uint64_t lo, hi;
+			if (!piece(descs[i], lo, hi)) {
+				poff[i] = 0;
+				continue;
+			}
+			memcpy(dst + o, umem + lo, hi - lo);
+			poff[i] = (uint32_t)(o >> 4);
+			o += (hi - lo + 15) & ~15ull;
+		}
+	});
+	if (total)
+		HIP_TRY(ctx, hipMemcpyAsync(s.d_pack, s.h_pack, total, hipMemcpyHostToDevice,
+					    s.stream));
+	HIP_TRY(ctx, hipMemcpyAsync(s.d_poff, s.h_poff, (size_t)n * 4, hipMemcpyHostToDevice,
+				    s.stream));
+	GatherArgs g;
+	memset(&g, 0, sizeof(g));
+	g.src = s.d_pack;
+	g.mirror = s.d_mirror;
+	g.usize = usize;
+	g.desc = s.d_desc;
+	g.hdesc = nullptr;
+	g.n = n;
+	g.over_all = over_all;
+	g.nbytes = nullptr;
+	g.poff = s.d_poff;
+	HIP_TRY(ctx, launch_umem_gather(g, s.stream));
+	ctx->hstats.umem_h2d_bytes += total;
+	ctx->hstats.desc_h2d_bytes += (uint64_t)n * 4;
+	ctx->hstats.umem_copies++;
+	ctx->hstats.umem_compacted++;
+	return 0;
+}
+
+int xdpgpu_host_threads(xdpgpu_ctx *ctx, uint32_t n)
+{
+	if (!ctx)
+		return -EINVAL;
+	for (uint32_t i = 0; i < kSlots; i++)
+		if (ctx->slot[i].busy)
+			return set_err(ctx, -EBUSY, "slot %u in flight", i);
+	const unsigned want = n ? std::min(n, 64u) : default_host_threads();
+	if (!ctx->hpool || ctx->hpool->size() != want) {
+		delete ctx->hpool;
+		ctx->hpool = new (std::nothrow) HostPool(want);
+		if (!ctx->hpool)
+			return set_err(ctx, -ENOMEM, "host threads");
+	}
+	ctx->host_threads = n;
+	return (int)want;
+}
+
 /* Copy a batch's frames into the slot's mirror: rows of chunks where they
  * pay (batch_rows), else spans (batch_runs).  Sets used (the bytes the
  * descriptors name) and adds the copy's bytes to the host stats. */
@@ -1514,7 +1800,8 @@ int xdpgpu_submit(xdpgpu_ctx *ctx, uint32_t slot, const xdpgpu_desc *descs,
 	/* the frames go to this slot's own mirror: a batch in flight on the
 	 * other slot never sees them, whatever the two batches' addresses */
 	uint64_t used = 0;
-	const bool gather = ctx->d_hview != nullptr;
+	const bool compact = (ctx->cfg.flags & XDPGPU_CFG_HOST_COMPACT) && ctx->chunk;
+	const bool gather = !compact && ctx->d_hview != nullptr;
 	if (gather)
 		used = sampled_used(descs, n);
 	const xdpgpu_desc *hdesc =
@@ -1522,7 +1809,8 @@ int xdpgpu_submit(xdpgpu_ctx *ctx, uint32_t slot, const xdpgpu_desc *descs,
 	if (!hdesc)
 		HIP_TRY(ctx, hipMemcpyAsync(s.d_desc, descs, (size_t)n * sizeof(*descs),
 					    hipMemcpyHostToDevice, s.stream));
-	rc = gather ? gather_batch(ctx, s, n, hdesc) : copy_batch(ctx, s, descs, n, used);
+	rc = compact ? compact_batch(ctx, s, descs, n, used)
+	     : gather ? gather_batch(ctx, s, n, hdesc) : copy_batch(ctx, s, descs, n, used);
 	if (rc)
 		return rc;
 	const bool echo = ctx->cfg.flags & XDPGPU_CFG_ICMP6_ECHO;

@@ -238,7 +238,12 @@ struct GatherArgs {
 	uint32_t n;
 	uint32_t over_all;         /* 1: every frame's byte len (multi-buffer
 				    * packets); 0: odd lengths only          */
-	unsigned long long *nbytes;   /* += the bytes read (host stats)    */
+	unsigned long long *nbytes;   /* += the bytes read (host stats), or
+				       * null                                 */
+	/* XDPGPU_CFG_HOST_COMPACT: non-null, src is the batch's pieces packed
+	 * on the host (copied to the device in one transfer) and frame i's
+	 * piece starts at src + 16 * poff[i] instead of src + (eff & ~15) */
+	const uint32_t *poff;
 };
 hipError_t launch_umem_gather(const GatherArgs &a, hipStream_t stream);
 

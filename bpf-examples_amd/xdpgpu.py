@@ -43,6 +43,7 @@ CFG_TIMING = 0x8
 CFG_STATS = 0x4
 CFG_FRAGS = 0x10      # multi-buffer packets (include/xdpgpu.h)
 CFG_UMEM_GATHER = 0x20   # host path: chunked UMEMs gathered by a kernel
+CFG_HOST_COMPACT = 0x40  # host path: chunked UMEMs packed by host threads
 PKT_CONTD = 0x1       # xdp_desc.options: the packet continues
 CFG_DEFAULT = CFG_VERIFY_CSUM | CFG_STATS
 
@@ -110,7 +111,7 @@ class HostStats(C.Structure):
     _fields_ = [("batches", C.c_uint64), ("frames", C.c_uint64),
                 ("umem_h2d_bytes", C.c_uint64), ("umem_copies", C.c_uint64),
                 ("desc_h2d_bytes", C.c_uint64), ("out_d2h_bytes", C.c_uint64),
-                ("umem_gathers", C.c_uint64)]
+                ("umem_gathers", C.c_uint64), ("umem_compacted", C.c_uint64)]
 
 
 class KTimes(C.Structure):
@@ -175,7 +176,7 @@ EXPORTS = (
     "xdpgpu_queue_stats", "xdpgpu_nat64_dynamic", "xdpgpu_nat64_clock",
     "xdpgpu_nat64_state", "xdpgpu_nat64_direction", "xdpgpu_synproxy_dev",
     "xdpgpu_host_stats", "xdpgpu_host_pin_refs", "xdpgpu_submit_dev",
-    "xdpgpu_slot_stream",
+    "xdpgpu_slot_stream", "xdpgpu_host_threads",
 )
 
 # struct xdpgpu_hints (XDP hints in front of a frame)
@@ -242,6 +243,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         lib.xdpgpu_slot_stream.argtypes = [vp, u32]
         lib.xdpgpu_slot_stream.restype = vp
         lib.xdpgpu_host_pin_refs.argtypes = [vp]
+        lib.xdpgpu_host_threads.argtypes = [vp, u32]
     _lib = lib
     return lib
 
@@ -392,6 +394,14 @@ class XdpGpu:
         self._check(self.lib.xdpgpu_submit(
             self.h, slot, descs.ctypes.data, len(descs), verdict.ctypes.data,
             _ptr(res), _ptr(tup)), "xdpgpu_submit")
+
+    def host_threads(self, n: int = 0) -> int:
+        """Threads that pack a batch under CFG_HOST_COMPACT (0: the CPUs
+        this process may use, at most 16); returns the count in effect."""
+        rc = self.lib.xdpgpu_host_threads(self.h, n)
+        if rc < 0:
+            self._check(rc, "xdpgpu_host_threads")
+        return rc
 
     def wait(self, slot: int) -> None:
         self._check(self.lib.xdpgpu_wait(self.h, slot), "xdpgpu_wait")

@@ -135,6 +135,16 @@ struct xdpgpu_network_tuple {
  * are used) for a UMEM registered without chunk_size or one the GPU cannot
  * map. */
 #define XDPGPU_CFG_UMEM_GATHER 0x20
+/* Host path on a chunked UMEM: the context's host threads copy each
+ * frame's bytes (the same 16-byte pieces the gather reads) out of its chunk
+ * into one page-locked staging buffer per slot, one transfer brings the
+ * batch over, and a device kernel puts each piece at its UMEM offset of the
+ * slot's mirror.  No kernel touches host memory; the copy engine moves one
+ * contiguous buffer instead of one row per chunk.
+ * xdpgpu_host_threads sets the thread count.  Takes precedence over
+ * XDPGPU_CFG_UMEM_GATHER; ignored for a UMEM registered without
+ * chunk_size. */
+#define XDPGPU_CFG_HOST_COMPACT 0x40
 #define XDPGPU_CFG_DEFAULT     (XDPGPU_CFG_VERIFY_CSUM | XDPGPU_CFG_STATS)
 
 struct xdpgpu_cfg {
@@ -253,8 +263,20 @@ struct xdpgpu_host_stats {
 	uint64_t desc_h2d_bytes;
 	uint64_t out_d2h_bytes;
 	uint64_t umem_gathers;
+	uint64_t umem_compacted;   /* batches packed by the host threads
+				    * (XDPGPU_CFG_HOST_COMPACT); their
+				    * staging bytes count in umem_h2d_bytes,
+				    * the 4-byte piece offsets in
+				    * desc_h2d_bytes */
 };
 int xdpgpu_host_stats(struct xdpgpu_ctx *ctx, struct xdpgpu_host_stats *out);
+
+/* XDPGPU_CFG_HOST_COMPACT: the number of host threads that pack a batch
+ * (the calling thread is one of them); 0 picks the CPUs this process may
+ * run on (its affinity set and cgroup CPU quota), at most 16.  Returns the
+ * count now in effect, or a negative errno (-EBUSY while a slot is in
+ * flight). */
+int xdpgpu_host_threads(struct xdpgpu_ctx *ctx, uint32_t n);
 
 /* Diagnostic: how many contexts hold the library's page-locking of the
  * host memory at p (several RX queues registering one UMEM share one

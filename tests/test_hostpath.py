@@ -359,8 +359,10 @@ def check_ring(got, want, host, ou, st, ost):
     assert [st["verdict"][x] for x in xdpgpu.VERDICT_NAMES] == ost["verdict"]
 
 
-def gather_bytes(descs, batches, usize, over_all=False):
-    """The 16-byte pieces umem_gather_kernel reads for the batches."""
+def gather_bytes(descs, batches, usize, over_all=False, packed=False):
+    """The 16-byte pieces umem_gather_kernel reads for the batches; packed:
+    the bytes XDPGPU_CFG_HOST_COMPACT's staging holds (each piece padded
+    to 16 bytes)."""
     tot = 0
     for b in batches:
         raw = descs["addr"][b].astype(np.uint64)
@@ -368,22 +370,33 @@ def gather_bytes(descs, batches, usize, over_all=False):
         ln = descs["len"][b].astype(np.int64)
         ok = (a < usize) & (ln <= usize - a)
         hi = np.minimum(a + ln + (1 if over_all else (ln & 1)), usize)
-        tot += int((np.minimum((hi + 15) & ~15, usize) - (a & ~15))[ok].sum())
+        piece = np.minimum((hi + 15) & ~15, usize) - (a & ~15)
+        if packed:
+            piece = (piece + 15) & ~15
+        tot += int(piece[ok].sum())
     return tot
 
 
-@pytest.mark.parametrize("gather,pinned", [(False, True), (True, True), (True, False)],
-                         ids=["rows", "gather", "gather_pageable_descs"])
+# how a chunked UMEM's frames reach the device: the copy engine's rows,
+# the gather kernel, or the host threads' compaction
+MODE_FLAGS = {"rows": 0, "gather": xdpgpu.CFG_UMEM_GATHER, "compact": xdpgpu.CFG_HOST_COMPACT}
+
+
+@pytest.mark.parametrize("mode,pinned", [("rows", True), ("gather", True), ("gather", False),
+                                         ("compact", True), ("compact", False)],
+                         ids=["rows", "gather", "gather_pageable_descs", "compact",
+                              "compact_pageable_descs"])
 @pytest.mark.parametrize("kind,size,ppm", [(xdpgpu.POOL_UDP4, 64, 300000),
                                            (xdpgpu.POOL_IMIX, 64, 200000)],
                          ids=["udp64", "imix"])
-def test_ring_chunked_umem(kind, size, ppm, gather, pinned):
+def test_ring_chunked_umem(kind, size, ppm, mode, pinned):
     """The reference's UMEM geometry (4 KiB chunks, each frame at its
     chunk's headroom) registered with its chunk size: the host path copies
     one window of each chunk (rows of a pitched copy), or with
     XDPGPU_CFG_UMEM_GATHER a kernel gathers each frame's bytes (reading
     page-locked descriptor arrays through their GPU mapping, pageable ones
-    after their copy).  Recycled,
+    after their copy), or with XDPGPU_CFG_HOST_COMPACT the host threads
+    pack the same bytes into one transfer.  Recycled,
     wrapping and strided batches (the scattered path merges chunk runs),
     echo replies written back: outputs and the whole host UMEM equal the
     oracle's."""
@@ -393,7 +406,7 @@ def test_ring_chunked_umem(kind, size, ppm, gather, pinned):
     batches = ring_batches(nframes, 12, 1024, 72)
     host = umem.copy()
     hs = {}
-    flags = ECHO | (xdpgpu.CFG_UMEM_GATHER if gather else 0)
+    flags = ECHO | MODE_FLAGS[mode]
     got, st = run_ring(host, descs, batches, flags, 0, window=0, chunk=CHUNK, host_stats=hs,
                        pinned=pinned)
     ou = umem.copy()
@@ -402,9 +415,15 @@ def test_ring_chunked_umem(kind, size, ppm, gather, pinned):
     ntx = sum(int((w[0] == xdpgpu.TX).sum()) for w in want)
     assert ntx > 100
     assert hs["frames"] == sum(len(b) for b in batches)
-    if gather:
+    if mode == "gather":
         assert hs["umem_gathers"] == len(batches), hs
         assert hs["umem_h2d_bytes"] == gather_bytes(descs, batches, umem.size), hs
+        return
+    if mode == "compact":
+        assert hs["umem_compacted"] == hs["umem_copies"] == len(batches), hs
+        assert hs["umem_gathers"] == 0, hs
+        assert hs["umem_h2d_bytes"] == gather_bytes(descs, batches, umem.size,
+                                                    packed=True), hs
         return
     assert hs["umem_gathers"] == 0, hs
     # at most one window of every chunk per batch (random recycled batches
@@ -416,8 +435,8 @@ def test_ring_chunked_umem(kind, size, ppm, gather, pinned):
     assert hs["umem_h2d_bytes"] < len(batches) * nframes * CHUNK // 2, hs
 
 
-@pytest.mark.parametrize("gather", [False, True], ids=["rows", "gather"])
-def test_chunked_consecutive_bytes(gather):
+@pytest.mark.parametrize("mode", ["rows", "gather", "compact"])
+def test_chunked_consecutive_bytes(mode):
     """Consecutive 64 B frames in 4 KiB chunks: exactly one row of the
     batch's window (its longest frame and udp_csum's over-read byte) per
     chunk, one copy per batch, or (gather) each frame's own 64 bytes;
@@ -427,14 +446,22 @@ def test_chunked_consecutive_bytes(gather):
     batches = [np.arange(k, k + B) for k in range(0, nframes, B)]
     host = umem.copy()
     hs = {}
-    flags = 0x5 | (xdpgpu.CFG_UMEM_GATHER if gather else 0)
+    flags = 0x5 | MODE_FLAGS[mode]
     got, st = run_ring(host, descs, batches, flags, 0, fmt=xdpgpu.TUPLE_V4, window=0,
                        chunk=CHUNK, host_stats=hs)
     ou = umem.copy()
     want, ost = oracle_ring(ou, descs, batches, 0x5, fmt=xdpgpu.TUPLE_V4)
     check_ring(got, want, host, ou, st, ost)
+    if mode == "compact":
+        # the descriptors and one 4-byte piece offset a frame; each frame's
+        # 64 bytes at the chunk's headroom (+ the over-read byte only for
+        # odd lengths): 64 bytes in one transfer a batch
+        assert hs["desc_h2d_bytes"] == nframes * (16 + 4), hs
+        assert hs["umem_h2d_bytes"] == gather_bytes(descs, batches, umem.size, packed=True)
+        assert hs["umem_compacted"] == hs["umem_copies"] == len(batches), hs
+        return
     assert hs["desc_h2d_bytes"] == nframes * 16
-    if gather:
+    if mode == "gather":
         assert hs["umem_h2d_bytes"] == gather_bytes(descs, batches, umem.size), hs
         assert hs["umem_h2d_bytes"] <= nframes * 64, hs
         assert hs["umem_gathers"] == hs["umem_copies"] == len(batches), hs
@@ -444,6 +471,37 @@ def test_chunked_consecutive_bytes(gather):
     # longest frame + 1, once per chunk
     assert hs["umem_h2d_bytes"] == sum(len(b) * (int(lens[b].max()) + 1) for b in batches), hs
     assert hs["umem_copies"] == len(batches), hs
+
+
+def test_compact_thread_counts():
+    """XDPGPU_CFG_HOST_COMPACT with 1, 3 and 7 packing threads (uneven shares
+    of an odd batch, IMIX frames with tags and IPv6 in 4 KiB chunks) and the
+    default count: outputs equal the oracle's every time, the same bytes
+    move, and the count cannot change while a slot is in flight."""
+    nframes = 3001
+    umem, descs, _ = chunked_pool(nframes, xdpgpu.POOL_IMIX, 64, 79)
+    ov, ores, otup, _ = oracle.process(umem.copy(), descs, 0x5, 0, xdpgpu.TUPLE_V4)
+    flags = 0x5 | xdpgpu.CFG_HOST_COMPACT
+    with xdpgpu.XdpGpu(0, flags, 0, xdpgpu.TUPLE_V4, 0, max_batch=nframes) as ctx:
+        ctx.register_umem(umem, CHUNK)
+        assert 1 <= ctx.host_threads(0) <= 16
+        for t in (1, 3, 7, 0):
+            got = ctx.host_threads(t)
+            assert got == t or t == 0
+            h0 = ctx.host_stats()
+            v, r, tup = ctx.process(descs)
+            h1 = ctx.host_stats()
+            np.testing.assert_array_equal(v, ov, err_msg=f"{t} threads")
+            assert r.tobytes() == ores.tobytes() and tup.tobytes() == otup.tobytes()
+            assert h1["umem_compacted"] - h0["umem_compacted"] == 1
+            assert (h1["umem_h2d_bytes"] - h0["umem_h2d_bytes"] ==
+                    gather_bytes(descs, [np.arange(nframes)], umem.size, packed=True))
+        hv = np.zeros(nframes, np.uint8)
+        ctx.submit(0, descs, hv)
+        with pytest.raises(xdpgpu.XdpGpuError, match="EBUSY|busy|in flight"):
+            ctx.host_threads(2)
+        ctx.wait(0)
+        np.testing.assert_array_equal(hv, ov)
 
 
 def udp_to_frame_end(umem, descs, length):
@@ -566,8 +624,9 @@ def test_gather_descs_inside_pinned_buffer():
             o.close()
 
 
+@pytest.mark.parametrize("mode", ["gather", "compact"])
 @pytest.mark.parametrize("size", [64, 65, 67, 600, 601])
-def test_gather_over_read_byte(size):
+def test_gather_over_read_byte(size, mode):
     """The gather copies a frame's own bytes and, for odd lengths, the byte
     after it (udp_csum's over-read, lib_checksum.h:175-176): frames whose
     UDP range runs to their last byte, every other byte of the 4 KiB chunks
@@ -590,13 +649,14 @@ def test_gather_over_read_byte(size):
     batches = [np.arange(k, k + B) for k in range(0, nframes, B)]
     host = umem.copy()
     hs = {}
-    got, st = run_ring(host, descs, batches, 0x4 | xdpgpu.CFG_UMEM_GATHER, 0,
+    got, st = run_ring(host, descs, batches, 0x4 | MODE_FLAGS[mode], 0,
                        fmt=xdpgpu.TUPLE_V4, window=0, chunk=CHUNK, host_stats=hs)
     ou = umem.copy()
     want, ost = oracle_ring(ou, descs, batches, 0x4, fmt=xdpgpu.TUPLE_V4)
     check_ring(got, want, host, ou, st, ost)
-    assert hs["umem_gathers"] == len(batches), hs
-    assert hs["umem_h2d_bytes"] == gather_bytes(descs, batches, umem.size), hs
+    packed = mode == "compact"
+    assert hs["umem_gathers" if not packed else "umem_compacted"] == len(batches), hs
+    assert hs["umem_h2d_bytes"] == gather_bytes(descs, batches, umem.size, packed=packed), hs
     assert ost["verdict"][xdpgpu.REDIRECT] > 0.9 * nframes
     z = umem.copy()
     idx = (addr + lens)[inr & (addr + lens < umem.size)]
@@ -605,8 +665,8 @@ def test_gather_over_read_byte(size):
     assert (size & 1) == any(not np.array_equal(a[1], b[1]) for a, b in zip(want, w2))
 
 
-@pytest.mark.parametrize("gather", [False, True], ids=["rows", "gather"])
-def test_chunked_fallbacks_and_umem_end(gather):
+@pytest.mark.parametrize("mode", ["rows", "gather", "compact"])
+def test_chunked_fallbacks_and_umem_end(mode):
     """The rows' edges: a frame whose over-read byte lies in the next chunk
     (the batch falls back to span copies; the gather reads the byte from
     the next chunk), and a UMEM whose size is not a whole number of chunks,
@@ -625,12 +685,14 @@ def test_chunked_fallbacks_and_umem_end(gather):
                            ("UMEM end", small, np.arange(nframes - 300, nframes))):
         host = u.copy()
         hs = {}
-        got, st = run_ring(host, d, [batch], 0x5 | (xdpgpu.CFG_UMEM_GATHER if gather else 0),
+        got, st = run_ring(host, d, [batch], 0x5 | MODE_FLAGS[mode],
                            0, fmt=xdpgpu.TUPLE_V4, window=0, chunk=CHUNK, host_stats=hs)
         ou = u.copy()
         want, ost = oracle_ring(ou, d, [batch], 0x5, fmt=xdpgpu.TUPLE_V4)
         check_ring(got, want, host, ou, st, ost)
         assert hs["frames"] == len(batch), name
-        assert hs["umem_gathers"] == (1 if gather else 0), (name, hs)
-        if gather:
-            assert hs["umem_h2d_bytes"] == gather_bytes(d, [batch], u.size), (name, hs)
+        assert hs["umem_gathers"] == (1 if mode == "gather" else 0), (name, hs)
+        assert hs["umem_compacted"] == (1 if mode == "compact" else 0), (name, hs)
+        if mode != "rows":
+            assert hs["umem_h2d_bytes"] == gather_bytes(d, [batch], u.size,
+                                                        packed=mode == "compact"), (name, hs)

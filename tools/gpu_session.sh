@@ -123,6 +123,12 @@ for s in "$@"; do
 		# shellcheck disable=SC2086
 		step "pmc_$arg" 900 env $geo DEST="$OUT/pmc_$arg.json" OUT="$OUT/pmc_$arg" \
 			PMC_CMD="$(workload "$arg")" LABEL="$arg" bash tools/pmc_profile.sh ;;
+	pmcprobe)
+		# PMC passes over tools/hbm_probe MODE, every kernel summarised
+		# (the access-shape calibration of FETCH_SIZE / WRITE_SIZE)
+		step "pmcprobe_$arg" 900 env PMC_ALL=1 DEST="$OUT/pmcprobe_$arg.json" \
+			OUT="$OUT/pmcprobe_$arg" PMC_CMD="tools/hbm_probe $arg" LABEL="hbm_probe $arg" \
+			bash tools/pmc_profile.sh ;;
 	ab)
 		for r in 1 2; do
 			for lib in bpf-examples_amd/csrc/libxdpgpu.so "$arg"; do

@@ -29,21 +29,27 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--frames", type=int, default=16 << 20)
     ap.add_argument("--modes", default="serial,slots")
+    ap.add_argument("--size", type=int, default=64)
+    ap.add_argument("--kind", type=int, default=0, help="0 UDP4, 1 IMIX")
+    ap.add_argument("--fmt", type=int, default=1, help="tuple format (1 V4, 2 NET)")
+    ap.add_argument("--window", type=int, default=64)
+    ap.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EED0002)
     ap.add_argument("--idle", type=float, default=0.0,
                     help="seconds of host sleep (GPU idle) before each run")
     ap.add_argument("--prewarm", type=int, default=0,
                     help="launches before each run's warmup (after the idle)")
     a = ap.parse_args()
     n = a.frames
-    umem, descs, expect = xdpgpu.pool_generate(n, xdpgpu.POOL_UDP4, 64, 0x5EED0002)
+    umem, descs, expect = xdpgpu.pool_generate(n, a.kind, a.size, a.seed)
+    tb = xdpgpu.TUPLE_BYTES[a.fmt]
     dev = torch.device("cuda:0")
     d_umem = torch.zeros(umem.nbytes + 64, dtype=torch.uint8, device=dev)
     d_umem[: umem.nbytes].copy_(torch.from_numpy(umem))
     d_desc = torch.from_numpy(descs.view(np.uint8).reshape(-1)).to(dev)
     outs = [(torch.empty(n, dtype=torch.uint8, device=dev),
              torch.empty(n * 16, dtype=torch.uint8, device=dev),
-             torch.empty(n * 16, dtype=torch.uint8, device=dev)) for _ in range(2)]
-    ctx = xdpgpu.XdpGpu(0, xdpgpu.CFG_DEFAULT, 0, xdpgpu.TUPLE_V4, 64)
+             torch.empty(n * tb, dtype=torch.uint8, device=dev)) for _ in range(2)]
+    ctx = xdpgpu.XdpGpu(0, xdpgpu.CFG_DEFAULT, 0, a.fmt, a.window)
     ss = [torch.cuda.ExternalStream(ctx.slot_stream(i), device=dev) for i in range(2)]
 
     def launch(mode, k):

@@ -23,7 +23,8 @@ def main(out, dest=None, frames=16 << 20, size=64, label=None):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 k = row.get("Kernel_Name", "?")
-                if "xdp_" not in k and "synproxy" not in k:
+                if ("xdp_" not in k and "synproxy" not in k and
+                        not os.environ.get("PMC_ALL")):
                     continue
                 name = row.get("Counter_Name")
                 val = float(row.get("Counter_Value", 0))
