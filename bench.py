@@ -831,6 +831,28 @@ def e2e_run(local, umem, descs, expect, B: int, nbatches: int, chunk: int, windo
             "verdicts_ok": ok}
 
 
+def huge_pages_copy(a: np.ndarray) -> np.ndarray:
+    """a copied into anonymous memory advised for transparent huge pages
+    (madvise MADV_HUGEPAGE): xdpsock maps its UMEM with MAP_HUGETLB in
+    unaligned-chunk mode (AF_XDP-example/xdpsock.c:1246, :2062).  The
+    array keeps the mapping alive."""
+    import mmap
+    mm = mmap.mmap(-1, max(a.nbytes, 1), flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
+    if hasattr(mm, "madvise") and hasattr(mmap, "MADV_HUGEPAGE"):
+        mm.madvise(mmap.MADV_HUGEPAGE)
+    out = np.frombuffer(mm, np.uint8)[: a.nbytes]
+    out[:] = a.view(np.uint8).reshape(-1)
+    return out
+
+
+def thp_mode() -> str:
+    try:
+        with open("/sys/kernel/mm/transparent_hugepage/enabled") as f:
+            return f.read().strip()
+    except OSError:
+        return "unknown"
+
+
 def gather_leg(frames: int, batches: int, ceil: dict) -> dict:
     """e2e_run with XDPGPU_CFG_UMEM_GATHER on the chunked leg's workload,
     run by tools/e2e_probe.py as a child process (its own GPU context):
@@ -1091,6 +1113,7 @@ def main():
     e2e_chunked = None
     e2e_gather = None
     e2e_compact = None
+    e2e_compact_huge = None
     if not args.no_e2e and rank == 0 and world == 1:
         ceil = pcie_ceiling(dev)
         # host path, the packed pool: pinned UMEM, H2D span + descs, kernel,
@@ -1118,7 +1141,17 @@ def main():
                                   args.window, ceil,
                                   flags=xdpgpu.CFG_DEFAULT | xdpgpu.CFG_HOST_COMPACT)
             e2e_compact["workload"] = e2e_chunked["workload"] + ", XDPGPU_CFG_HOST_COMPACT"
-            del cu, cd, ce
+            # the same UMEM in transparent huge pages (xdpsock's MAP_HUGETLB
+            # UMEM): one 4 KiB chunk a frame is one page walk a frame in 4 KiB
+            # pages (tools/pack_probe.c)
+            hu = huge_pages_copy(cu)
+            e2e_compact_huge = e2e_run(local, hu, cd, ce, nc // 2, args.e2e_batches, 4096,
+                                       args.window, ceil,
+                                       flags=xdpgpu.CFG_DEFAULT | xdpgpu.CFG_HOST_COMPACT)
+            e2e_compact_huge["workload"] = (e2e_compact["workload"] +
+                                            ", UMEM in transparent huge pages (madvise; "
+                                            f"THP {thp_mode()})")
+            del hu, cu, cd, ce
             # the same with XDPGPU_CFG_UMEM_GATHER (a kernel reads each
             # frame's bytes through the UMEM's GPU mapping), in a child
             # process: the one kernel that reads host memory (DESIGN.md
@@ -1190,6 +1223,8 @@ def main():
             line["e2e_host_path_chunked"] = e2e_chunked
         if e2e_compact:
             line["e2e_host_path_chunked_compact"] = e2e_compact
+        if e2e_compact_huge:
+            line["e2e_host_path_chunked_compact_huge"] = e2e_compact_huge
         if e2e_gather:
             line["e2e_host_path_chunked_gather"] = e2e_gather
         print(json.dumps(line), flush=True)

@@ -1496,6 +1496,7 @@ static const void *host_view(const void *p)
 static int gather_batch(xdpgpu_ctx *ctx, Slot &s, uint32_t n, const xdpgpu_desc *hdesc)
 {
 	GatherArgs g;
+	memset(&g, 0, sizeof(g));   /* poff null: the pieces at their UMEM offsets */
 	g.src = ctx->d_hview;
 	g.mirror = s.d_mirror;
 	g.usize = ctx->umem_size;
@@ -1800,7 +1801,7 @@ int xdpgpu_submit(xdpgpu_ctx *ctx, uint32_t slot, const xdpgpu_desc *descs,
 	/* the frames go to this slot's own mirror: a batch in flight on the
 	 * other slot never sees them, whatever the two batches' addresses */
 	uint64_t used = 0;
-	const bool compact = (ctx->cfg.flags & XDPGPU_CFG_HOST_COMPACT) && ctx->chunk;
+	const bool compact = ctx->cfg.flags & XDPGPU_CFG_HOST_COMPACT;
 	const bool gather = !compact && ctx->d_hview != nullptr;
 	if (gather)
 		used = sampled_used(descs, n);

@@ -135,15 +135,16 @@ struct xdpgpu_network_tuple {
  * are used) for a UMEM registered without chunk_size or one the GPU cannot
  * map. */
 #define XDPGPU_CFG_UMEM_GATHER 0x20
-/* Host path on a chunked UMEM: the context's host threads copy each
- * frame's bytes (the same 16-byte pieces the gather reads) out of its chunk
- * into one page-locked staging buffer per slot, one transfer brings the
- * batch over, and a device kernel puts each piece at its UMEM offset of the
- * slot's mirror.  No kernel touches host memory; the copy engine moves one
- * contiguous buffer instead of one row per chunk.
+/* Host path: the context's host threads copy each frame's bytes (the same
+ * 16-byte pieces the gather reads, udp_csum's over-read byte included) out
+ * of the registered UMEM into one page-locked staging buffer per slot, one
+ * transfer brings the batch over, and a device kernel puts each piece at
+ * its UMEM offset of the slot's mirror.  No kernel touches host memory; the
+ * copy engine moves one contiguous buffer instead of one row per chunk.
+ * For sparse frames (the reference's 4 KiB chunks, aligned or unaligned
+ * mode); a packed UMEM's span copies need no host pass.
  * xdpgpu_host_threads sets the thread count.  Takes precedence over
- * XDPGPU_CFG_UMEM_GATHER; ignored for a UMEM registered without
- * chunk_size. */
+ * XDPGPU_CFG_UMEM_GATHER. */
 #define XDPGPU_CFG_HOST_COMPACT 0x40
 #define XDPGPU_CFG_DEFAULT     (XDPGPU_CFG_VERIFY_CSUM | XDPGPU_CFG_STATS)
 

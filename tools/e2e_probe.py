@@ -118,6 +118,8 @@ def main():
     ap.add_argument("--batches", type=int, default=32)
     ap.add_argument("--gather-only", action="store_true")
     ap.add_argument("--no-submit-cost", action="store_true")
+    ap.add_argument("--compact", action="store_true",
+                    help="XDPGPU_CFG_HOST_COMPACT on 4 KiB pages and on huge pages")
     ap.add_argument("--h2d-ceil", type=float, default=57.0,
                     help="the box's pinned H2D GB/s (bench.py pcie_ceiling)")
     ap.add_argument("--d2h-ceil", type=float, default=57.0)
@@ -167,14 +169,19 @@ def main():
     modes = [("gather", xdpgpu.CFG_DEFAULT | xdpgpu.CFG_UMEM_GATHER)]
     if not args.gather_only:
         modes.insert(0, ("rows", xdpgpu.CFG_DEFAULT))
+    if args.compact:
+        modes = [("compact", xdpgpu.CFG_DEFAULT | xdpgpu.CFG_HOST_COMPACT),
+                 ("compact_huge", xdpgpu.CFG_DEFAULT | xdpgpu.CFG_HOST_COMPACT)]
+    hu = bench.huge_pages_copy(cu) if args.compact else None
     for slots in (int(x) for x in args.slots.split(",")):
         for name, flags in modes:
-            r = bench.e2e_run(0, cu, cd, ce, nc // 2, args.batches, 4096, 0, ceil, flags,
+            u = hu if name.endswith("_huge") else cu
+            r = bench.e2e_run(0, u, cd, ce, nc // 2, args.batches, 4096, 0, ceil, flags,
                               slots)
             r.pop("pcie_ceiling", None)
             r["mode"] = name
             if not args.no_submit_cost:
-                r["submit_host_ms"] = round(submit_cost(cu, cd, nc // 2, flags) * 1e3, 3)
+                r["submit_host_ms"] = round(submit_cost(u, cd, nc // 2, flags) * 1e3, 3)
             print(json.dumps(r), flush=True)
 
 
