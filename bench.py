@@ -820,7 +820,10 @@ def e2e_run(local, umem, descs, expect, B: int, nbatches: int, chunk: int, windo
             s1["umem_gathers"] > s0["umem_gathers"],
             "host_compact": bool(flags & xdpgpu.CFG_HOST_COMPACT) and
             s1["umem_compacted"] > s0["umem_compacted"],
-            **({"host_threads": threads} if threads else {}),
+            **({"host_threads": threads,
+                "pack_ms_per_batch": round((s1["compact_ns"] - s0["compact_ns"]) / 1e6 /
+                                           max(1, s1["umem_compacted"] - s0["umem_compacted"]),
+                                           3)} if threads else {}),
             "h2d_bytes_per_frame": round(h2d / fr, 1),
             "umem_copies_per_batch": round((s1["umem_copies"] - s0["umem_copies"]) /
                                            max(1, s1["batches"] - s0["batches"]), 1),

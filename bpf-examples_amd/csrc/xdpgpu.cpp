@@ -1595,6 +1595,8 @@ static int compact_batch(xdpgpu_ctx *ctx, Slot &s, const xdpgpu_desc *descs, uin
 	HostPool *pool = host_pool(ctx);
 	if (!pool)
 		return set_err(ctx, -ENOMEM, "host threads");
+	struct timespec ts0, ts1;
+	clock_gettime(CLOCK_MONOTONIC, &ts0);
 	const unsigned T = pool->size();
 	const uint64_t usize = ctx->umem_size;
 	const uint32_t over_all = (ctx->cfg.flags & XDPGPU_CFG_FRAGS) ? 1u : 0u;
@@ -1611,27 +1613,35 @@ static int compact_batch(xdpgpu_ctx *ctx, Slot &s, const xdpgpu_desc *descs, uin
 		hi = std::min<uint64_t>((end + 15) & ~15ull, usize);
 		return true;
 	};
-	std::vector<uint64_t> base(T + 1, 0), lens(T, 0);
+	/* the batch in kParts parts of T shares each: a part's transfer is
+	 * issued as soon as it is packed, under the packing of the next
+	 * (a 512 K batch of 64-byte frames: 0.9 ms of packing on 16 threads
+	 * beside 0.9 ms of transfer) */
+	constexpr unsigned kParts = 4;
+	const unsigned S = kParts * T;
+	auto share = [n, S](unsigned k) { return (uint32_t)((uint64_t)n * k / S); };
+	std::vector<uint64_t> base(S + 1, 0), lens(S, 0);
 	pool->run([&](unsigned t) {
-		const uint32_t i0 = (uint32_t)((uint64_t)n * t / T);
-		const uint32_t i1 = (uint32_t)((uint64_t)n * (t + 1) / T);
-		uint64_t b = 0, l = 0;
-		for (uint32_t i = i0; i < i1; i++) {
-			uint64_t lo, hi;
-			if (piece(descs[i], lo, hi)) {
-				b += (hi - lo + 15) & ~15ull;
-				l += descs[i].len;
+		for (unsigned q = 0; q < kParts; q++) {
+			const unsigned k = q * T + t;
+			uint64_t b = 0, l = 0;
+			for (uint32_t i = share(k); i < share(k + 1); i++) {
+				uint64_t lo, hi;
+				if (piece(descs[i], lo, hi)) {
+					b += (hi - lo + 15) & ~15ull;
+					l += descs[i].len;
+				}
 			}
+			base[k + 1] = b;
+			lens[k] = l;
 		}
-		base[t + 1] = b;
-		lens[t] = l;
 	});
 	used = 0;
-	for (unsigned t = 0; t < T; t++) {
-		base[t + 1] += base[t];
-		used += lens[t];
+	for (unsigned k = 0; k < S; k++) {
+		base[k + 1] += base[k];
+		used += lens[k];
 	}
-	const uint64_t total = base[T];
+	const uint64_t total = base[S];
 	if (total / 16 > UINT32_MAX)
 		return set_err(ctx, -E2BIG, "batch of %llu packed bytes",
 			       (unsigned long long)total);
@@ -1639,32 +1649,41 @@ static int compact_batch(xdpgpu_ctx *ctx, Slot &s, const xdpgpu_desc *descs, uin
 		return rc;
 	uint8_t *dst = s.h_pack;
 	uint32_t *poff = s.h_poff;
-	pool->run([&](unsigned t) {
-		const uint32_t i0 = (uint32_t)((uint64_t)n * t / T);
-		const uint32_t i1 = (uint32_t)((uint64_t)n * (t + 1) / T);
-		uint64_t o = base[t];
-		for (uint32_t i = i0; i < i1; i++) {
-			if (i + 8 < i1) {
-				const xdpgpu_desc &f = descs[i + 8];
-				const uint64_t e = (f.addr & ((1ull << 48) - 1)) + (f.addr >> 48);
-				if (e < usize) {
-					__builtin_prefetch(umem + e);
-					__builtin_prefetch(umem + std::min(e + 64, usize - 1));
+	uint64_t pack_ns = 0;
+	for (unsigned q = 0; q < kParts; q++) {
+		pool->run([&](unsigned t) {
+			const unsigned k = q * T + t;
+			const uint32_t i1 = share(k + 1);
+			uint64_t o = base[k];
+			for (uint32_t i = share(k); i < i1; i++) {
+				if (i + 8 < i1) {
+					const xdpgpu_desc &f = descs[i + 8];
+					const uint64_t e = (f.addr & ((1ull << 48) - 1)) + (f.addr >> 48);
+					if (e < usize) {
+						__builtin_prefetch(umem + e);
+						__builtin_prefetch(umem + std::min(e + 64, usize - 1));
+					}
 				}
+				uint64_t lo, hi;
+				if (!piece(descs[i], lo, hi)) {
+					poff[i] = 0;
+					continue;
+				}
+				memcpy(dst + o, umem + lo, hi - lo);
+				poff[i] = (uint32_t)(o >> 4);
+				o += (hi - lo + 15) & ~15ull;
 			}
-			uint64_t lo, hi;
-			if (!piece(descs[i], lo, hi)) {
-				poff[i] = 0;
-				continue;
-			}
-			memcpy(dst + o, umem + lo, hi - lo);
-			poff[i] = (uint32_t)(o >> 4);
-			o += (hi - lo + 15) & ~15ull;
-		}
-	});
-	if (total)
-		HIP_TRY(ctx, hipMemcpyAsync(s.d_pack, s.h_pack, total, hipMemcpyHostToDevice,
-					    s.stream));
+		});
+		clock_gettime(CLOCK_MONOTONIC, &ts1);
+		pack_ns += (uint64_t)(ts1.tv_sec - ts0.tv_sec) * 1000000000ull +
+			   (uint64_t)ts1.tv_nsec - (uint64_t)ts0.tv_nsec;
+		const uint64_t b0 = base[q * T], b1 = base[(q + 1) * T];
+		if (b1 > b0)
+			HIP_TRY(ctx, hipMemcpyAsync(s.d_pack + b0, s.h_pack + b0, b1 - b0,
+						    hipMemcpyHostToDevice, s.stream));
+		clock_gettime(CLOCK_MONOTONIC, &ts0);
+	}
+	ctx->hstats.compact_ns += pack_ns;
 	HIP_TRY(ctx, hipMemcpyAsync(s.d_poff, s.h_poff, (size_t)n * 4, hipMemcpyHostToDevice,
 				    s.stream));
 	GatherArgs g;

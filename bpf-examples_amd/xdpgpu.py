@@ -111,7 +111,8 @@ class HostStats(C.Structure):
     _fields_ = [("batches", C.c_uint64), ("frames", C.c_uint64),
                 ("umem_h2d_bytes", C.c_uint64), ("umem_copies", C.c_uint64),
                 ("desc_h2d_bytes", C.c_uint64), ("out_d2h_bytes", C.c_uint64),
-                ("umem_gathers", C.c_uint64), ("umem_compacted", C.c_uint64)]
+                ("umem_gathers", C.c_uint64), ("umem_compacted", C.c_uint64),
+                ("compact_ns", C.c_uint64)]
 
 
 class KTimes(C.Structure):

@@ -269,6 +269,7 @@ struct xdpgpu_host_stats {
 				    * staging bytes count in umem_h2d_bytes,
 				    * the 4-byte piece offsets in
 				    * desc_h2d_bytes */
+	uint64_t compact_ns;       /* host time those batches' packing took */
 };
 int xdpgpu_host_stats(struct xdpgpu_ctx *ctx, struct xdpgpu_host_stats *out);
 

@@ -120,6 +120,8 @@ def main():
     ap.add_argument("--no-submit-cost", action="store_true")
     ap.add_argument("--compact", action="store_true",
                     help="XDPGPU_CFG_HOST_COMPACT on 4 KiB pages and on huge pages")
+    ap.add_argument("--threads", default="0",
+                    help="compaction thread counts to run (0: the library's default)")
     ap.add_argument("--h2d-ceil", type=float, default=57.0,
                     help="the box's pinned H2D GB/s (bench.py pcie_ceiling)")
     ap.add_argument("--d2h-ceil", type=float, default=57.0)
@@ -173,16 +175,21 @@ def main():
         modes = [("compact", xdpgpu.CFG_DEFAULT | xdpgpu.CFG_HOST_COMPACT),
                  ("compact_huge", xdpgpu.CFG_DEFAULT | xdpgpu.CFG_HOST_COMPACT)]
     hu = bench.huge_pages_copy(cu) if args.compact else None
-    for slots in (int(x) for x in args.slots.split(",")):
-        for name, flags in modes:
-            u = hu if name.endswith("_huge") else cu
-            r = bench.e2e_run(0, u, cd, ce, nc // 2, args.batches, 4096, 0, ceil, flags,
-                              slots)
-            r.pop("pcie_ceiling", None)
-            r["mode"] = name
-            if not args.no_submit_cost:
-                r["submit_host_ms"] = round(submit_cost(u, cd, nc // 2, flags) * 1e3, 3)
-            print(json.dumps(r), flush=True)
+    runs = [(slots, name, flags, th) for slots in (int(x) for x in args.slots.split(","))
+            for th in (int(x) for x in args.threads.split(","))
+            for name, flags in modes if th == 0 or args.compact]
+    for slots, name, flags, th in runs:
+        if th:
+            os.environ["XDPGPU_HOST_THREADS"] = str(th)
+        else:
+            os.environ.pop("XDPGPU_HOST_THREADS", None)
+        u = hu if name.endswith("_huge") else cu
+        r = bench.e2e_run(0, u, cd, ce, nc // 2, args.batches, 4096, 0, ceil, flags, slots)
+        r.pop("pcie_ceiling", None)
+        r["mode"] = name
+        if not args.no_submit_cost:
+            r["submit_host_ms"] = round(submit_cost(u, cd, nc // 2, flags) * 1e3, 3)
+        print(json.dumps(r), flush=True)
 
 
 if __name__ == "__main__":

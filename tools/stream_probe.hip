@@ -91,6 +91,10 @@ __global__ __launch_bounds__(1024, 1) void stream_probe_kernel(Args a)
 		uint32_t nwin = (uint32_t)((A1 - A0 + kWin - 1) / kWin);
 		if (nwin > kMaxWin)
 			nwin = kMaxWin;   /* (the probe's pools stay far below) */
+		/* windows no frame starts in after the last start: empty */
+		for (uint32_t k = threadIdx.x; k <= nwin; k += blockDim.x)
+			wstart[k] = f1;
+		__syncthreads();
 		/* producer: window w's 32 loads of 1 KiB, wave p the p-th of each
 		 * four */
 		auto produce = [&](uint32_t w) {
@@ -132,8 +136,6 @@ __global__ __launch_bounds__(1024, 1) void stream_probe_kernel(Args a)
 				for (uint32_t k = wp + 1; k <= w && k < kMaxWin; k++)
 					wstart[k] = f;
 			}
-			if (threadIdx.x == 64 * kProd)
-				wstart[nwin] = f1;
 		}
 		__syncthreads();
 		for (uint32_t k = 0; k < nwin; k++) {

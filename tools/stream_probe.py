@@ -87,12 +87,22 @@ def main():
     idx = rng.choice(n, 4096, replace=False)
     r = rec.cpu().numpy().view(np.uint32).reshape(n, 4)
     bad = 0
+    badv = []
     for i in idx:
         lo, hi = int(eff[i]) & ~15, (int(eff[i]) + int(descs["len"][i]) + 15) & ~15
         s = int(umem[lo:hi].view("<u2").astype(np.uint64).sum())
         while s >> 16:
             s = (s & 0xFFFF) + (s >> 16)
-        bad += int(r[i, 0] != s)
+        if r[i, 0] != s:
+            bad += 1
+            f0 = (int(i) // 2048) * 2048
+            a0 = int(eff[f0]) & ~15
+            badv.append({"i": int(i), "len": int(descs["len"][i]), "seg_pos": int(i) - f0,
+                         "off": int(eff[i]) - a0, "win": (int(eff[i]) - a0) // 32768,
+                         "in_win": (int(eff[i]) - a0) % 32768, "got": int(r[i, 0]), "want": s,
+                         "rec": [int(x) for x in r[i, 1:]]})
+    for b in badv[:12]:
+        print("bad", b)
     algo = n * (16 + 16 + 44 + 1) + int(descs["len"].astype(np.int64).sum())
     out = {"frames": n, "pool_bytes": int(umem.nbytes), "algorithmic_bytes": algo,
            "probe_ms_median": float(np.median(res["probe_ms"])),
