@@ -48,10 +48,18 @@ constexpr uint32_t kDefaultMaxBatch = 1u << 20;
  * and returns when every call has. */
 class HostPool {
 public:
-	explicit HostPool(unsigned n) : n_(n ? n : 1)
+	/* as many of the n threads as the system gives (at least the
+	 * caller's): a failed thread creation must not cross the C ABI */
+	explicit HostPool(unsigned n)
 	{
-		for (unsigned t = 1; t < n_; t++)
-			th_.emplace_back([this, t] { loop(t); });
+		for (unsigned t = 1; t < n; t++) {
+			try {
+				th_.emplace_back([this, t] { loop(t); });
+			} catch (...) {
+				break;
+			}
+			n_ = t + 1;
+		}
 	}
 	~HostPool()
 	{
@@ -102,7 +110,7 @@ private:
 				done_.notify_one();
 		}
 	}
-	unsigned n_;
+	unsigned n_ = 1;
 	std::vector<std::thread> th_;
 	std::mutex mu_;
 	std::condition_variable cv_, done_;
@@ -1720,7 +1728,7 @@ int xdpgpu_host_threads(xdpgpu_ctx *ctx, uint32_t n)
 			return set_err(ctx, -ENOMEM, "host threads");
 	}
 	ctx->host_threads = n;
-	return (int)want;
+	return (int)ctx->hpool->size();
 }
 
 /* Copy a batch's frames into the slot's mirror: rows of chunks where they
