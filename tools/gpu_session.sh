@@ -33,6 +33,7 @@
 #   probe                  tools/order_probe (LDS-DMA / vmcnt ordering)
 #   hbm[:MODE]             tools/hbm_probe [MODE] (access-shape ceilings)
 #   e2e                    PCIe-inclusive host path (bench.py --e2e)
+#   e2ec[:T,T]             host compaction legs (tools/e2e_probe.py --compact)
 #   cli                    xdpsock-gpu over a 16 M-frame pool
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -174,6 +175,11 @@ for s in "$@"; do
 	probe) step probe 120 tools/order_probe 64 ;;
 	hbm) step "hbm_${arg:-all}" 300 tools/hbm_probe $arg ;;
 	e2e) step e2e 600 python3 bench.py --no-cpu --no-secondary --steps 10 ;;
+	e2ec)
+		# the chunked host path with XDPGPU_CFG_HOST_COMPACT, 4 KiB and huge
+		# pages, at the thread counts given (comma list, 0: the default)
+		step "e2ec_${arg:-0}" 600 python3 tools/e2e_probe.py --compact --no-submit-cost \
+			--threads "${arg:-0}" ;;
 	cli) step cli 300 bpf-examples_amd/apps/xdpsock-gpu --pool 16777216 --pool-kind udp4 \
 		-b 1048576 -C 67108864 --json -Q ;;
 	*) echo "unknown step $s"; exit 2 ;;
