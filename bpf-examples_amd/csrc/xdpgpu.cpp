@@ -29,6 +29,7 @@
 #include <thread>
 
 #include <sched.h>
+#include <sys/mman.h>
 
 #include "xdpgpu.h"
 #include "xdpgpu_internal.h"
@@ -269,6 +270,34 @@ const char *xdpgpu_last_error(xdpgpu_ctx *ctx)
 	return ctx ? ctx->err : "no context";
 }
 
+/* Host staging of the compaction: ordinary write-back memory (2 MiB
+ * aligned, advised for huge pages) that is then page-locked for the copy
+ * engine, so the host threads write it through their caches. */
+static void *staging_alloc(uint64_t bytes)
+{
+	const uint64_t sz = (bytes + (2u << 20) - 1) & ~(uint64_t)((2u << 20) - 1);
+	void *p = nullptr;
+	if (posix_memalign(&p, 2u << 20, sz))
+		return nullptr;
+	(void)madvise(p, sz, MADV_HUGEPAGE);
+	memset(p, 0, sz);   /* fault the pages in before they are locked */
+	if (hipHostRegister(p, sz, hipHostRegisterDefault) != hipSuccess) {
+		(void)hipGetLastError();
+		free(p);
+		return nullptr;
+	}
+	return p;
+}
+
+static void staging_free(void *p)
+{
+	if (!p)
+		return;
+	if (hipHostUnregister(p) != hipSuccess)
+		(void)hipGetLastError();
+	free(p);
+}
+
 static void free_slot(Slot &s)
 {
 	if (s.d_stats)
@@ -292,10 +321,8 @@ static void free_slot(Slot &s)
 	(void)hipFree(s.d_mirror);
 	(void)hipFree(s.d_pack);
 	(void)hipFree(s.d_poff);
-	if (s.h_pack)
-		(void)hipHostFree(s.h_pack);
-	if (s.h_poff)
-		(void)hipHostFree(s.h_poff);
+	staging_free(s.h_pack);
+	staging_free(s.h_poff);
 	(void)hipFree(s.d_erec);
 	(void)hipFree(s.d_ecnt);
 	if (s.h_ecnt)
@@ -1559,12 +1586,11 @@ static int ensure_pack(xdpgpu_ctx *ctx, Slot &s, uint64_t bytes, uint32_t n)
 	if (s.pack_cap < bytes + 64) {
 		const uint64_t cap = bytes + bytes / 4 + 64;
 		(void)hipFree(s.d_pack);
-		if (s.h_pack)
-			(void)hipHostFree(s.h_pack);
+		staging_free(s.h_pack);
 		s.d_pack = nullptr;
 		s.h_pack = nullptr;
 		s.pack_cap = 0;
-		if (hipHostMalloc((void **)&s.h_pack, cap, 0) != hipSuccess ||
+		if (!(s.h_pack = (uint8_t *)staging_alloc(cap)) ||
 		    hipMalloc(&s.d_pack, cap) != hipSuccess)
 			return set_err(ctx, -ENOMEM, "compaction staging of %llu bytes",
 				       (unsigned long long)cap);
@@ -1573,12 +1599,11 @@ static int ensure_pack(xdpgpu_ctx *ctx, Slot &s, uint64_t bytes, uint32_t n)
 	if (s.poff_cap < n) {
 		const uint64_t cap = (uint64_t)n + n / 4 + 64;
 		(void)hipFree(s.d_poff);
-		if (s.h_poff)
-			(void)hipHostFree(s.h_poff);
+		staging_free(s.h_poff);
 		s.d_poff = nullptr;
 		s.h_poff = nullptr;
 		s.poff_cap = 0;
-		if (hipHostMalloc((void **)&s.h_poff, cap * 4, 0) != hipSuccess ||
+		if (!(s.h_poff = (uint32_t *)staging_alloc(cap * 4)) ||
 		    hipMalloc(&s.d_poff, cap * 4) != hipSuccess)
 			return set_err(ctx, -ENOMEM, "compaction offsets");
 		s.poff_cap = cap;
