@@ -29,12 +29,26 @@
 
 namespace {
 
-constexpr int kWaves = 16, kProd = 4, kCons = kWaves - kProd;
-constexpr int kWin = 32 * 1024, kSlots = 4, kRing = kWin * kSlots;
-constexpr int kGroup = 8;                       /* lanes a frame */
+#ifndef SP_PROD
+#define SP_PROD 4
+#endif
+#ifndef SP_WIN_KB
+#define SP_WIN_KB 32
+#endif
+#ifndef SP_GROUP
+#define SP_GROUP 8
+#endif
+constexpr int kWaves = 16, kProd = SP_PROD, kCons = kWaves - kProd;
+constexpr int kWin = SP_WIN_KB * 1024, kSlots = 4, kRing = kWin * kSlots;
+constexpr int kGroup = SP_GROUP;                /* lanes a frame */
+static_assert(kWin % (1024 * kProd) == 0, "whole 1 KiB loads per producer");
+/* s_waitcnt vmcnt(one window's loads of a producer wave), nothing else */
+constexpr int kLoadsPerWin = kWin / 1024 / kProd;
+static_assert(kLoadsPerWin < 64, "vmcnt is 6 bits");
+constexpr int kVmcntNew = 0x0f70 | (kLoadsPerWin & 15) | ((kLoadsPerWin >> 4) << 14);
 constexpr int kFramesPerRound = kCons * 64 / kGroup;
 constexpr uint32_t kSeg = 2048;
-constexpr uint32_t kMaxWin = 256;             /* windows a segment       */
+constexpr uint32_t kMaxWin = 512;             /* windows a segment       */
 
 struct Args {
 	const uint8_t *pool;
@@ -143,7 +157,7 @@ __global__ __launch_bounds__(1024, 1) void stream_probe_kernel(Args a)
 				if (k + 3 < nwin) {
 					produce(k + 3);
 					/* window k + 3's 8 loads may stay in flight */
-					__builtin_amdgcn_s_waitcnt(0x0f70 | (kWin / 1024 / kProd));
+					__builtin_amdgcn_s_waitcnt(kVmcntNew);
 				} else {
 					__builtin_amdgcn_s_waitcnt(0x0f70);
 				}
@@ -178,8 +192,8 @@ __global__ __launch_bounds__(1024, 1) void stream_probe_kernel(Args a)
 					const uint32_t o0 = (uint32_t)((lo - A0) % kRing);
 					const uint4 h = *reinterpret_cast<const uint4 *>(
 						ring + ((o0 + 16 * (sub & 3)) % kRing));
-					const uint32_t hx = __shfl(h.x, (lane & ~7) + 1, 64);
-					const uint32_t hy = __shfl(h.y, (lane & ~7) + 2, 64);
+					const uint32_t hx = __shfl(h.x, (lane & ~(kGroup - 1)) + 1, 64);
+					const uint32_t hy = __shfl(h.y, (lane & ~(kGroup - 1)) + 2, 64);
 					if (sub == 0) {
 						a.verdict[f] = (uint8_t)(4 ^ (fold16(s) & 1));
 						a.rec[f] = make_uint4(fold16(s), h.x, hx, len);

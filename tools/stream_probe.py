@@ -29,8 +29,10 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--kind", type=int, default=xdpgpu.POOL_IMIX)
     ap.add_argument("--size", type=int, default=64)
+    ap.add_argument("--lib", default="tools/libstream_probe.so",
+                    help="the probe build (a variant) to time")
     a = ap.parse_args()
-    lib = C.CDLL(os.path.join(ROOT, "tools", "libstream_probe.so"))
+    lib = C.CDLL(os.path.join(ROOT, a.lib))
     lib.stream_probe.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32, C.c_void_p,
                                  C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
     n = a.frames
@@ -104,7 +106,7 @@ def main():
     for b in badv[:12]:
         print("bad", b)
     algo = n * (16 + 16 + 44 + 1) + int(descs["len"].astype(np.int64).sum())
-    out = {"frames": n, "pool_bytes": int(umem.nbytes), "algorithmic_bytes": algo,
+    out = {"lib": a.lib, "frames": n, "pool_bytes": int(umem.nbytes), "algorithmic_bytes": algo,
            "probe_ms_median": float(np.median(res["probe_ms"])),
            "product_ms_median": float(np.median(res["product_ms"])),
            "probe_frac": round(algo / (np.median(res["probe_ms"]) * 1e-3) / 8e12, 4),
