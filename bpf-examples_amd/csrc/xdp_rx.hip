@@ -808,72 +808,112 @@ __device__ __forceinline__ uint32_t swap_in_halves(uint32_t x)
 	return ((x & 0x00ff00ffu) << 8) | ((x >> 8) & 0x00ff00ffu);
 }
 
+/* The payload sums of the multi-buffer packets of a batch (the lanes with
+ * need): packet bytes [max(l4, WIN), rhi) summed fragment by fragment, each
+ * fragment's part with the parity of its offset in the packet, the check
+ * word taken out where it lies past the window.  Four packets at a time,
+ * 16 lanes each, 1 KiB of a packet a step (kPktU 16-byte loads a lane):
+ * four chains of dependent loads run at once where round 5's form (the
+ * whole wave on one packet at a time, 4 KiB a step) ran one.  262 144 x
+ * 9000 B packets in 4 KiB fragments: 0.490 vs 0.587-0.602 ms, alternating
+ * processes on one box (tools/r06_pk_session.sh); the next fragment's
+ * descriptor loaded under the current one's steps was slower (0.505-0.515).
+ * The packet kernel runs at two blocks a CU for it (166 VGPRs, no spill;
+ * 128 spilled). */
+constexpr int kPktG = 4, kPktL = kWave / kPktG, kPktU = 4;
 template <int WIN>
 __device__ uint32_t pkt_ext_sums(const RxArgs &a, bool need, uint64_t head, uint32_t last,
 				 uint32_t l4, uint32_t rhi, uint32_t chk, uint32_t c4,
 				 int lane)
 {
+	const int grp = lane / kPktL, gl = lane % kPktL;
 	uint64_t mask = __ballot(need);
 	uint32_t out = 0;
 	while (mask) {
-		const int sl = __builtin_ctzll(mask);
-		mask &= mask - 1;
-		const uint64_t first = ((uint64_t)readlane32((uint32_t)(head >> 32), sl) << 32) |
-				       readlane32((uint32_t)head, sl);
-		const uint32_t lst = readlane32(last, sl);
-		const uint32_t sl4 = readlane32(l4, sl);
+		/* group g takes the g-th lowest packet left (none: -1) */
+		int sl = -1;
+		uint64_t m = mask;
+#pragma unroll
+		for (int g = 0; g < kPktG; g++) {
+			const int b = m ? __builtin_ctzll(m) : -1;
+			if (g == grp)
+				sl = b;
+			m &= m - 1;
+		}
+		mask = m;
+		const int src = sl >= 0 ? sl : 0;
+		/* (descriptor indices are below a.n, a u32) */
+		const uint32_t first = (uint32_t)__shfl((int)(uint32_t)head, src, kWave);
+		const uint32_t lst = (uint32_t)__shfl((int)last, src, kWave);
+		const uint32_t sl4 = (uint32_t)__shfl((int)l4, src, kWave);
+		const uint32_t hi = (uint32_t)__shfl((int)rhi, src, kWave);
 		const uint32_t lo = sl4 > (uint32_t)WIN ? sl4 : (uint32_t)WIN;
-		const uint32_t hi = readlane32(rhi, sl);
 		uint32_t acc = 0;
-		uint32_t o = 0;       /* the fragment's packet offset */
-		for (uint64_t j = first; j <= lst && o < hi; j++) {
-			const xdpgpu_desc d = a.desc[j];
-			const uint64_t eff = (d.addr & ((1ull << 48) - 1)) + (d.addr >> 48);
-			const uint32_t fend = o + d.len + (j == lst ? 1u : 0u);
-			const uint32_t x0 = lo > o ? lo : o, x1 = hi < fend ? hi : fend;
-			if (x0 < x1) {
-				const uint64_t p0 = eff + (x0 - o);
-				uint64_t p1 = eff + (x1 - o);
-				p1 = p1 < a.usize ? p1 : a.usize;
-				const bool sw = ((eff - o) & 1) != 0;
-				for (uint64_t b = p0 & ~15ull; b < p1; b += 4 * 16 * kWave) {
-					uint4 v[4];
-					uint64_t q[4];
+		if (sl >= 0) {
+			uint32_t o = 0;       /* the fragment's packet offset */
+			for (uint32_t j = first; j <= lst && o < hi; j++) {
+				const uint4 d = *reinterpret_cast<const uint4 *>(a.desc + j);
+				const uint64_t addr = ((uint64_t)d.y << 32) | d.x;
+				const uint64_t eff = (addr & ((1ull << 48) - 1)) + (addr >> 48);
+				const uint32_t dlen = d.z;
+				const uint32_t fend = o + dlen + (j == lst ? 1u : 0u);
+				const uint32_t x0 = lo > o ? lo : o, x1 = hi < fend ? hi : fend;
+				if (x0 < x1) {
+					const uint64_t p0 = eff + (x0 - o);
+					uint64_t p1 = eff + (x1 - o);
+					p1 = p1 < a.usize ? p1 : a.usize;
+					const bool sw = ((eff - o) & 1) != 0;
+					for (uint64_t b = p0 & ~15ull; b < p1; b += kPktU * 16 * kPktL) {
+						uint4 v[kPktU];
+						uint64_t q[kPktU];
 #pragma unroll
-					for (int k = 0; k < 4; k++) {
-						q[k] = b + 16ull * (lane + kWave * k);
-						v[k] = make_uint4(0, 0, 0, 0);
-						if (q[k] < p1)
-							v[k] = *reinterpret_cast<const uint4 *>(a.umem + q[k]);
-					}
+						for (int k = 0; k < kPktU; k++) {
+							q[k] = b + 16ull * (gl + kPktL * k);
+							v[k] = make_uint4(0, 0, 0, 0);
+							if (q[k] < p1)
+								v[k] = *reinterpret_cast<const uint4 *>(a.umem + q[k]);
+						}
 #pragma unroll
-					for (int k = 0; k < 4; k++) {
-						if (q[k] < p0 || q[k] + 16 > p1) {
-							const uint4 m = chunk_keep(q[k], p0, p1);
-							v[k].x &= m.x;
-							v[k].y &= m.y;
-							v[k].z &= m.z;
-							v[k].w &= m.w;
+						for (int k = 0; k < kPktU; k++) {
+							if (q[k] < p0 || q[k] + 16 > p1) {
+								const uint4 mk = chunk_keep(q[k], p0, p1);
+								v[k].x &= mk.x;
+								v[k].y &= mk.y;
+								v[k].z &= mk.z;
+								v[k].w &= mk.w;
+							}
+							if (sw) {
+								v[k].x = swap_in_halves(v[k].x);
+								v[k].y = swap_in_halves(v[k].y);
+								v[k].z = swap_in_halves(v[k].z);
+								v[k].w = swap_in_halves(v[k].w);
+							}
+							acc += halves(v[k].x) + halves(v[k].y) + halves(v[k].z) +
+							       halves(v[k].w);
 						}
-						if (sw) {
-							v[k].x = swap_in_halves(v[k].x);
-							v[k].y = swap_in_halves(v[k].y);
-							v[k].z = swap_in_halves(v[k].z);
-							v[k].w = swap_in_halves(v[k].w);
-						}
-						acc += halves(v[k].x) + halves(v[k].y) + halves(v[k].z) +
-						       halves(v[k].w);
 					}
 				}
+				o += dlen;
 			}
-			o += d.len;
 		}
-		uint32_t t = wave_sum32(acc);
-		if (readlane32(chk, sl) >= (uint32_t)WIN)
-			t -= readlane32(c4, sl);
+		/* the group's sum (16 lanes), the check word out, folded */
+#pragma unroll
+		for (int off = 1; off < kPktL; off <<= 1)
+			acc += (uint32_t)__shfl_xor((int)acc, off, kPktL);
+		const uint32_t schk = (uint32_t)__shfl((int)chk, src, kWave);
+		const uint32_t sc4 = (uint32_t)__shfl((int)c4, src, kWave);
+		uint32_t t = acc;
+		if (schk >= (uint32_t)WIN)
+			t -= sc4;
 		const uint32_t f = fold16(t);
-		if (lane == sl)
-			out = f;
+		/* to the packet's own lane */
+#pragma unroll
+		for (int g = 0; g < kPktG; g++) {
+			const int sg = __builtin_amdgcn_readlane(sl, g * kPktL);
+			const uint32_t fg = (uint32_t)__builtin_amdgcn_readlane((int)f, g * kPktL);
+			if (lane == sg)
+				out = fg;
+		}
 	}
 	return out;
 }
@@ -3405,7 +3445,7 @@ __global__ __launch_bounds__(kCuBlock, 1) void xdp_rx_db_kernel(RxArgs a)
  * frag_count): a lane per descriptor, the packets' first descriptors
  * through generic_batch<WIN, true>, grid-strided over the batch's tiles. */
 template <int WIN>
-__global__ __launch_bounds__(kBlock, 4) void xdp_rx_packet_kernel(RxArgs a)
+__global__ __launch_bounds__(kBlock, 2) void xdp_rx_packet_kernel(RxArgs a)
 {
 	constexpr int SDW = WIN / 4 + 1;
 	__shared__ uint32_t lds[kWavesPerBlock * kWave * SDW + 8];

@@ -169,13 +169,16 @@ def test_tx_only_write_back():
     assert np.array_equal(host, ou)
 
 
-@pytest.mark.parametrize("gather", [False, True], ids=["copies", "gather"])
-def test_frags_ring_host_path(gather):
+@pytest.mark.parametrize("mode", ["copies", "gather", "compact"])
+def test_frags_ring_host_path(mode):
     """Multi-buffer packets on the host path, two slots in flight, echo on:
     every fragment's bytes only as the oracle writes them.  With the gather
-    (the UMEM registered with a chunk size) every fragment takes the byte
-    after it, so the packet's over-read byte after its last fragment is
-    there."""
+    (the UMEM registered with a chunk size) or the host compaction every
+    fragment takes the byte after it, so the packet's over-read byte after
+    its last fragment is there."""
+    gather = mode == "gather"
+    flags = {"copies": 0, "gather": xdpgpu.CFG_UMEM_GATHER,
+             "compact": xdpgpu.CFG_HOST_COMPACT}[mode]
     import test_frags as TF
     umem, descs = TF.pool("echo6")
     u2, d2, _ = TF.split_pool(umem, descs, 3)
@@ -188,10 +191,11 @@ def test_frags_ring_host_path(gather):
         batches.append(np.arange(bounds[p0], bounds[min(p0 + per, len(heads))]))
     host = u2.copy()
     hs = {}
-    got, st = run_ring(host, d2, batches,
-                       ECHO | xdpgpu.CFG_FRAGS | (xdpgpu.CFG_UMEM_GATHER if gather else 0), 0,
-                       fmt=xdpgpu.TUPLE_V4, chunk=4096 if gather else 0, host_stats=hs)
+    got, st = run_ring(host, d2, batches, ECHO | xdpgpu.CFG_FRAGS | flags, 0,
+                       fmt=xdpgpu.TUPLE_V4, chunk=4096 if mode != "copies" else 0,
+                       host_stats=hs)
     assert hs["umem_gathers"] == (len(batches) if gather else 0), hs
+    assert hs["umem_compacted"] == (len(batches) if mode == "compact" else 0), hs
     ou = u2.copy()
     want, ost = oracle_ring(ou, d2, batches, ECHO | xdpgpu.CFG_FRAGS, fmt=xdpgpu.TUPLE_V4)
     for k, (g, w) in enumerate(zip(got, want)):
@@ -310,6 +314,10 @@ def test_device_entry_points_reject_host_memory():
         for host in (pinned.array, umem):
             with pytest.raises(xdpgpu.XdpGpuError, match="-22|Invalid"):
                 ctx.process_dev(host, umem.nbytes, dd, n, dv)
+            # the two-slot form checks the same way, on either slot
+            for slot in (0, 1):
+                with pytest.raises(xdpgpu.XdpGpuError, match="-22|Invalid"):
+                    ctx.submit_dev(slot, host, umem.nbytes, dd, n, dv)
         du = to_dev(umem)
         ctx.process_dev(du, umem.nbytes, dd, n, dv)
         torch.cuda.synchronize()
