@@ -1451,9 +1451,34 @@ constexpr bool kTup6Tile = XDP_TUP6_TILE != 0;
 /* Diagnostic builds of the bulk pass (XDP_TAIL_DIAG, never the product):
  * bit 0: no output stores (record, verdict, tuple); bit 1: no payload
  * loads (the range summed as zeros); bit 2: no record store; bit 3: no
- * verdict store */
+ * verdict store; bit 4: the record stored over the frame's n/2 away;
+ * bit 5: a load of the record instead of its store; bit 6: lane 0's record
+ * alone; bit 7: one dword of each record */
 #ifndef XDP_TAIL_DIAG
 #define XDP_TAIL_DIAG 0
+#endif
+/* The bulk pass's record store as a buffer store with these cache-policy
+ * bits (A/B knob; -1: the plain non-temporal global store) */
+#ifndef XDP_TAIL_REC_AUX
+#define XDP_TAIL_REC_AUX -1
+#endif
+/* Latency probe of the bulk pass (stamps builds only, XDP_LAT_PROBE): per
+ * wave, slot 4 counts bulk batches (x100), slot 6 the ticks from a batch's
+ * start to its list entry, descriptor and record in registers (an explicit
+ * vmcnt(0): with bit 1 clear it also waits for the previous batch's record
+ * store, vmcnt retiring in order), slot 7 (bit 1) the ticks of a vmcnt(0)
+ * right after the record store */
+#if defined(XDPGPU_STAMPS) && defined(XDP_LAT_PROBE)
+#define LAT_NOW(v) \
+	asm volatile("" ::: "memory"); \
+	const unsigned long long v = __builtin_amdgcn_s_memrealtime(); \
+	asm volatile("" ::: "memory")
+#define LAT_WAIT() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+#define LAT_ACC(sid, lane, k, d) \
+	do { \
+		if ((lane) == 0 && (sid) < (uint64_t)kStampWaves) \
+			g_stamp[8 * (sid) + (k)] += (d); \
+	} while (0)
 #endif
 /* Batch-adaptive group size (build knob): 1 smaller groups for batches
  * of short ranges only; 0 always G */
@@ -1581,8 +1606,12 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 					   uint4 *part4, int lane,
 					   const void *list, uint32_t nb,
 					   uint32_t (&cnt)[CNT_FRAG + 1],
-					   uint64_t &my_bytes)
+					   uint64_t &my_bytes, uint64_t sid = 0)
 {
+	(void)sid;
+#ifdef LAT_NOW
+	LAT_NOW(lat0);
+#endif
 	uint32_t *part = reinterpret_cast<uint32_t *>(part4);
 	const bool act = (uint32_t)lane < nb;
 	uint4 ye = make_uint4(0, 0, 0, 0);
@@ -1597,6 +1626,12 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 		i = 0;
 	const uint4 dv = *reinterpret_cast<const uint4 *>(a.desc + i);
 	uint4 rv = *reinterpret_cast<const uint4 *>(a.res + i);
+#ifdef LAT_NOW
+	LAT_WAIT();
+	LAT_NOW(lat1);
+	LAT_ACC(sid, lane, 6, lat1 - lat0);
+	LAT_ACC(sid, lane, 4, 100ull);
+#endif
 	/* an IPv6 frame whose 128-byte window summed to byte 128 (fast_tile's
 	 * mark in the nvlan byte, cleared here) */
 	bool w6 = false, tsh = false;
@@ -1782,10 +1817,44 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 		rv.w = l4 | (cl << 16);
 		if constexpr (XDP_TAIL_DIAG & 4) {
 			/* diagnostic: no record store */
+		} else if constexpr (XDP_TAIL_DIAG & 16) {
+			/* diagnostic: the record stored over another frame's, half
+			 * the batch away (a line this pass has not read) */
+			st_nt16(a.res + (i + a.n / 2) % a.n, rv);
+		} else if constexpr (XDP_TAIL_DIAG & 256) {
+			/* diagnostic (pools without exception frames only): the
+			 * record stored into the payload list's scratch, lines no
+			 * pass of the launch writes */
+			st_nt16(a.ylist ? reinterpret_cast<uint4 *>(a.ylist) + i
+					: reinterpret_cast<uint4 *>(a.res + i), rv);
+		} else if constexpr (XDP_TAIL_DIAG & 32) {
+			/* diagnostic: a load of the record instead of its store */
+			const uint4 q = ld_nt16(a.res + i);
+			my_bytes += q.x == 0x9e3779b9u;
+		} else if constexpr (XDP_TAIL_DIAG & 64) {
+			/* diagnostic: lane 0's record alone */
+			if (lane == 0)
+				st_nt16(a.res + i, rv);
+		} else if constexpr (XDP_TAIL_DIAG & 128) {
+			/* diagnostic: the record's second dword alone */
+			__builtin_nontemporal_store(rv.y, reinterpret_cast<uint32_t *>(a.res + i) + 1);
+		} else if constexpr (XDP_TAIL_REC_AUX >= 0) {
+			const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+				a.res, 0, 0x7fffffff, 0x00020000);
+			__builtin_amdgcn_raw_buffer_store_b128((v4u_t){rv.x, rv.y, rv.z, rv.w}, rr,
+							       (uint32_t)(16 * i), 0, XDP_TAIL_REC_AUX);
 		} else if constexpr (kTailRecNt)
 			st_nt16(a.res + i, rv);
 		else
 			*reinterpret_cast<uint4 *>(a.res + i) = rv;
+#ifdef LAT_NOW
+		if constexpr ((XDP_LAT_PROBE & 2) != 0) {
+			LAT_NOW(lat2);
+			LAT_WAIT();
+			LAT_NOW(lat3);
+			LAT_ACC(sid, lane, 7, lat3 - lat2);
+		}
+#endif
 		if (tup6) {
 			/* the addresses and ports, from the words loaded with
 			 * the batch, shifted by the tags (nv dwords; the fast
@@ -2649,7 +2718,8 @@ __device__ __forceinline__ void rx_tail(const RxArgs &a, const FastWave &w,
 			const uint32_t b = (q - nxb) * kWave;
 			bulk_batch<kTailU, true, false, kTailG, WIN, EC>(
 				a, meta, part4, lane, w.bl + b,
-				bc - b < (uint32_t)kWave ? bc - b : kWave, cnt, my_bytes);
+				bc - b < (uint32_t)kWave ? bc - b : kWave, cnt, my_bytes,
+				rb * nw + wid);
 			STAMP_ADD(rb * nw + wid, lane, 5);
 			continue;
 		}
