@@ -185,12 +185,15 @@ def device_identity(local: int) -> dict:
 def check_distinct_devices(idents: list, rehearse: bool) -> None:
     """One rank per GPU: two ranks on one device would time each other's
     launches as their own (the scaling curve would be wrong, not slow), so
-    unless rehearsing that is an error naming the ranks."""
+    unless rehearsing that is an error naming the ranks.  Two ranks share a
+    device when both their UUIDs and their PCI bus ids match, so that a
+    driver reporting one UUID (or one bus id) for every device does not stop
+    a run on distinct GPUs."""
     if rehearse:
         return
     seen = {}
     for r, d in enumerate(idents):
-        key = d.get("uuid") or d["pci_bus_id"]
+        key = (d.get("uuid") or "", d["pci_bus_id"])
         if key in seen:
             raise SystemExit(f"ranks {seen[key]} and {r} share device {d['pci_bus_id']} "
                              f"({key}): one rank per GPU (XDPGPU_BENCH_REHEARSE=1 rehearses "

@@ -100,8 +100,8 @@ def test_gather_leg_child(monkeypatch):
 
 def test_check_distinct_devices():
     """One rank per GPU unless rehearsing: two ranks on one device (same
-    UUID, or the same PCI bus id when the UUID is empty) is an error naming
-    both ranks."""
+    UUID and same PCI bus id) is an error naming both ranks; one UUID, or
+    one bus id, reported for distinct devices is not."""
     a = {"pci_bus_id": "0000:05:00", "uuid": "u0"}
     b = {"pci_bus_id": "0000:15:00", "uuid": "u1"}
     bench.check_distinct_devices([a, b], False)
@@ -110,6 +110,8 @@ def test_check_distinct_devices():
     with pytest.raises(SystemExit, match="ranks 1 and 2 share"):
         bench.check_distinct_devices([a, dict(b, uuid=""), dict(b, uuid="")], False)
     bench.check_distinct_devices([a, dict(a)], True)
+    bench.check_distinct_devices([a, dict(b, uuid="u0")], False)
+    bench.check_distinct_devices([a, dict(b, pci_bus_id=a["pci_bus_id"])], False)
 
 
 def _gather_rank(rank, world, port, out_dir):
