@@ -1601,12 +1601,35 @@ __device__ __forceinline__ void stream_short(const RxArgs &a, const uint4 *meta,
 	}
 }
 
+/* The bulk pass's records staged in the wave's free LDS (build knob,
+ * XDP_REC_STAGE batches, 0 off) and stored XDP_REC_STAGE batches at a
+ * time: a 64-lane record store costs the launch about 0.36 us of its CU's
+ * time while payload loads stream (EXPERIMENTS.md §5.2, round 6) */
+#ifndef XDP_REC_STAGE
+#define XDP_REC_STAGE 4
+#endif
+constexpr uint32_t kRecStage = XDP_REC_STAGE;
+static_assert(kRecStage <= 4, "the tail's free LDS holds four batches of records");
+/* a wave's staged records (rec: kRecStage x 64 uint4) and their frame
+ * indices (idx: kRecStage x 64, ~0 none), stored and emptied */
+__device__ __forceinline__ void rec_flush(const RxArgs &a, const uint4 *rec,
+					  const uint32_t *idx, uint32_t &nst, int lane)
+{
+	for (uint32_t s = 0; s < nst; s++) {
+		const uint32_t i = idx[s * kWave + lane];
+		const uint4 r = rec[s * kWave + lane];
+		if (i != ~0u)
+			st_nt16(a.res + i, r);
+	}
+	nst = 0;
+}
+
 template <int U, bool NT, bool GEN, int G, int WIN = 64, bool EC = true>
 __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 					   uint4 *part4, int lane,
 					   const void *list, uint32_t nb,
 					   uint32_t (&cnt)[CNT_FRAG + 1],
-					   uint64_t &my_bytes, uint64_t sid = 0)
+					   uint64_t &my_bytes, uint32_t &nst, uint64_t sid = 0)
 {
 	(void)sid;
 #ifdef LAT_NOW
@@ -1838,6 +1861,9 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 		} else if constexpr (XDP_TAIL_DIAG & 128) {
 			/* diagnostic: the record's second dword alone */
 			__builtin_nontemporal_store(rv.y, reinterpret_cast<uint32_t *>(a.res + i) + 1);
+		} else if constexpr (kRecStage > 0) {
+			/* staged (rec_flush) */
+			meta[320 + nst * kWave + lane] = rv;
 		} else if constexpr (XDP_TAIL_REC_AUX >= 0) {
 			const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
 				a.res, 0, 0x7fffffff, 0x00020000);
@@ -1907,6 +1933,22 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 		cnt[CNT_L4_ABSENT] += __popcll(__ballot(fin && absent));
 		if constexpr (GEN)
 			cnt[CNT_FRAG] += __popcll(__ballot(act && (rv.z & XDPGPU_F_FRAG)));
+	}
+	if constexpr (kRecStage > 0) {
+		uint32_t *idx = reinterpret_cast<uint32_t *>(meta + 320 + kRecStage * kWave);
+		idx[nst * kWave + lane] = act && !abort6 && !(XDP_TAIL_DIAG & 1) ? (uint32_t)i : ~0u;
+		nst = __builtin_amdgcn_readfirstlane(nst + 1);
+		if (nst == kRecStage) {
+			__builtin_amdgcn_wave_barrier();
+#pragma unroll
+			for (uint32_t s = 0; s < kRecStage; s++) {
+				const uint32_t j = idx[s * kWave + lane];
+				const uint4 r = meta[320 + s * kWave + lane];
+				if (j != ~0u)
+					st_nt16(a.res + j, r);
+			}
+			nst = 0;
+		}
 	}
 	__builtin_amdgcn_wave_barrier();
 }
@@ -2697,6 +2739,8 @@ __device__ __forceinline__ void rx_tail(const RxArgs &a, const FastWave &w,
 	 * entries visible): by then only batches already claimed remain. */
 	const uint32_t nbb = (bc + kWave - 1) / kWave, nxb = (xc + kWave - 1) / kWave;
 	uint32_t ycn = 0, nyb = 0;
+	/* staged batches of records (kRecStage) */
+	uint32_t nst = 0;
 	bool ready = nxb == 0;
 	STAMP_T0();
 	for (;;) {
@@ -2718,7 +2762,7 @@ __device__ __forceinline__ void rx_tail(const RxArgs &a, const FastWave &w,
 			const uint32_t b = (q - nxb) * kWave;
 			bulk_batch<kTailU, true, false, kTailG, WIN, EC>(
 				a, meta, part4, lane, w.bl + b,
-				bc - b < (uint32_t)kWave ? bc - b : kWave, cnt, my_bytes,
+				bc - b < (uint32_t)kWave ? bc - b : kWave, cnt, my_bytes, nst,
 				rb * nw + wid);
 			STAMP_ADD(rb * nw + wid, lane, 5);
 			continue;
@@ -2743,9 +2787,12 @@ __device__ __forceinline__ void rx_tail(const RxArgs &a, const FastWave &w,
 		const uint32_t b = yq * kWave;
 		bulk_batch<kTailU, true, true, kTailG>(
 			a, meta, part4, lane, yl + b, ycn - b < (uint32_t)kWave ? ycn - b : kWave,
-			cnt, my_bytes);
+			cnt, my_bytes, nst);
 		STAMP_ADD(rb * nw + wid, lane, 6);
 	}
+	if constexpr (kRecStage > 0)
+		rec_flush(a, meta + 320,
+			  reinterpret_cast<const uint32_t *>(meta + 320 + kRecStage * kWave), nst, lane);
 }
 
 /*
