@@ -1608,18 +1608,84 @@ __device__ __forceinline__ void stream_short(const RxArgs &a, const uint4 *meta,
 #ifndef XDP_REC_STAGE
 #define XDP_REC_STAGE 4
 #endif
+/* XDP_REC_RELOAD (build knob): 0 stages whole records (16 bytes and the
+ * frame index a frame, four batches in the 5 KiB); 1 stages only what the
+ * bulk pass adds (the frame index, ~sum and l4 offset a frame, two flag
+ * masks a batch: up to nine batches), merged into the tile's record
+ * reloaded at the store (a load of that shape is free, a store is not) */
+#ifndef XDP_REC_RELOAD
+#define XDP_REC_RELOAD 0
+#endif
 constexpr uint32_t kRecStage = XDP_REC_STAGE;
-static_assert(kRecStage <= 4, "the tail's free LDS holds four batches of records");
-/* a wave's staged records (rec: kRecStage x 64 uint4) and their frame
- * indices (idx: kRecStage x 64, ~0 none), stored and emptied */
-__device__ __forceinline__ void rec_flush(const RxArgs &a, const uint4 *rec,
-					  const uint32_t *idx, uint32_t &nst, int lane)
+constexpr bool kRecReload = XDP_REC_RELOAD != 0;
+/* records reloaded at once when a full stage is stored (XDP_REC_GROUP) */
+#ifndef XDP_REC_GROUP
+#define XDP_REC_GROUP 4
+#endif
+constexpr uint32_t kRecGroup = XDP_REC_GROUP;
+static_assert(kRecStage <= (kRecReload ? 9u : 4u),
+	      "the tail's free LDS (wave buffer from uint4 320) holds these batches");
+/* the staging area: whole records (kRecReload 0) at meta + 320, then the
+ * frame indices (~0: none), then (kRecReload 1) the ~sum | l4 << 16 words
+ * and the batches' L4_OK / L4_ABSENT masks */
+__device__ __forceinline__ uint32_t *stage_idx(uint4 *meta)
+{
+	return reinterpret_cast<uint32_t *>(meta + 320 + (kRecReload ? 0u : kRecStage * kWave));
+}
+
+/* store staged batch s (lane's frame) */
+__device__ __forceinline__ void rec_store_staged(const RxArgs &a, uint4 *meta, uint32_t s, int lane)
+{
+	const uint32_t *ix = stage_idx(meta);
+	const uint32_t j = ix[s * kWave + lane];
+	if constexpr (!kRecReload) {
+		const uint4 r = meta[320 + s * kWave + lane];
+		if (j != ~0u)
+			st_nt16(a.res + j, r);
+	}
+}
+
+/* the reload form for batches [s0, s0 + C): C records loaded, merged and
+ * stored */
+template <uint32_t C>
+__device__ __forceinline__ void rec_flush_reload(const RxArgs &a, uint4 *meta, uint32_t s0,
+						 int lane)
+{
+	const uint32_t *ix = stage_idx(meta);
+	const uint32_t *pw = ix + kRecStage * kWave;
+	const uint64_t *mk = reinterpret_cast<const uint64_t *>(ix + 2 * kRecStage * kWave);
+	uint32_t j[C];
+	uint4 r[C];
+#pragma unroll
+	for (uint32_t u = 0; u < C; u++) {
+		j[u] = ix[(s0 + u) * kWave + lane];
+		r[u] = make_uint4(0, 0, 0, 0);
+		if (j[u] != ~0u)
+			r[u] = *reinterpret_cast<const uint4 *>(a.res + j[u]);
+	}
+#pragma unroll
+	for (uint32_t u = 0; u < C; u++) {
+		const uint32_t p = pw[(s0 + u) * kWave + lane];
+		const uint64_t okm = mk[2 * (s0 + u)], abm = mk[2 * (s0 + u) + 1];
+		uint4 x = r[u];
+		x.y = (x.y & 0xffff) | (p << 16);
+		/* (fast_tile's marks in bits 30-31 cleared; nvlan is 0..2) */
+		x.z = (x.z & 0x3fffffffu) | (((okm >> lane) & 1) ? XDPGPU_F_L4_OK : 0u) |
+		      (((abm >> lane) & 1) ? XDPGPU_F_L4_ABSENT : 0u);
+		x.w = (p >> 16) | (x.w & 0xffff0000u);
+		if (j[u] != ~0u)
+			st_nt16(a.res + j[u], x);
+	}
+}
+
+/* every staged batch stored (the end of the tail) */
+__device__ __forceinline__ void rec_flush(const RxArgs &a, uint4 *meta, uint32_t &nst, int lane)
 {
 	for (uint32_t s = 0; s < nst; s++) {
-		const uint32_t i = idx[s * kWave + lane];
-		const uint4 r = rec[s * kWave + lane];
-		if (i != ~0u)
-			st_nt16(a.res + i, r);
+		if constexpr (kRecReload)
+			rec_flush_reload<1>(a, meta, s, lane);
+		else
+			rec_store_staged(a, meta, s, lane);
 	}
 	nst = 0;
 }
@@ -1862,8 +1928,9 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 			/* diagnostic: the record's second dword alone */
 			__builtin_nontemporal_store(rv.y, reinterpret_cast<uint32_t *>(a.res + i) + 1);
 		} else if constexpr (kRecStage > 0) {
-			/* staged (rec_flush) */
-			meta[320 + nst * kWave + lane] = rv;
+			/* staged (rec_flush; the reload form keeps its own words) */
+			if constexpr (!kRecReload)
+				meta[320 + nst * kWave + lane] = rv;
 		} else if constexpr (XDP_TAIL_REC_AUX >= 0) {
 			const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
 				a.res, 0, 0x7fffffff, 0x00020000);
@@ -1935,17 +2002,33 @@ __device__ __forceinline__ void bulk_batch(const RxArgs &a, uint4 *meta,
 			cnt[CNT_FRAG] += __popcll(__ballot(act && (rv.z & XDPGPU_F_FRAG)));
 	}
 	if constexpr (kRecStage > 0) {
-		uint32_t *idx = reinterpret_cast<uint32_t *>(meta + 320 + kRecStage * kWave);
-		idx[nst * kWave + lane] = act && !abort6 && !(XDP_TAIL_DIAG & 1) ? (uint32_t)i : ~0u;
+		const bool st = act && !abort6 && !(XDP_TAIL_DIAG & 1);
+		uint32_t *ix = stage_idx(meta);
+		ix[nst * kWave + lane] = st ? (uint32_t)i : ~0u;
+		if constexpr (kRecReload) {
+			ix[(kRecStage + nst) * kWave + lane] = (~sum4 & 0xffff) | (l4 << 16);
+			const uint64_t okm = __ballot(st && l4_ok), abm = __ballot(st && absent);
+			uint64_t *mk = reinterpret_cast<uint64_t *>(ix + 2 * kRecStage * kWave);
+			if (lane == 0) {
+				mk[2 * nst] = okm;
+				mk[2 * nst + 1] = abm;
+			}
+		}
 		nst = __builtin_amdgcn_readfirstlane(nst + 1);
 		if (nst == kRecStage) {
 			__builtin_amdgcn_wave_barrier();
+			if constexpr (kRecReload) {
+				/* groups of kRecGroup reloads in flight */
 #pragma unroll
-			for (uint32_t s = 0; s < kRecStage; s++) {
-				const uint32_t j = idx[s * kWave + lane];
-				const uint4 r = meta[320 + s * kWave + lane];
-				if (j != ~0u)
-					st_nt16(a.res + j, r);
+				for (uint32_t s = 0; s + kRecGroup <= kRecStage; s += kRecGroup)
+					rec_flush_reload<kRecGroup>(a, meta, s, lane);
+				if constexpr (kRecStage % kRecGroup)
+					rec_flush_reload<kRecStage % kRecGroup>(
+						a, meta, kRecStage - kRecStage % kRecGroup, lane);
+			} else {
+#pragma unroll
+				for (uint32_t s = 0; s < kRecStage; s++)
+					rec_store_staged(a, meta, s, lane);
 			}
 			nst = 0;
 		}
@@ -2791,8 +2874,7 @@ __device__ __forceinline__ void rx_tail(const RxArgs &a, const FastWave &w,
 		STAMP_ADD(rb * nw + wid, lane, 6);
 	}
 	if constexpr (kRecStage > 0)
-		rec_flush(a, meta + 320,
-			  reinterpret_cast<const uint32_t *>(meta + 320 + kRecStage * kWave), nst, lane);
+		rec_flush(a, meta, nst, lane);
 }
 
 /*
